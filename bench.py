@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident rx parse + checksum + flow-classify throughput.
+
+Metric (BASELINE.json): Mpps + GB/s, device-resident, 64 B & 1500 B frames.
+A "step" = one pass of the hot path (rxg_classify_dev: the fused gfx950
+kernel) over one burst of synthetic frames already resident in HBM, plus at
+N > 1 the per-flow count all-reduce (the path's only exchange).
+Default workload = BASELINE configs[1] (64 B UDP, 1024 flows, 16M frames per
+GPU); configs[2] (1500 B TCP, 4096 flows, 4M frames per GPU, the HBM-roofline
+run) is measured in the same run and reported under "cfg3".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2,cfg3]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "dpdk-tcp-udp_protocol_stack_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rxdist  # noqa: E402
+import rxgpu as R  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------
+def run_workload(name, ctx, rank, world, steps, warmup, dev):
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name, rank, world)
+    n = w["n"]
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    nflows = len(udp) + len(tcb)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(n, dtype=torch.int32, device=dev)
+    ln = torch.empty(n, dtype=torch.int16, device=dev)
+    out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    counts = torch.zeros(max(nflows, 1), dtype=torch.int64, device=dev)
+    step_counts = torch.zeros_like(counts)
+    R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
+    torch.cuda.synchronize(dev)
+    frame_bytes = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item())
+    alg_bytes = frame_bytes + 22 * n  # frame + off(4) + len(2) read + verdict(16) written
+
+    def step(ev=None):
+        tgt = counts if world == 1 else step_counts
+        if world > 1:
+            step_counts.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, tgt, stream=sh)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            rxdist.allreduce_counts(step_counts, world)
+            counts.add_(step_counts)
+
+    for _ in range(warmup):
+        step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for a, b in evs]
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    # self-consistency of the burst (parity proper lives in tests/): every
+    # delivered verdict was counted exactly once per step on this rank
+    v = out.view(n, 16)
+    rc = v[:, 11].view(torch.int8)
+    n_ok = int((rc == 0).sum().item())
+    total_steps = warmup + steps
+    counted = int(counts.sum().item())
+    expect = n_ok * total_steps if world == 1 else None
+    kavg = float(np.mean(kms))
+    res = dict(
+        workload=name, desc=w["desc"], n_per_gpu=n, nflows=nflows,
+        mpps=n * world * steps / el / 1e6,
+        gbps=alg_bytes * world * steps / el / 1e9,
+        ms_per_step=el / steps * 1e3,
+        kernel_ms_avg=kavg, kernel_ms_min=float(np.min(kms)),
+        alg_bytes_per_launch=alg_bytes, frame_bytes=frame_bytes,
+        rc0_frac=n_ok / n, counts_ok=(expect is None or counted == expect),
+    )
+    achieved = alg_bytes / (kavg * 1e-3) / 1e9
+    res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
+                           unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                           traffic=pmc_traffic(name))
+    del pk, off, ln, out
+    torch.cuda.empty_cache()
+    return res
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch from the newest committed PMC summary for this
+    workload (profiles/pmc_*.json, written by tools/pmc_traffic.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if name in d.get("workloads", {}):
+            return d["workloads"][name].get("hbm_bytes_per_launch")
+    return None
+
+
+# ---------------------------------------------------------------------------
+def cpu_baseline(name, budget_s):
+    """The oracle (C restatement of the reference path, linked-list lookups,
+    -O2, one core — the reference runs one pkt_process lcore) on a bounded
+    sample of the same workload, cycled until ~budget_s of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as O  # cpu_baseline leg only
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name)
+    sample = {"cfg2": 1 << 20, "cfg3": 1 << 16, "cfg4": 1 << 16, "cfg5": 1 << 12}[name]
+    pk, off, ln = R.gen_host(cfg, 0, sample, w["unit_log2"])
+    udp, tcb = R.gen_flows(cfg)
+    tb = O.Tables(udp, tcb)
+    # calibrate on a slice, then size the run to the budget
+    t0 = time.perf_counter()
+    k = min(sample, 4096)
+    tb.classify(pk, off[:k], ln[:k], w["unit_log2"])
+    per = (time.perf_counter() - t0) / k
+    total = max(k, int(budget_s / max(per, 1e-9)))
+    done, t0 = 0, time.perf_counter()
+    while done < total:
+        m = min(sample, total - done)
+        tb.classify(pk, off[:m], ln[:m], w["unit_log2"])
+        done += m
+    el = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(value=round(done / el / 1e6, 4), unit="Mpps", cores=1, kind="port",
+                sample=f"{done} frames ({sample} distinct, cycled) of {name}: {w['desc']}; "
+                       f"oracle/ref_cpu.c -O2, list-scan lookups, 1 thread; host {cpu}, "
+                       f"nproc {os.cpu_count()}",
+                seconds=round(el, 2))
+
+
+# ---------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg2,cfg3")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    ctx = R.Context(local)
+    names = [s.strip() for s in a.workload.split(",") if s.strip()]
+    results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}
+    head = results[names[0]]
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(names[0], a.cpu_budget)
+        for nm in names[1:]:
+            results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget / 2)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
+            "value": round(head["mpps"], 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(head["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic counter-based pktgen, generated in HBM)",
+            "config": {"workload": f"{names[0]}: {head['desc']}", "frames_per_gpu": head["n_per_gpu"],
+                       "flows": head["nflows"], "parallelism": f"rss-shard x{world}"},
+            "gb_per_s": round(head["gbps"], 2),
+            "roofline": head["roofline"],
+            "cpu_baseline": cpu,
+            "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
+            "counts_ok": head["counts_ok"],
+        }
+        for nm in names[1:]:
+            r = results[nm]
+            line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

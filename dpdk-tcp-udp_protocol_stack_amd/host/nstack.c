@@ -1,0 +1,751 @@
+/*
+ * nstack.c — socket layer of the stack (host C) over librxgpu.
+ *
+ * Control blocks, lists and socket calls follow the reference
+ * (common.c:262-666, udp.h:10-44, tcp.h:29-84); the receive path is a GPU
+ * burst (rxg_process_mbufs) followed by UDP delivery with the reference's
+ * offload semantics (udp.c:25-52).  See include/nstack.h for the deliberate
+ * differences.
+ */
+#define _GNU_SOURCE
+#include "../../include/nstack.h"
+
+#include <errno.h>
+#include <netinet/in.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define D_DEFAULT_FD_NUM 3   /* common.h:33 */
+#define D_MAX_FD_COUNT 1024  /* common.h:34 */
+#define D_RING_SIZE 1024     /* common.h:29 */
+#define D_TCP_INITIAL_WINDOW 14600
+
+enum {
+    TCP_STATUS_CLOSED = 0,
+    TCP_STATUS_LISTEN,
+    TCP_STATUS_SYN_RCVD,
+    TCP_STATUS_SYN_SENT,
+    TCP_STATUS_ESTABLISHED,
+    TCP_STATUS_FIN_WAIT_1,
+    TCP_STATUS_FIN_WAIT_2,
+    TCP_STATUS_CLOSING,
+    TCP_STATUS_TIME_WAIT,
+    TCP_STATUS_CLOSE_WAIT,
+    TCP_STATUS_LAST_ACK
+}; /* tcp.h:10-26 */
+
+/* ---- rings (stand-in for rte_ring; guarded by the owner's mutex) -------- */
+struct nring {
+    void **slot;
+    uint32_t cap, head, count;
+};
+
+static struct nring *ring_create(uint32_t cap) {
+    struct nring *r = calloc(1, sizeof(*r));
+    if (!r) return NULL;
+    r->slot = calloc(cap, sizeof(void *));
+    if (!r->slot) {
+        free(r);
+        return NULL;
+    }
+    r->cap = cap;
+    return r;
+}
+static void ring_free(struct nring *r) {
+    if (r) free(r->slot);
+    free(r);
+}
+static int ring_enqueue(struct nring *r, void *p) {
+    if (r->count == r->cap) return -ENOBUFS;
+    r->slot[(r->head + r->count) % r->cap] = p;
+    r->count++;
+    return 0;
+}
+static int ring_dequeue(struct nring *r, void **p) {
+    if (!r->count) return -ENOENT;
+    *p = r->slot[r->head];
+    r->head = (r->head + 1) % r->cap;
+    r->count--;
+    return 0;
+}
+
+/* ---- control blocks (udp.h:10-44, tcp.h:29-84) ------------------------- */
+struct localhost {
+    int fd;
+    uint32_t localip;
+    unsigned char localmac[6];
+    uint16_t localport;
+    unsigned char protocol;
+    struct nring *sndbuf, *rcvbuf;
+    struct localhost *prev, *next;
+    pthread_cond_t cond;
+    pthread_mutex_t mutex;
+};
+
+struct offload {
+    uint32_t sip, dip;
+    uint16_t sport, dport;
+    int protocol;
+    unsigned char *data;
+    uint16_t length;
+};
+
+struct tcp_stream {
+    int fd;
+    uint32_t dip;
+    uint8_t localmac[6];
+    uint16_t dport;
+    uint8_t protocol;
+    uint16_t sport;
+    uint32_t sip;
+    uint32_t snd_nxt, rcv_nxt;
+    int status;
+    struct nring *sndbuf, *rcvbuf;
+    struct tcp_stream *prev, *next;
+    pthread_cond_t cond;
+    pthread_mutex_t mutex;
+    pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
+};
+
+struct tcp_fragment {
+    uint16_t sport, dport;
+    uint32_t seqnum, acknum;
+    uint8_t hdrlen_off, tcp_flags;
+    uint16_t windows, cksum, tcp_urp;
+    int optlen;
+    uint32_t option[10];
+    unsigned char *data;
+    uint32_t length;
+};
+
+#define LL_ADD(item, list)                                                                         \
+    do {                                                                                           \
+        (item)->prev = NULL;                                                                       \
+        (item)->next = (list);                                                                     \
+        if ((list) != NULL) (list)->prev = (item);                                                 \
+        (list) = (item);                                                                           \
+    } while (0)
+
+#define LL_REMOVE(item, list)                                                                      \
+    do {                                                                                           \
+        if ((item)->prev != NULL) (item)->prev->next = (item)->next;                               \
+        if ((item)->next != NULL) (item)->next->prev = (item)->prev;                               \
+        if ((list) == (item)) (list) = (item)->next;                                               \
+        (item)->prev = (item)->next = NULL;                                                        \
+    } while (0)
+
+/* ---- process-wide state (netfamily.c:16-18) ----------------------------- */
+static struct localhost *g_pstHost;
+static struct tcp_stream *g_tcb_set;
+static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
+static rxg_ctx *g_ctx;
+static int g_dirty = 1;
+static uint64_t g_stat[4];
+
+/* snapshot: creation-order arrays given to rxg_flows_sync, and the blocks
+ * their flow ids name */
+static rxg_udp_sock *s_udp;
+static struct localhost **s_udp_cb;
+static uint32_t s_nu, s_udp_cap;
+static rxg_tcb *s_tcb;
+static struct tcp_stream **s_tcb_cb;
+static uint32_t s_nt, s_tcb_cap;
+static rxg_verdict *s_v;
+static uint32_t s_v_cap;
+
+static int get_fd_frombitmap(void) { /* common.c:72-85 */
+    for (int fd = D_DEFAULT_FD_NUM; fd < D_MAX_FD_COUNT; fd++)
+        if ((g_ucFdTable[fd / 8] & (0x1 << (fd % 8))) == 0) {
+            g_ucFdTable[fd / 8] |= (0x1 << (fd % 8));
+            return fd;
+        }
+    return -1;
+}
+
+static int set_fd_frombitmap(int fd) { /* common.c:87-95 */
+    if (fd < 0 || fd >= D_MAX_FD_COUNT) return -1;
+    g_ucFdTable[fd / 8] &= ~(0x1 << (fd % 8));
+    return 0;
+}
+
+/* common.c:111-143 (loop advances correctly here) */
+static void *get_hostinfo_fromfd(int fd) {
+    for (struct localhost *h = g_pstHost; h; h = h->next)
+        if (h->fd == fd) return h;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
+        if (s->fd == fd) return s;
+    return NULL;
+}
+
+/* common.c:58-70 */
+static struct tcp_stream *get_accept_tcb(uint16_t dport) {
+    for (struct tcp_stream *apt = g_tcb_set; apt; apt = apt->next)
+        if (dport == apt->dport && apt->fd == -1) return apt;
+    return NULL;
+}
+
+static int grow(void **p, uint32_t *cap, uint32_t need, size_t elem) {
+    if (*cap >= need && *p) return 0;
+    uint32_t c = *cap ? *cap : 64;
+    while (c < need) c *= 2;
+    void *q = realloc(*p, (size_t)c * elem);
+    if (!q) return -1;
+    *p = q;
+    *cap = c;
+    return 0;
+}
+
+/* rebuild the creation-order snapshot (g_lock held) */
+static int snapshot(void) {
+    uint32_t nu = 0, nt = 0;
+    struct localhost *h, *hlast = NULL;
+    struct tcp_stream *s, *slast = NULL;
+    for (h = g_pstHost; h; h = h->next) nu++, hlast = h;
+    for (s = g_tcb_set; s; s = s->next) nt++, slast = s;
+    uint32_t cu = s_udp_cap, ct = s_tcb_cap;
+    if (grow((void **)&s_udp, &s_udp_cap, nu, sizeof(rxg_udp_sock))) return RXG_ENOMEM;
+    if (grow((void **)&s_udp_cb, &cu, nu, sizeof(void *))) return RXG_ENOMEM;
+    if (grow((void **)&s_tcb, &s_tcb_cap, nt, sizeof(rxg_tcb))) return RXG_ENOMEM;
+    if (grow((void **)&s_tcb_cb, &ct, nt, sizeof(void *))) return RXG_ENOMEM;
+    uint32_t i = 0;
+    for (h = hlast; h; h = h->prev, i++) { /* tail = oldest */
+        s_udp[i].localip = h->localip;
+        s_udp[i].localport = h->localport;
+        s_udp[i].protocol = h->protocol;
+        s_udp[i]._pad = 0;
+        s_udp_cb[i] = h;
+    }
+    i = 0;
+    for (s = slast; s; s = s->prev, i++) {
+        s_tcb[i].sip = s->sip;
+        s_tcb[i].dip = s->dip;
+        s_tcb[i].sport = s->sport;
+        s_tcb[i].dport = s->dport;
+        s_tcb[i].status = (uint32_t)s->status;
+        s_tcb_cb[i] = s;
+    }
+    s_nu = nu;
+    s_nt = nt;
+    int rc = rxg_flows_sync(g_ctx, s_udp, nu, s_tcb, nt);
+    if (rc == RXG_OK) g_dirty = 0;
+    return rc;
+}
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
+    pthread_mutex_lock(&g_lock);
+    int rc = RXG_OK;
+    if (!g_ctx) rc = rxg_open(&g_ctx, device, max_burst, max_bytes);
+    g_dirty = 1;
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+void nstack_fini(void) {
+    pthread_mutex_lock(&g_lock);
+    while (g_pstHost) {
+        struct localhost *h = g_pstHost;
+        LL_REMOVE(h, g_pstHost);
+        void *p;
+        while (ring_dequeue(h->rcvbuf, &p) == 0) {
+            free(((struct offload *)p)->data);
+            free(p);
+        }
+        while (ring_dequeue(h->sndbuf, &p) == 0) {
+            free(((struct offload *)p)->data);
+            free(p);
+        }
+        ring_free(h->rcvbuf);
+        ring_free(h->sndbuf);
+        free(h);
+    }
+    while (g_tcb_set) {
+        struct tcp_stream *s = g_tcb_set;
+        LL_REMOVE(s, g_tcb_set);
+        void *p;
+        while (ring_dequeue(s->rcvbuf, &p) == 0) {
+            free(((struct tcp_fragment *)p)->data);
+            free(p);
+        }
+        while (ring_dequeue(s->sndbuf, &p) == 0) {
+            free(((struct tcp_fragment *)p)->data);
+            free(p);
+        }
+        ring_free(s->rcvbuf);
+        ring_free(s->sndbuf);
+        free(s);
+    }
+    memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
+    free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v);
+    s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL;
+    s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = 0;
+    memset(g_stat, 0, sizeof(g_stat));
+    if (g_ctx) rxg_close(g_ctx);
+    g_ctx = NULL;
+    g_dirty = 1;
+    pthread_mutex_unlock(&g_lock);
+}
+
+/* ---- socket API (common.c:262-666) --------------------------------------- */
+int nsocket(int domain, int type, int protocol) {
+    (void)domain, (void)protocol;
+    pthread_mutex_lock(&g_lock);
+    int fd = get_fd_frombitmap();
+    if (fd < 0) {
+        pthread_mutex_unlock(&g_lock);
+        return -1;
+    }
+    if (type == SOCK_DGRAM) { /* :270-303 */
+        struct localhost *h = calloc(1, sizeof(*h));
+        if (!h) goto fail;
+        h->fd = fd;
+        h->protocol = IPPROTO_UDP;
+        h->rcvbuf = ring_create(D_RING_SIZE);
+        h->sndbuf = ring_create(D_RING_SIZE);
+        if (!h->rcvbuf || !h->sndbuf) {
+            ring_free(h->rcvbuf);
+            ring_free(h->sndbuf);
+            free(h);
+            goto fail;
+        }
+        pthread_cond_init(&h->cond, NULL);
+        pthread_mutex_init(&h->mutex, NULL);
+        LL_ADD(h, g_pstHost);
+    } else if (type == SOCK_STREAM) { /* :304-337 */
+        struct tcp_stream *s = calloc(1, sizeof(*s));
+        if (!s) goto fail;
+        s->fd = fd;
+        s->protocol = IPPROTO_TCP;
+        s->rcvbuf = ring_create(D_RING_SIZE);
+        s->sndbuf = ring_create(D_RING_SIZE);
+        if (!s->rcvbuf || !s->sndbuf) {
+            ring_free(s->rcvbuf);
+            ring_free(s->sndbuf);
+            free(s);
+            goto fail;
+        }
+        pthread_cond_init(&s->cond, NULL);
+        pthread_cond_init(&s->accept_cond, NULL);
+        pthread_mutex_init(&s->mutex, NULL);
+        LL_ADD(s, g_tcb_set);
+    }
+    g_dirty = 1;
+    pthread_mutex_unlock(&g_lock);
+    return fd;
+fail:
+    set_fd_frombitmap(fd);
+    pthread_mutex_unlock(&g_lock);
+    return -1;
+}
+
+int nbind(int sockfd, const struct sockaddr *addr, socklen_t addrlen) { /* :342-371 */
+    (void)addrlen;
+    if (!addr) return -1;
+    const struct sockaddr_in *a = (const struct sockaddr_in *)addr;
+    pthread_mutex_lock(&g_lock);
+    void *info = get_hostinfo_fromfd(sockfd);
+    int rc = -1;
+    if (info) {
+        struct localhost *h = info;
+        if (h->protocol == IPPROTO_UDP) {
+            h->localport = a->sin_port;
+            memcpy(&h->localip, &a->sin_addr.s_addr, 4);
+        } else {
+            struct tcp_stream *s = info;
+            s->dport = a->sin_port;
+            memcpy(&s->dip, &a->sin_addr.s_addr, 4);
+            s->status = TCP_STATUS_CLOSED;
+        }
+        g_dirty = 1;
+        rc = 0;
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+int nlisten(int sockfd, int backlog) { /* :373-386 */
+    (void)backlog;
+    pthread_mutex_lock(&g_lock);
+    struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
+    int rc = -1;
+    if (s) {
+        if (s->protocol == IPPROTO_TCP) s->status = TCP_STATUS_LISTEN;
+        g_dirty = 1;
+        rc = 0;
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+int naccept(int sockfd, struct sockaddr *addr, socklen_t *addrlen) { /* :388-416 */
+    (void)addrlen;
+    pthread_mutex_lock(&g_lock);
+    struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
+    if (!s || s->protocol != IPPROTO_TCP) {
+        pthread_mutex_unlock(&g_lock);
+        return -1;
+    }
+    struct tcp_stream *apt;
+    while ((apt = get_accept_tcb(s->dport)) == NULL) {
+        /* wait on the listener's cond; g_lock doubles as its mutex here so a
+         * tcb added between the check and the wait cannot be missed */
+        pthread_cond_wait(&s->accept_cond, &g_lock);
+    }
+    apt->fd = get_fd_frombitmap();
+    if (addr) {
+        struct sockaddr_in *sa = (struct sockaddr_in *)addr;
+        sa->sin_family = AF_INET;
+        sa->sin_port = apt->sport;
+        memcpy(&sa->sin_addr.s_addr, &apt->sip, 4);
+    }
+    int fd = apt->fd;
+    pthread_mutex_unlock(&g_lock);
+    return fd;
+}
+
+ssize_t nsend(int sockfd, const void *buf, size_t len, int flags) { /* :418-460 */
+    (void)flags;
+    pthread_mutex_lock(&g_lock);
+    struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
+    ssize_t n = -1;
+    if (s) {
+        n = 0;
+        if (s->protocol == IPPROTO_TCP) {
+            struct tcp_fragment *f = calloc(1, sizeof(*f));
+            if (!f) {
+                n = -2;
+            } else if (!(f->data = calloc(1, len + 1))) {
+                free(f);
+                n = -1;
+            } else {
+                f->dport = s->sport;
+                f->sport = s->dport;
+                f->acknum = s->rcv_nxt;
+                f->seqnum = s->snd_nxt;
+                f->tcp_flags = 0x10 | 0x08; /* ACK | PSH */
+                f->windows = D_TCP_INITIAL_WINDOW;
+                f->hdrlen_off = 0x50;
+                memcpy(f->data, buf, len);
+                f->length = (uint32_t)len;
+                pthread_mutex_lock(&s->mutex);
+                if (ring_enqueue(s->sndbuf, f)) {
+                    free(f->data);
+                    free(f);
+                    n = -1;
+                } else {
+                    n = (ssize_t)len;
+                }
+                pthread_mutex_unlock(&s->mutex);
+            }
+        }
+    }
+    pthread_mutex_unlock(&g_lock);
+    return n;
+}
+
+ssize_t nrecv(int sockfd, void *buf, size_t len, int flags) { /* :462-515 */
+    pthread_mutex_lock(&g_lock);
+    struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
+    pthread_mutex_unlock(&g_lock);
+    if (!s) return -1;
+    if (s->protocol != IPPROTO_TCP) return 0;
+    struct tcp_fragment *f = NULL;
+    pthread_mutex_lock(&s->mutex);
+    while (ring_dequeue(s->rcvbuf, (void **)&f) < 0) {
+        if (flags & MSG_DONTWAIT) {
+            pthread_mutex_unlock(&s->mutex);
+            errno = EAGAIN;
+            return -1;
+        }
+        pthread_cond_wait(&s->cond, &s->mutex);
+    }
+    ssize_t length;
+    if (f->length > len) { /* :483-496: split, re-enqueue the rest */
+        memcpy(buf, f->data, len);
+        memmove(f->data, f->data + len, f->length - len);
+        f->length -= (uint32_t)len;
+        length = f->length; /* the reference returns the REMAINING length here */
+        ring_enqueue(s->rcvbuf, f);
+    } else if (f->length == 0) { /* :497-501: 0-length fragment = EOF */
+        free(f->data);
+        free(f);
+        length = 0;
+    } else {
+        memcpy(buf, f->data, f->length);
+        length = f->length;
+        free(f->data);
+        free(f);
+    }
+    pthread_mutex_unlock(&s->mutex);
+    return length;
+}
+
+ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr *src_addr,
+                  socklen_t *addrlen) { /* :517-565 */
+    (void)addrlen;
+    pthread_mutex_lock(&g_lock);
+    struct localhost *h = get_hostinfo_fromfd(sockfd);
+    pthread_mutex_unlock(&g_lock);
+    if (!h) return -1;
+    struct offload *o = NULL;
+    pthread_mutex_lock(&h->mutex);
+    while (ring_dequeue(h->rcvbuf, (void **)&o) < 0) {
+        if (flags & MSG_DONTWAIT) {
+            pthread_mutex_unlock(&h->mutex);
+            errno = EAGAIN;
+            return -1;
+        }
+        pthread_cond_wait(&h->cond, &h->mutex);
+    }
+    if (src_addr) {
+        struct sockaddr_in *a = (struct sockaddr_in *)src_addr;
+        a->sin_family = AF_INET;
+        a->sin_port = o->sport;
+        memcpy(&a->sin_addr.s_addr, &o->sip, 4);
+    }
+    if (len < o->length) { /* :542-556: copy len, keep the rest queued */
+        memcpy(buf, o->data, len);
+        memmove(o->data, o->data + len, o->length - len);
+        o->length = (uint16_t)(o->length - len);
+        ring_enqueue(h->rcvbuf, o);
+        pthread_mutex_unlock(&h->mutex);
+        return (ssize_t)len;
+    }
+    pthread_mutex_unlock(&h->mutex);
+    ssize_t n = o->length; /* :558-564 */
+    memcpy(buf, o->data, o->length);
+    free(o->data);
+    free(o);
+    return n;
+}
+
+ssize_t nsendto(int sockfd, const void *buf, size_t len, int flags,
+                const struct sockaddr *dest_addr, socklen_t addrlen) { /* :567-607 */
+    (void)flags, (void)addrlen;
+    const struct sockaddr_in *a = (const struct sockaddr_in *)dest_addr;
+    pthread_mutex_lock(&g_lock);
+    struct localhost *h = get_hostinfo_fromfd(sockfd);
+    pthread_mutex_unlock(&g_lock);
+    if (!h || !a) return -1;
+    struct offload *o = calloc(1, sizeof(*o));
+    if (!o) return -1;
+    o->dip = a->sin_addr.s_addr;
+    o->dport = a->sin_port;
+    o->sip = h->localip;
+    o->sport = h->localport;
+    o->length = (uint16_t)len;
+    o->data = malloc(len ? len : 1);
+    if (!o->data) {
+        free(o);
+        return -1;
+    }
+    memcpy(o->data, buf, len);
+    pthread_mutex_lock(&h->mutex);
+    int e = ring_enqueue(h->sndbuf, o);
+    pthread_mutex_unlock(&h->mutex);
+    if (e) {
+        free(o->data);
+        free(o);
+        return -1;
+    }
+    return (ssize_t)len;
+}
+
+int nclose(int fd) { /* :609-666 */
+    pthread_mutex_lock(&g_lock);
+    void *info = get_hostinfo_fromfd(fd);
+    if (!info) {
+        pthread_mutex_unlock(&g_lock);
+        return -1;
+    }
+    struct localhost *h = info;
+    if (h->protocol == IPPROTO_UDP) {
+        LL_REMOVE(h, g_pstHost);
+        void *p;
+        while (ring_dequeue(h->rcvbuf, &p) == 0) {
+            free(((struct offload *)p)->data);
+            free(p);
+        }
+        while (ring_dequeue(h->sndbuf, &p) == 0) {
+            free(((struct offload *)p)->data);
+            free(p);
+        }
+        ring_free(h->rcvbuf);
+        ring_free(h->sndbuf);
+        free(h);
+        set_fd_frombitmap(fd);
+    } else {
+        struct tcp_stream *s = info;
+        if (s->status != TCP_STATUS_LISTEN) { /* queue FIN, wait for LAST_ACK */
+            struct tcp_fragment *f = calloc(1, sizeof(*f));
+            if (f) {
+                f->sport = s->dport;
+                f->dport = s->sport;
+                f->seqnum = s->snd_nxt;
+                f->acknum = s->rcv_nxt;
+                f->tcp_flags = 0x01 | 0x10; /* FIN | ACK */
+                f->windows = D_TCP_INITIAL_WINDOW;
+                f->hdrlen_off = 0x50;
+                pthread_mutex_lock(&s->mutex);
+                if (ring_enqueue(s->sndbuf, f)) free(f);
+                pthread_mutex_unlock(&s->mutex);
+            }
+            s->status = TCP_STATUS_LAST_ACK;
+            set_fd_frombitmap(fd);
+        } else {
+            LL_REMOVE(s, g_tcb_set);
+            ring_free(s->rcvbuf);
+            ring_free(s->sndbuf);
+            free(s);
+            /* the reference leaves the listener's fd set in the bitmap here */
+        }
+    }
+    g_dirty = 1;
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+/* ---- receive path --------------------------------------------------------- */
+static inline uint32_t rd32(const uint8_t *p) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+static inline uint16_t rd16(const uint8_t *p) {
+    uint16_t v;
+    memcpy(&v, p, 2);
+    return v;
+}
+
+/* udp.c:25-52 for one verdict (g_lock held) */
+static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v) {
+    if (v->cls == RXG_CLS_TCP) {
+        if (v->rc == RXG_RC_OK) g_stat[2]++;
+        return 0;
+    }
+    if (v->cls != RXG_CLS_UDP) {
+        g_stat[3]++;
+        return 0;
+    }
+    if (v->rc != RXG_RC_OK || v->flow_id >= s_nu) return 0;
+    struct localhost *h = s_udp_cb[v->flow_id];
+    const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
+    const uint32_t cap = m->data_len;
+    struct offload *o = calloc(1, sizeof(*o));
+    if (!o) return 0;
+    o->sip = cap >= 30 ? rd32(f + 26) : 0;
+    o->dip = cap >= 34 ? rd32(f + 30) : 0;
+    o->sport = cap >= 36 ? rd16(f + 34) : 0;
+    o->dport = cap >= 38 ? rd16(f + 36) : 0;
+    o->protocol = IPPROTO_UDP;
+    o->length = (uint16_t)(v->payload_len + 8); /* = dgram_len (udp.c:37) */
+    o->data = calloc(1, o->length);             /* payload + 8 zero bytes (see nstack.h) */
+    if (!o->data) {
+        free(o);
+        return 0;
+    }
+    uint32_t avail = cap > v->payload_off ? cap - v->payload_off : 0;
+    uint32_t ncopy = v->payload_len < avail ? v->payload_len : avail;
+    memcpy(o->data, f + v->payload_off, ncopy); /* udp.c:46 */
+    pthread_mutex_lock(&h->mutex);
+    int e = ring_enqueue(h->rcvbuf, o); /* udp.c:48 */
+    if (!e) pthread_cond_signal(&h->cond); /* udp.c:50-52 */
+    pthread_mutex_unlock(&h->mutex);
+    if (e) {
+        free(o->data);
+        free(o);
+        g_stat[1]++;
+        return 0;
+    }
+    g_stat[0]++;
+    return 1;
+}
+
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v) {
+    if (!m || !v) return n ? RXG_EINVAL : 0;
+    pthread_mutex_lock(&g_lock);
+    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    if (rc == RXG_OK && g_dirty) rc = snapshot();
+    int delivered = 0;
+    if (rc == RXG_OK)
+        for (uint32_t i = 0; i < n; i++) delivered += deliver_one(m[i], &v[i]);
+    pthread_mutex_unlock(&g_lock);
+    return rc == RXG_OK ? delivered : rc;
+}
+
+int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
+    if (!m && n) return RXG_EINVAL;
+    pthread_mutex_lock(&g_lock);
+    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    if (rc == RXG_OK && g_dirty) rc = snapshot();
+    if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
+        rc = RXG_ENOMEM;
+    if (rc == RXG_OK) rc = rxg_process_mbufs(g_ctx, m, n, s_v);
+    int delivered = 0;
+    if (rc == RXG_OK) {
+        for (uint32_t i = 0; i < n; i++) {
+            delivered += deliver_one(m[i], &s_v[i]);
+            if (rc_out) rc_out[i] = s_v[i].rc;
+        }
+        if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc == RXG_OK ? delivered : rc;
+}
+
+int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status) {
+    struct tcp_stream *s = calloc(1, sizeof(*s)); /* tcp_stream_create, tcp.c:3-41 */
+    if (!s) return -1;
+    s->sip = sip;
+    s->dip = dip;
+    s->sport = sport;
+    s->dport = dport;
+    s->protocol = IPPROTO_TCP;
+    s->fd = -1;
+    s->status = status;
+    s->rcvbuf = ring_create(D_RING_SIZE);
+    s->sndbuf = ring_create(D_RING_SIZE);
+    if (!s->rcvbuf || !s->sndbuf) {
+        ring_free(s->rcvbuf);
+        ring_free(s->sndbuf);
+        free(s);
+        return -1;
+    }
+    pthread_cond_init(&s->cond, NULL);
+    pthread_cond_init(&s->accept_cond, NULL);
+    pthread_mutex_init(&s->mutex, NULL);
+    pthread_mutex_lock(&g_lock);
+    LL_ADD(s, g_tcb_set); /* tcp.c:52 */
+    g_dirty = 1;
+    /* wake naccept waiters on a listener of this port (tcp.c:108-116) */
+    for (struct tcp_stream *l = g_tcb_set; l; l = l->next)
+        if (l->dport == dport && l->status == TCP_STATUS_LISTEN)
+            pthread_cond_broadcast(&l->accept_cond);
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
+                 uint32_t *nt) {
+    pthread_mutex_lock(&g_lock);
+    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    if (rc == RXG_OK && g_dirty) rc = snapshot();
+    if (rc == RXG_OK) {
+        if (nu) *nu = s_nu;
+        if (nt) *nt = s_nt;
+        if (u) memcpy(u, s_udp, (size_t)(s_nu < cap_u ? s_nu : cap_u) * sizeof(*u));
+        if (t) memcpy(t, s_tcb, (size_t)(s_nt < cap_t ? s_nt : cap_t) * sizeof(*t));
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+uint64_t nstack_stat(int which) {
+    if (which < 0 || which > 3) return 0;
+    pthread_mutex_lock(&g_lock);
+    uint64_t v = g_stat[which];
+    pthread_mutex_unlock(&g_lock);
+    return v;
+}

@@ -1,0 +1,380 @@
+"""ctypes binding of librxgpu.so (include/rxgpu.h) and libnstack.so (include/nstack.h).
+
+This module is plumbing for tests and bench.py: every verdict it returns is
+computed by the gfx950 kernel in librxgpu.so.  There is no Python or CPU
+fallback — if the shared library is missing, importing this module raises.
+
+Reference interface mirrored (see include/rxgpu.h for file:line citations):
+  pkt_process loop body (netfamily.c:152-200) -> Context.classify* / process_mbufs
+  udp_process / tcp_process return codes       -> verdict['rc']
+  get_hostinfo_fromip_port / tcp_stream_search -> verdict['flow_id'], lookup_udp/lookup_tcp
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librxgpu.so")
+NSTACK_PATH = os.path.join(_HERE, "libnstack.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make -C {_HERE}` (or __graft_entry__.build()); "
+        "there is no fallback path")
+_lib = C.CDLL(LIB_PATH)
+
+# ---- constants (mirror include/rxgpu.h) -----------------------------------
+FLOW_NONE = 0xFFFFFFFF
+CLS_ARP, CLS_NON_IP, CLS_IPV4_OTHER, CLS_UDP, CLS_TCP = 0, 1, 2, 3, 4
+RC_OK, RC_TCP_BAD_CKSUM, RC_TCP_NO_TCB, RC_UDP_NOMEM, RC_UDP_NO_SOCKET, RC_KNI = 0, -1, -2, -2, -3, 1
+F_TRUNC, F_TCP_NEGLEN, F_UDP_SHORT = 0x1, 0x2, 0x4
+TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
+HOST_ONLY = -1
+
+VERDICT_DTYPE = np.dtype([
+    ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
+    ("cls", "u1"), ("rc", "i1"), ("cksum_ok", "u1"), ("flags", "u1"), ("stored_cksum", "<u2"),
+])
+assert VERDICT_DTYPE.itemsize == 16
+UDP_SOCK_DTYPE = np.dtype([("localip", "<u4"), ("localport", "<u2"), ("protocol", "u1"),
+                           ("_pad", "u1")])
+TCB_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+                      ("status", "<u4")])
+
+
+class GenCfg(C.Structure):
+    """rxg_gen_cfg"""
+    _fields_ = [
+        ("seed", C.c_uint64), ("size_mode", C.c_uint32), ("frame_len", C.c_uint32),
+        ("slot_bytes", C.c_uint32), ("proto_mode", C.c_uint32), ("n_udp", C.c_uint32),
+        ("n_tcp", C.c_uint32), ("local_ip", C.c_uint32), ("udp_base_port", C.c_uint16),
+        ("tcp_port", C.c_uint16), ("bad_cksum_per10k", C.c_uint32),
+        ("unknown_per10k", C.c_uint32), ("other_per10k", C.c_uint32), ("shard", C.c_uint32),
+        ("n_shards", C.c_uint32),
+    ]
+
+
+class Mbuf(C.Structure):
+    """rxg_mbuf: rte_mbuf-shaped descriptor (buf_addr@0, data_off@16, data_len@40)."""
+    _fields_ = [("buf_addr", C.c_void_p), ("_r0", C.c_uint8 * 8), ("data_off", C.c_uint16),
+                ("_r1", C.c_uint8 * 22), ("data_len", C.c_uint16), ("_r2", C.c_uint8 * 86)]
+
+
+assert C.sizeof(Mbuf) == 128
+
+_vp, _u32, _u64, _i32, _u16 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_uint16
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_open = _sig("rxg_open", _i32, C.POINTER(_vp), _i32, _u32, _u64)
+_close = _sig("rxg_close", None, _vp)
+_strerror = _sig("rxg_strerror", C.c_char_p, _i32)
+_last_hip = _sig("rxg_last_hip_error", C.c_char_p)
+_flows_sync = _sig("rxg_flows_sync", _i32, _vp, _vp, _u32, _vp, _u32)
+_classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
+_classify = _sig("rxg_classify", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp)
+_process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
+_flow_counts = _sig("rxg_flow_counts", _i32, _vp, _vp, _u32)
+_counts_reset = _sig("rxg_counts_reset", _i32, _vp)
+_num_flows = _sig("rxg_num_flows", _u32, _vp)
+_lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
+_lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
+_rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
+_gen_flows = _sig("rxg_gen_flows", _i32, C.POINTER(GenCfg), _vp, _vp)
+_gen_host = _sig("rxg_gen_host", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32)
+_gen_dev = _sig("rxg_gen_dev", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32, _vp)
+
+EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
+            "rxg_classify_dev", "rxg_classify", "rxg_process_mbufs", "rxg_flow_counts",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev"]
+
+
+class RxgError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        msg = _strerror(rc).decode()
+        if rc == -1000:
+            msg += " [" + _last_hip().decode() + "]"
+        super().__init__(f"{what}: {msg} ({rc})")
+        self.rc = rc
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RxgError(rc, what)
+
+
+def _ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to librxgpu must be contiguous"
+    return a.ctypes.data
+
+
+def _tptr(t):
+    """device pointer of a torch tensor (or None)"""
+    return None if t is None else t.data_ptr()
+
+
+# ---- byte-order helpers (raw network-order values as the reference stores them)
+def ip_raw(dotted: str) -> int:
+    b = bytes(int(x) for x in dotted.split("."))
+    return int.from_bytes(b, "little")
+
+
+def port_raw(port: int) -> int:
+    return int.from_bytes(port.to_bytes(2, "big"), "little")
+
+
+class Context:
+    """rxg_ctx: one per rx thread (device = HIP ordinal, or HOST_ONLY)."""
+
+    def __init__(self, device: int = 0, max_pkts: int = 0, max_bytes: int = 0):
+        h = _vp()
+        _check(_open(C.byref(h), device, max_pkts, max_bytes), "rxg_open")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def flows_sync(self, udp: np.ndarray | None = None, tcb: np.ndarray | None = None):
+        udp = np.ascontiguousarray(udp if udp is not None else np.zeros(0, UDP_SOCK_DTYPE),
+                                   UDP_SOCK_DTYPE)
+        tcb = np.ascontiguousarray(tcb if tcb is not None else np.zeros(0, TCB_DTYPE), TCB_DTYPE)
+        _check(_flows_sync(self._h, _ptr(udp) if len(udp) else None, len(udp),
+                           _ptr(tcb) if len(tcb) else None, len(tcb)), "rxg_flows_sync")
+        self.nu, self.nt = len(udp), len(tcb)
+
+    @property
+    def num_flows(self) -> int:
+        return _num_flows(self._h)
+
+    def lookup_udp(self, dip: int, dport: int) -> int:
+        return _lk_udp(self._h, dip, dport)
+
+    def lookup_tcp(self, sip: int, dip: int, sport: int, dport: int) -> int:
+        return _lk_tcp(self._h, sip, dip, sport, dport)
+
+    def classify(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
+                 off_unit_log2: int) -> np.ndarray:
+        """Host buffers in, verdicts out (PCIe-inclusive, synchronous)."""
+        pkts = np.ascontiguousarray(pkts, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        lens = np.ascontiguousarray(lens, np.uint16)
+        out = np.zeros(len(off), VERDICT_DTYPE)
+        _check(_classify(self._h, _ptr(pkts), _ptr(off), _ptr(lens), len(off), off_unit_log2,
+                         _ptr(out)), "rxg_classify")
+        return out
+
+    def classify_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
+                     d_out, d_counts=None, stream=None):
+        """Device tensors in/out (torch tensors or raw ints), asynchronous on `stream`."""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        _check(_classify_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, len_hint,
+                             p(d_out), p(d_counts), stream), "rxg_classify_dev")
+
+    def process_mbufs(self, mbufs) -> np.ndarray:
+        arr = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])
+        out = np.zeros(len(mbufs), VERDICT_DTYPE)
+        _check(_process_mbufs(self._h, C.cast(arr, _vp), len(mbufs), _ptr(out)),
+               "rxg_process_mbufs")
+        return out
+
+    def flow_counts(self) -> np.ndarray:
+        n = self.num_flows
+        out = np.zeros(max(n, 1), np.uint64)
+        _check(_flow_counts(self._h, _ptr(out), n), "rxg_flow_counts")
+        return out[:n]
+
+    def counts_reset(self):
+        _check(_counts_reset(self._h), "rxg_counts_reset")
+
+
+def rss_hash(sip: int, dip: int, sport: int, dport: int) -> int:
+    return _rss(sip, dip, sport, dport)
+
+
+def make_gen_cfg(**kw) -> GenCfg:
+    d = dict(seed=0x5EED0001, size_mode=0, frame_len=64, slot_bytes=64, proto_mode=0, n_udp=1024,
+             n_tcp=0, local_ip=ip_raw("192.168.100.77"), udp_base_port=20000, tcp_port=9999,
+             bad_cksum_per10k=100, unknown_per10k=50, other_per10k=50, shard=0, n_shards=1)
+    d.update(kw)
+    return GenCfg(**d)
+
+
+def gen_flows(cfg: GenCfg):
+    udp = np.zeros(cfg.n_udp, UDP_SOCK_DTYPE)
+    tcb = np.zeros(cfg.n_tcp + 1 if cfg.n_tcp else 0, TCB_DTYPE)
+    _check(_gen_flows(C.byref(cfg), _ptr(udp) if len(udp) else None,
+                      _ptr(tcb) if len(tcb) else None), "rxg_gen_flows")
+    return udp, tcb
+
+
+def gen_host(cfg: GenCfg, first: int, n: int, off_unit_log2: int = 6):
+    pkts = np.zeros(n * cfg.slot_bytes, np.uint8)
+    off = np.zeros(n, np.uint32)
+    lens = np.zeros(n, np.uint16)
+    _check(_gen_host(C.byref(cfg), first, n, _ptr(pkts), _ptr(off), _ptr(lens), off_unit_log2),
+           "rxg_gen_host")
+    return pkts, off, lens
+
+
+def gen_dev(cfg: GenCfg, first: int, n: int, d_pkts, d_off, d_len, off_unit_log2: int = 6,
+            stream=None):
+    _check(_gen_dev(C.byref(cfg), first, n, _tptr(d_pkts), _tptr(d_off), _tptr(d_len),
+                    off_unit_log2, stream), "rxg_gen_dev")
+
+
+# ---- libnstack: the socket layer (include/nstack.h) ------------------------
+AF_INET, SOCK_STREAM, SOCK_DGRAM, MSG_DONTWAIT = 2, 1, 2, 0x40
+
+
+class SockaddrIn(C.Structure):
+    _fields_ = [("sin_family", C.c_uint16), ("sin_port", C.c_uint16), ("sin_addr", C.c_uint32),
+                ("sin_zero", C.c_uint8 * 8)]
+
+
+def sockaddr(ip: str, port: int) -> SockaddrIn:
+    return SockaddrIn(AF_INET, port_raw(port), ip_raw(ip))
+
+
+class NStack:
+    """Process-wide socket layer (one per process, like the reference's globals)."""
+    _lib = None
+
+    def __init__(self, device: int = HOST_ONLY, max_burst: int = 4096, max_bytes: int = 1 << 24):
+        if NStack._lib is None:
+            if not os.path.exists(NSTACK_PATH):
+                raise ImportError(f"{NSTACK_PATH} missing: run make -C {_HERE}")
+            lib = C.CDLL(NSTACK_PATH)
+            ssz = C.c_ssize_t
+            sig = [("nstack_init", _i32, [_i32, _u32, _u64]), ("nstack_fini", None, []),
+                   ("nsocket", _i32, [_i32, _i32, _i32]), ("nbind", _i32, [_i32, _vp, _u32]),
+                   ("nlisten", _i32, [_i32, _i32]), ("naccept", _i32, [_i32, _vp, _vp]),
+                   ("nsend", ssz, [_i32, _vp, C.c_size_t, _i32]),
+                   ("nrecv", ssz, [_i32, _vp, C.c_size_t, _i32]),
+                   ("nrecvfrom", ssz, [_i32, _vp, C.c_size_t, _i32, _vp, _vp]),
+                   ("nsendto", ssz, [_i32, _vp, C.c_size_t, _i32, _vp, _u32]),
+                   ("nclose", _i32, [_i32]),
+                   ("nstack_rx_burst", _i32, [_vp, _u32, _vp, _vp]),
+                   ("nstack_deliver", _i32, [_vp, _u32, _vp]),
+                   ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
+                   ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp]),
+                   ("nstack_stat", _u64, [_i32])]
+            for name, res, args in sig:
+                f = getattr(lib, name)
+                f.restype, f.argtypes = res, args
+            NStack._lib = lib
+        self.lib = NStack._lib
+        _check(self.lib.nstack_init(device, max_burst, max_bytes), "nstack_init")
+
+    def fini(self):
+        self.lib.nstack_fini()
+
+    # socket calls: thin pass-through with the reference's argument meaning
+    def socket(self, type_):
+        return self.lib.nsocket(AF_INET, type_, 0)
+
+    def bind(self, fd, ip, port):
+        a = sockaddr(ip, port)
+        return self.lib.nbind(fd, C.byref(a), C.sizeof(a))
+
+    def listen(self, fd):
+        return self.lib.nlisten(fd, 10)
+
+    def accept(self, fd):
+        a = SockaddrIn()
+        n = C.c_uint32(C.sizeof(a))
+        r = self.lib.naccept(fd, C.byref(a), C.byref(n))
+        return r, a
+
+    def recvfrom(self, fd, n, flags=MSG_DONTWAIT):
+        buf = C.create_string_buffer(max(n, 1))
+        a = SockaddrIn()
+        al = C.c_uint32(C.sizeof(a))
+        r = self.lib.nrecvfrom(fd, buf, n, flags, C.byref(a), C.byref(al))
+        return r, buf.raw[:max(r, 0)], a
+
+    def recv(self, fd, n, flags=MSG_DONTWAIT):
+        buf = C.create_string_buffer(max(n, 1))
+        r = self.lib.nrecv(fd, buf, n, flags)
+        return r, buf.raw[:max(r, 0)]
+
+    def sendto(self, fd, data: bytes, ip, port):
+        a = sockaddr(ip, port)
+        return self.lib.nsendto(fd, data, len(data), 0, C.byref(a), C.sizeof(a))
+
+    def send(self, fd, data: bytes):
+        return self.lib.nsend(fd, data, len(data), 0)
+
+    def close(self, fd):
+        return self.lib.nclose(fd)
+
+    def tcb_add(self, sip, dip, sport, dport, status=TCP_STATUS_ESTABLISHED):
+        return self.lib.nstack_tcb_add(ip_raw(sip), ip_raw(dip), port_raw(sport),
+                                       port_raw(dport), status)
+
+    def flows(self):
+        nu, nt = C.c_uint32(), C.c_uint32()
+        _check(self.lib.nstack_flows(None, 0, C.byref(nu), None, 0, C.byref(nt)), "nstack_flows")
+        u = np.zeros(nu.value, UDP_SOCK_DTYPE)
+        t = np.zeros(nt.value, TCB_DTYPE)
+        _check(self.lib.nstack_flows(_ptr(u) if len(u) else None, len(u), None,
+                                     _ptr(t) if len(t) else None, len(t), None), "nstack_flows")
+        return u, t
+
+    @staticmethod
+    def mbufs(frames: list[bytes]):
+        """rte_mbuf-shaped descriptors over the given frames (kept alive by the return)"""
+        bufs = [C.create_string_buffer(f, len(f) + 16) for f in frames]
+        ms = [Mbuf() for _ in frames]
+        for m, b, f in zip(ms, bufs, frames):
+            m.buf_addr = C.cast(b, C.c_void_p)
+            m.data_off = 0
+            m.data_len = len(f)
+        arr = (C.POINTER(Mbuf) * len(ms))(*[C.pointer(m) for m in ms])
+        return arr, (bufs, ms)
+
+    def deliver(self, frames: list[bytes], verdicts: np.ndarray) -> int:
+        arr, keep = self.mbufs(frames)
+        r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts))
+        if r < 0:
+            _check(r, "nstack_deliver")
+        return r
+
+    def rx_burst(self, frames: list[bytes]):
+        arr, keep = self.mbufs(frames)
+        rcs = np.zeros(len(frames), np.int32)
+        v = np.zeros(len(frames), VERDICT_DTYPE)
+        r = self.lib.nstack_rx_burst(C.cast(arr, _vp), len(frames), _ptr(rcs), _ptr(v))
+        if r < 0:
+            _check(r, "nstack_rx_burst")
+        return r, rcs, v
+
+    def stat(self, which):
+        return self.lib.nstack_stat(which)

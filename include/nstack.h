@@ -1,0 +1,87 @@
+/*
+ * nstack.h — socket-style API of the stack, host C, over librxgpu.
+ *
+ * Same names, signatures and return conventions as the reference's socket
+ * layer (common.h:189-200, bodies common.c:262-666), so an application
+ * written against the reference (netfamily.c:211-383) links unchanged.  The
+ * control blocks are the reference's (struct localhost udp.h:10-29, struct
+ * tcp_stream tcp.h:29-55) in the same head-inserted lists; what changes is
+ * the receive path: instead of per-frame udp_process/tcp_process calls on the
+ * protocol lcore, a burst goes through nstack_rx_burst(), which classifies it
+ * on the GPU (rxg_process_mbufs) and then delivers UDP payloads into the
+ * sockets' receive rings with the reference's `struct offload` semantics
+ * (udp.c:25-52), where nrecvfrom() picks them up.
+ *
+ * Deliberate differences (DESIGN.md §Socket layer):
+ *   - the lists are guarded by a lock (the reference mutates them from the
+ *     app lcore while the protocol lcore walks them, common.c:302,336,620,660);
+ *   - get_hostinfo_fromfd walks the list correctly (common.c:116 advances
+ *     from the list head and never terminates past the second socket);
+ *   - nrecvfrom/nrecv/naccept honour MSG_DONTWAIT in `flags` (the reference
+ *     ignores flags and always blocks); naccept has no flags: it blocks;
+ *   - the 8 bytes nrecvfrom returns past the payload (offload.length =
+ *     dgram_len, udp.c:37, but only dgram_len-8 bytes are stored, udp.c:38) read
+ *     as zeros instead of adjacent heap memory.
+ * TCP segments are classified (verdicts/return codes) but not yet delivered:
+ * the TCP state machine (tcp.c:43-331) is out of this round's scope.
+ */
+#ifndef NSTACK_H
+#define NSTACK_H
+
+#include <stdint.h>
+#include <sys/socket.h>
+#include <sys/types.h>
+
+#include "rxgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Process-wide stack, like the reference's globals (netfamily.c:16-18).
+ * device = HIP ordinal, or RXG_HOST_ONLY for a stack without a GPU (socket
+ * API + nstack_deliver work; nstack_rx_burst returns RXG_ENODEV). */
+int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes);
+void nstack_fini(void);
+
+/* socket API (common.h:189-200) */
+int nsocket(int domain, int type, int protocol);
+int nbind(int sockfd, const struct sockaddr *addr, socklen_t addrlen);
+int nlisten(int sockfd, int backlog);
+int naccept(int sockfd, struct sockaddr *addr, socklen_t *addrlen);
+ssize_t nsend(int sockfd, const void *buf, size_t len, int flags);
+ssize_t nrecv(int sockfd, void *buf, size_t len, int flags);
+ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr *src_addr,
+                  socklen_t *addrlen);
+ssize_t nsendto(int sockfd, const void *buf, size_t len, int flags, const struct sockaddr *dest_addr,
+                socklen_t addrlen);
+int nclose(int fd);
+
+/* Receive burst: the loop body of pkt_process (netfamily.c:152-200) for n
+ * frames at once.  rc_out[i] (nullable) = what udp_process/tcp_process would
+ * have returned (KNI frames: 1); v_out (nullable) = the verdicts.
+ * Returns the number of UDP datagrams delivered, or a negative RXG_E* code. */
+int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
+
+/* Delivery half only: apply verdicts computed by rxg_* for the current
+ * control-block snapshot to the frames (UDP -> socket receive rings). */
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v);
+
+/* Install a tcb as tcp_stream_create + LL_ADD do on a SYN (tcp.c:3-52) and
+ * wake a blocked naccept (tcp.c:108-116).  All values raw network order. */
+int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status);
+
+/* The current control-block snapshot in creation order (what rxg_flows_sync
+ * receives).  Counts are always written; arrays up to their capacities. */
+int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
+                 uint32_t *nt);
+
+/* counters: 0 = UDP datagrams delivered, 1 = dropped (receive ring full),
+ * 2 = TCP segments accepted by classify but not delivered (state machine out
+ * of scope), 3 = frames handed to KNI */
+uint64_t nstack_stat(int which);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,220 @@
+/*
+ * rxgpu.h — C ABI of the MI355X receive front end (librxgpu.so).
+ *
+ * Replaces the per-frame body of the reference's protocol lcore loop
+ * (pkt_process, netfamily.c:152-200) and the front halves of
+ *   int udp_process(struct rte_mbuf *)   udp.h:6,  udp.c:4-57
+ *   int tcp_process(struct rte_mbuf *)   tcp.h:6,  tcp.c:333-371
+ * together with the two flow lookups they call
+ *   get_hostinfo_fromip_port(dip, port, proto)       common.c:97-108
+ *   tcp_stream_search(sip, dip, sport, dport)        common.c:31-55
+ * and the DPDK 19.11.12 checksum they call (rte_ip.h:121-349, inlined
+ * into the reference as rte_ipv4_udptcp_cksum).
+ *
+ * A per-frame GPU call is meaningless, so the boundary is a BURST: the
+ * caller hands over N frames (packed buffer + offsets + lengths) and gets
+ * back N 16-byte verdicts that carry exactly what the reference functions
+ * decide per frame (return code, matched control block, payload window,
+ * checksum).  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Threading: one rxg_ctx per rx thread; a context is not thread-safe.
+ * Errors: API calls return 0 or a negative RXG_E* code (rxg_strerror);
+ * the library never exits the process (the reference rte_exit()s).
+ */
+#ifndef RXGPU_H
+#define RXGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- verdict --------------------------------------------------------- */
+
+#define RXG_FLOW_NONE 0xFFFFFFFFu
+
+/* frame class: the branch pkt_process takes (netfamily.c:156-199) */
+enum {
+    RXG_CLS_ARP = 0,        /* ether_type == BE 0x0806 (then also KNI, :194-199) */
+    RXG_CLS_NON_IP = 1,     /* any other non-IPv4 ether_type -> KNI (:194-199) */
+    RXG_CLS_IPV4_OTHER = 2, /* IPv4, next_proto_id not 6/17 -> KNI (:188-191) */
+    RXG_CLS_UDP = 3,        /* IPv4 proto 17 -> udp_process (:178-181) */
+    RXG_CLS_TCP = 4         /* IPv4 proto 6  -> tcp_process (:183-186) */
+};
+
+/* per-frame return codes, identical to the reference's */
+enum {
+    RXG_RC_OK = 0,              /* udp.c:56 / tcp.c:417 */
+    RXG_RC_TCP_BAD_CKSUM = -1,  /* tcp.c:352-357 */
+    RXG_RC_TCP_NO_TCB = -2,     /* tcp.c:363-371 */
+    RXG_RC_UDP_NOMEM = -2,      /* udp.c:38-43: rte_malloc(dgram_len-8) fails when
+                                   dgram_len <= 8 (size 0 or wrapped size_t) */
+    RXG_RC_UDP_NO_SOCKET = -3,  /* udp.c:15-19 */
+    RXG_RC_KNI = 1              /* non-TCP/UDP frame handed to KNI */
+};
+
+/* verdict.flags */
+#define RXG_F_TRUNC 0x01     /* the reference would read past the captured frame
+                                (ip total_length or dgram_len beyond caplen): the
+                                bytes past caplen are taken as zero here; the
+                                reference reads adjacent memory (parity undefined) */
+#define RXG_F_TCP_NEGLEN 0x02 /* TCP tl-20-hl < 0 (reference enqueues 0-length, tcp.c:157) */
+#define RXG_F_UDP_SHORT 0x04  /* UDP dgram_len <= 8 (rc -2, see RXG_RC_UDP_NOMEM) */
+
+typedef struct rxg_verdict {
+    uint32_t flow_id;      /* index of the matched control block in the arrays
+                              last given to rxg_flows_sync (UDP: into u[], TCP:
+                              into t[]); RXG_FLOW_NONE if no match / not looked up */
+    uint16_t payload_off;  /* UDP: 42 (udp.c:46 copies from udp+1); TCP: 34+hl */
+    uint16_t payload_len;  /* UDP: dgram_len-8 (udp.c:38); TCP: tl-20-hl (tcp.c:145-159);
+                              clamped at 0 (see flags) */
+    uint16_t l4_cksum;     /* rte_ipv4_udptcp_cksum with the L4 checksum field
+                              taken as 0 (tcp.c:349-351); 0 for non TCP/UDP */
+    uint8_t cls;           /* RXG_CLS_* */
+    int8_t rc;             /* RXG_RC_* */
+    uint8_t cksum_ok;      /* stored == l4_cksum (TCP verdict input; informational
+                              for UDP, which the reference never verifies) */
+    uint8_t flags;         /* RXG_F_* */
+    uint16_t stored_cksum; /* the L4 checksum field as stored in the frame (LE u16) */
+} rxg_verdict;
+
+/* ---- control-block snapshot (flow table source) ---------------------- */
+
+/* One UDP socket = one `struct localhost` of the reference (udp.h:10-29).
+ * Fields are raw network-order values exactly as the reference stores them
+ * (nbind, common.c:350-353). */
+typedef struct rxg_udp_sock {
+    uint32_t localip;
+    uint16_t localport;
+    uint8_t protocol; /* IPPROTO_UDP for every socket nsocket() makes */
+    uint8_t _pad;
+} rxg_udp_sock;
+
+/* One `struct tcp_stream` (tcp.h:29-55): key fields + status. sip/sport are
+ * the remote side as read from the packet (tcp_stream_create, tcp.c:16-19). */
+typedef struct rxg_tcb {
+    uint32_t sip;
+    uint32_t dip;
+    uint16_t sport;
+    uint16_t dport;
+    uint32_t status; /* TCP_STATUS_* of tcp.h:10-26; LISTEN == 1 */
+} rxg_tcb;
+
+#define RXG_TCP_STATUS_LISTEN 1u
+
+/* ---- mbuf-shaped descriptor (rte_mbuf field offsets, DPDK 19.11) ------- */
+typedef struct rxg_mbuf {
+    void *buf_addr;        /* @0  */
+    uint8_t _r0[8];
+    uint16_t data_off;     /* @16 */
+    uint8_t _r1[22];
+    uint16_t data_len;     /* @40 */
+    uint8_t _r2[86];
+} rxg_mbuf;                /* 128 bytes, like rte_mbuf */
+
+/* ---- error codes ------------------------------------------------------ */
+enum {
+    RXG_OK = 0,
+    RXG_EINVAL = -22,
+    RXG_ENOMEM = -12,
+    RXG_ENODEV = -19,
+    RXG_ERANGE = -34,
+    RXG_EHIP = -1000 /* HIP runtime error (details: rxg_last_hip_error) */
+};
+
+typedef struct rxg_ctx rxg_ctx;
+
+/* device argument of rxg_open for a control-plane-only context: flow tables
+ * and host lookups work, every burst call returns RXG_ENODEV */
+#define RXG_HOST_ONLY (-1)
+
+/* Open a context on HIP device `device`. max_pkts / max_bytes size the pinned
+ * host staging and device buffers used by rxg_classify (host-buffer path);
+ * rxg_classify_dev needs neither. */
+int rxg_open(rxg_ctx **ctx, int device, uint32_t max_pkts, uint64_t max_bytes);
+void rxg_close(rxg_ctx *ctx);
+const char *rxg_strerror(int err);
+const char *rxg_last_hip_error(void);
+
+/* Mirror of the reference's control-block lists, given in CREATION order
+ * (oldest first = the reverse of the head-inserted list, common.h:43-49), so
+ * that on duplicate keys the highest index (the newest block) wins exactly as
+ * the reference's first-match list scan does.  Builds the device flow table
+ * (bucketised hash for exact keys, direct port table for listeners). */
+int rxg_flows_sync(rxg_ctx *ctx, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t,
+                   uint32_t nt);
+
+/* Device-resident burst: all pointers are device pointers.  Frame i starts at
+ * d_pkts + (d_off[i] << off_unit_log2) (off_unit_log2 >= 4: 16-byte aligned
+ * starts) and has d_len[i] captured bytes; the buffer must extend to the next
+ * 16-byte boundary after every frame.  len_hint = typical frame length (picks
+ * lanes per frame; 0 = 1518).  If d_counts != NULL, per-flow packet counts are
+ * added into it (u64[nu + nt]: UDP flows first, then TCP).  Asynchronous on
+ * `stream` (a hipStream_t; NULL = the null stream). */
+int rxg_classify_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                     const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                     uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
+                     void *stream);
+
+/* Host-buffer burst (PCIe-inclusive): copies frames + descriptors to the
+ * device, classifies, copies verdicts back, accumulates the context's own
+ * per-flow counts.  Synchronous. */
+int rxg_classify(rxg_ctx *ctx, const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                 uint32_t n, uint32_t off_unit_log2, rxg_verdict *out);
+
+/* The reference's calling convention: a burst of mbuf pointers as dequeued at
+ * netfamily.c:147.  Frames are gathered into the context's staging buffer. */
+int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
+
+/* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
+int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
+int rxg_counts_reset(rxg_ctx *ctx);
+uint32_t rxg_num_flows(const rxg_ctx *ctx);
+
+/* Host-side lookups through the built flow table (same code path as the
+ * device probe, for control-plane use and tests). */
+uint32_t rxg_ft_lookup_udp(const rxg_ctx *ctx, uint32_t dip, uint16_t dport);
+uint32_t rxg_ft_lookup_tcp(const rxg_ctx *ctx, uint32_t sip, uint32_t dip, uint16_t sport,
+                           uint16_t dport);
+
+/* RSS: Toeplitz hash (standard 40-byte key) over sip,dip,sport,dport in
+ * network byte order, as a multi-queue NIC computes it; shard = hash % n. */
+uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
+
+/* ---- synthetic traffic (pktgen) --------------------------------------- */
+/* Deterministic counter-based generator: frame i is a pure function of
+ * (cfg, i), identical on host and device. Frames are written at
+ * off[i] = i * (slot_bytes >> off_unit_log2). */
+typedef struct rxg_gen_cfg {
+    uint64_t seed;
+    uint32_t size_mode;     /* 0 fixed frame_len, 1 IMIX 64/576/1500 at 7:4:1 */
+    uint32_t frame_len;     /* fixed-size frames (>= 64 for TCP/UDP) */
+    uint32_t slot_bytes;    /* bytes reserved per frame (multiple of 16, >= max frame) */
+    uint32_t proto_mode;    /* 0 UDP only, 1 TCP only, 2 TCP/UDP 50/50 */
+    uint32_t n_udp;         /* UDP sockets: local_ip:(udp_base_port + k) */
+    uint32_t n_tcp;         /* established tcbs: (10.128.x.y : 1024+..) -> local_ip:tcp_port */
+    uint32_t local_ip;      /* network order (192.168.100.77 = netfamily.c:11) */
+    uint16_t udp_base_port; /* host order */
+    uint16_t tcp_port;      /* host order (9999 = netfamily.c:270) */
+    uint32_t bad_cksum_per10k; /* one flipped payload bit after the checksum */
+    uint32_t unknown_per10k;   /* destination port with no socket / listener */
+    uint32_t other_per10k;     /* ICMP or ARP frames */
+    uint32_t shard;         /* keep only tuples whose rxg_rss_hash % n_shards == shard */
+    uint32_t n_shards;      /* 1 = no sharding */
+} rxg_gen_cfg;
+
+/* Flow set the generator assumes (the sockets/tcbs a test or bench binds). */
+int rxg_gen_flows(const rxg_gen_cfg *cfg, rxg_udp_sock *u, rxg_tcb *t);
+/* Host generation of frames [first, first+n) into caller buffers (slot i-first). */
+int rxg_gen_host(const rxg_gen_cfg *cfg, uint64_t first, uint32_t n, uint8_t *pkts,
+                 uint32_t *off, uint16_t *len, uint32_t off_unit_log2);
+/* Device generation (same frames), asynchronous on stream. */
+int rxg_gen_dev(const rxg_gen_cfg *cfg, uint64_t first, uint32_t n, uint8_t *d_pkts,
+                uint32_t *d_off, uint16_t *d_len, uint32_t off_unit_log2, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RXGPU_H */

@@ -1,0 +1,50 @@
+/*
+ * ref_cpu.h — CPU restatement of the reference receive front end.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker (and the CPU
+ * baseline timed by bench.py's cpu_baseline leg).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline may load it; the
+ * product path (librxgpu.so) never links, calls or falls back to it.
+ *
+ * Parity pin status: see ref_cpu.c header.
+ */
+#ifndef REF_CPU_H
+#define REF_CPU_H
+
+#include <stdint.h>
+
+#include "../include/rxgpu.h" /* verdict / control-block layouts only (types, no code) */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* DPDK 19.11.12 rte_ip.h restatements */
+uint32_t oracle_raw_cksum_acc(const void *buf, uint32_t len, uint32_t sum); /* __rte_raw_cksum */
+uint16_t oracle_raw_cksum(const void *buf, uint32_t len);                  /* rte_raw_cksum */
+uint16_t oracle_ipv4_phdr_cksum(const uint8_t *ipv4_hdr);                  /* rte_ipv4_phdr_cksum */
+uint16_t oracle_ipv4_udptcp_cksum(const uint8_t *ipv4_hdr, const uint8_t *l4); /* rte_ipv4_udptcp_cksum */
+uint16_t oracle_ipv4_cksum(const uint8_t *ipv4_hdr);                       /* rte_ipv4_cksum */
+
+/* control-block lists in the reference's own shape (head-inserted lists) */
+typedef struct oracle_tables oracle_tables;
+oracle_tables *oracle_tables_new(const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t, uint32_t nt);
+void oracle_tables_free(oracle_tables *tb);
+/* get_hostinfo_fromip_port / tcp_stream_search: return creation index or RXG_FLOW_NONE */
+uint32_t oracle_lookup_udp(const oracle_tables *tb, uint32_t dip, uint16_t port, uint8_t proto);
+uint32_t oracle_lookup_tcp(const oracle_tables *tb, uint32_t sip, uint32_t dip, uint16_t sport,
+                           uint16_t dport);
+
+/* pkt_process loop body + udp_process/tcp_process fronts, per frame.
+ * counts (nullable): u64[nu+nt], += 1 per frame with flow_id != NONE. */
+void oracle_classify(const oracle_tables *tb, const uint8_t *pkts, const uint32_t *off,
+                     const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out,
+                     uint64_t *counts);
+
+/* Toeplitz RSS (same definition as rxg_rss_hash, written independently) */
+uint32_t oracle_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

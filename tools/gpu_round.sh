@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a crash/timeout (anything but 0/1 from
+# pytest, anything but 0 elsewhere) ends the script there.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+TAG=${1:-r01}
+STEPS=${STEPS:-20}
+
+step() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" ; date +%T
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 5 "$OUT/$name.log"
+  return $rc
+}
+
+step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step bench 600 python bench.py --steps $STEPS --warmup 5 || exit $?
+grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
+if [ "${PROF:-1}" = 1 ]; then
+  export TMPDIR=/tmp
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
+      -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
+fi
+echo ALLDONE
