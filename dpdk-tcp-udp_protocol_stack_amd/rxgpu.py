@@ -20,6 +20,16 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librxgpu.so")
 NSTACK_PATH = os.path.join(_HERE, "libnstack.so")
 
+# One HIP runtime per process: PyTorch (the plumbing for device memory, streams
+# and torch.distributed) ships its own libamdhip64.so.7 with the same SONAME as
+# /opt/rocm's.  Loading torch first makes librxgpu bind to that copy; loading
+# librxgpu first would bring a second HIP/HSA runtime into the process, and the
+# two then contend for the device (observed: hipGetDeviceCount fails in one).
+try:
+    import torch  # noqa: F401
+except ImportError:  # a pure-C deployment links /opt/rocm's runtime directly
+    pass
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"{LIB_PATH} is missing: build it with `make -C {_HERE}` (or __graft_entry__.build()); "

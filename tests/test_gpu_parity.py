@@ -234,3 +234,13 @@ def test_full_size_properties(ctx, torch_dev, name):
         assert vh[i].tobytes() == want[0].tobytes(), (int(i), vh[i], want[0])
     del d_pk, outs
     torch.cuda.empty_cache()
+
+
+def test_single_hip_runtime_loaded(ctx):
+    """librxgpu and torch share one libamdhip64 (see rxgpu.py)."""
+    libs = set()
+    for line in open("/proc/self/maps"):
+        if "libamdhip64" in line:
+            libs.add(os.path.realpath(line.split()[-1]))
+    assert len(libs) == 1, libs
+    assert any("librxgpu.so" in line for line in open("/proc/self/maps"))

@@ -18,14 +18,14 @@ step() { # name timeout cmd...
   return $rc
 }
 
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step pytest_gpu 420 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-step bench 600 python bench.py --steps $STEPS --warmup 5 || exit $?
+step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step bench 300 python bench.py --steps $STEPS --warmup 5 || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
 if [ "${PROF:-1}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
+  step rocprof 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
       -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
 fi
 echo ALLDONE
