@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--workload", default="cfg2,cfg3")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
+                    "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -196,6 +198,16 @@ def main():
     torch.cuda.set_device(dev)
 
     ctx = R.Context(local)
+    if a.sweep:
+        for nm in a.sweep.split(","):
+            for var in R.KERNEL_VARIANTS:
+                ctx.tune(*var)
+                r = run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev)
+                log(f"sweep {nm} variant={var}: kernel {r['kernel_ms_avg']:.4f} ms "
+                    f"(min {r['kernel_ms_min']:.4f}), {r['mpps']:.1f} Mpps, "
+                    f"{r['roofline']['achieved']:.0f} GB/s")
+            ctx.tune(0)
+        return
     names = [s.strip() for s in a.workload.split(",") if s.strip()]
     results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}
     head = results[names[0]]

@@ -1,245 +1,358 @@
 // rx_classify.hip — K1: fused parse + L4 checksum + flow classify (gfx950).
 //
-// One frame is owned by a lane GROUP of G lanes (G = 4..64, a power of two,
-// chosen per burst from the typical frame length).  Lane k of the group reads
-// the 16-B chunks k, k+G, k+2G, ... of the frame, so one wave-instruction
-// loads 64 x 16 B = 1 KiB of contiguous frame bytes (frames are packed in
-// HBM), and a 64-B frame is exactly one load per lane at G = 4.
+// Work decomposition
+//   A frame is owned by a lane GROUP of G lanes (G = 4..64, power of two).
+//   Lane k of the group reads the 16-B chunks k, k+G, k+2G, ... of the frame;
+//   one "pass" of the group covers 16*G contiguous frame bytes, so a wave
+//   instruction loads 64 x 16 B = 1 KiB of contiguous HBM (frames are packed).
+//   Each group handles FPG frames per loop trip, and each frame's first P
+//   passes are loaded up front: all FPG*P loads of a lane are in flight before
+//   the first one is consumed (memory-level parallelism without LDS staging;
+//   the bytes are touched once, so there is nothing to reuse from LDS).
+//   A block (256 threads) covers a tile of (256/G)*FPG consecutive frames per
+//   trip; blocks stride over tiles, and the grid is sized to the number of
+//   blocks the chip keeps resident, so every block gets the same share.
 //
-// What each frame goes through (reference behaviour, see ../../include/rxgpu.h):
+// Per frame (reference behaviour, see ../../include/rxgpu.h)
 //   pkt_process demux           netfamily.c:152-200
 //   udp_process front           udp.c:11-19, 37-46
-//   tcp_process front           tcp.c:345-371 (checksum with field zeroed)
-//   rte_ipv4_udptcp_cksum       rte_ip.h:325-349 (DPDK 19.11.12, IHL ignored)
+//   tcp_process front           tcp.c:345-371 (checksum with the field zeroed)
+//   rte_ipv4_udptcp_cksum       rte_ip.h:325-349 (DPDK 19.11.12; IHL ignored)
 //   get_hostinfo_fromip_port    common.c:97-108   -> UDP bucket probe
 //   tcp_stream_search           common.c:31-55    -> TCP bucket probe, then listener table
 //
-// Checksum: the one's-complement sum is order-independent as long as the
-// total is formed without losing carries; a u32 holds the plain sum of up to
-// 65535 bytes of 16-bit words (< 2^31), so every lane accumulates a plain u32,
-// the group adds the lane sums with a shuffle butterfly, and the fold happens
-// once.  Words are little-endian 16-bit words at even frame offsets, exactly
-// the reference's native-word view (frame starts are 16-B aligned).
+// Checksum arithmetic
+//   The reference value is fold(S), S = plain sum of the little-endian 16-bit
+//   words of [ip.src, ip+tl) plus the pseudo words {0,proto} and be16(tl-20),
+//   with the L4 checksum field read as 0; fold = end-around-carry reduction,
+//   0 iff S == 0.  fold only depends on S mod 0xFFFF and on S == 0, so any
+//   split of the words over lanes works as long as partial sums are exact
+//   integers: each lane adds its dwords' two halves with v_dot2_u32_u16
+//   (x.lo*1 + x.hi*1 + acc), the group adds lane sums with DPP / swizzle, and
+//   the one fold happens at the end.  Bytes outside [26, min(34+tl-20, caplen))
+//   and the 2-byte checksum field are masked out: lanes 0..3 of pass 0 own the
+//   header bytes (compile-time masks), only the chunk that straddles the end
+//   needs a computed mask.
 //
-// Flow probe: the 4 lowest lanes of the group load one 64-B bucket (4 slots)
-// and __ballot the compare; the matching lane's value is shuffled to the group.
+// Flow probe
+//   Buckets are 4 slots x 16 B = one 64-B line; lanes 0..3 of the group load
+//   the 4 slots of a bucket in one coalesced access and __ballot the compare.
 #include <hip/hip_runtime.h>
 
 #include "rx_common.h"
 
 namespace {
 
-// bytes [lo, hi) of the 4-byte little-endian word that starts at `pos`
-__device__ __forceinline__ uint32_t keep_mask(int32_t pos, int32_t lo, int32_t hi) {
-    int32_t a = lo - pos;
-    int32_t b = hi - pos;
-    a = a < 0 ? 0 : (a > 4 ? 4 : a);
-    b = b < 0 ? 0 : (b > 4 ? 4 : b);
-    uint64_t m = ((1ull << (8 * b)) - 1ull) & ~((1ull << (8 * a)) - 1ull);
-    return (uint32_t)m;
-}
-
-// sum of the LE 16-bit words of chunk c (frame bytes [s, s+16)) restricted to
-// [lo, hi), with the 2-byte field at `hole` (even; -64 = none) taken as zero
-__device__ __forceinline__ uint32_t chunk_sum(uint4 c, int32_t s, int32_t lo, int32_t hi,
-                                              int32_t hole) {
-    uint32_t x[4] = {c.x, c.y, c.z, c.w};
-    uint32_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        int32_t pos = s + 4 * j;
-        uint32_t m = keep_mask(pos, lo, hi);
-        // hole bytes [hole, hole+2) inside this word?
-        int32_t hd = hole - pos; // 0 or 2 when inside (hole is even)
-        if (hd == 0) m &= 0xFFFF0000u;
-        if (hd == 2) m &= 0x0000FFFFu;
-        uint32_t v = x[j] & m;
-        acc += (v & 0xFFFFu) + (v >> 16);
+// ---- intra-group broadcast / reduction (group = G aligned lanes) ----------
+template <int G, int K>
+__device__ __forceinline__ uint32_t gbcast(uint32_t x) {
+    static_assert(K < G, "lane out of group");
+    if constexpr (G == 4) {
+        return __builtin_amdgcn_update_dpp(0u, x, K * 0x55, 0xF, 0xF, false); // quad_perm [K,K,K,K]
+    } else if constexpr (G <= 32) {
+        // ds_swizzle bitmask mode: lane' = (lane & and) | or, within 32 lanes
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (0x1F & ~(G - 1)) | (K << 5));
+    } else {
+        return __builtin_amdgcn_readlane(x, K);
     }
-    return acc;
-}
-
-__device__ __forceinline__ uint4 mask_chunk(uint4 c, int32_t s, int32_t cap) {
-    c.x &= keep_mask(s + 0, 0, cap);
-    c.y &= keep_mask(s + 4, 0, cap);
-    c.z &= keep_mask(s + 8, 0, cap);
-    c.w &= keep_mask(s + 12, 0, cap);
-    return c;
 }
 
 template <int G>
+__device__ __forceinline__ uint32_t gsum(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x += __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xF, 0xF, false); // row_half_mirror
+    if constexpr (G >= 16) x += __builtin_amdgcn_update_dpp(0u, x, 0x140, 0xF, 0xF, false); // row_mirror
+    if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 10)); // xor 16
+    if constexpr (G == 64) x = __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 32);
+    return x;
+}
+
+typedef unsigned short rx_us2 __attribute__((ext_vector_type(2)));
+
+// acc + x.lo + x.hi in one v_dot2_u32_u16
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t x) {
+    const rx_us2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(rx_us2, x), one, acc, false);
+}
+
+// keep only the bytes of dword x (at frame offset pos) that lie below `end`
+__device__ __forceinline__ uint32_t keep_below(uint32_t x, int32_t pos, int32_t end) {
+    int32_t k = end - pos;
+    k = k < 0 ? 0 : (k > 4 ? 4 : k);
+    return k == 4 ? x : (x & ((1u << (8 * k)) - 1u));
+}
+
+__device__ __forceinline__ uint4 chunk_below(uint4 c, int32_t s, int32_t end) {
+    c.x = keep_below(c.x, s + 0, end);
+    c.y = keep_below(c.y, s + 4, end);
+    c.z = keep_below(c.z, s + 8, end);
+    c.w = keep_below(c.w, s + 12, end);
+    return c;
+}
+
+typedef unsigned int rx_u32x4 __attribute__((ext_vector_type(4)));
+
+// streaming 16-B load / store (frames and verdicts are touched once: nt)
+__device__ __forceinline__ uint4 ldg16(const uint8_t *p) {
+    const rx_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rx_u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
+    const rx_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(p));
+}
+
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+    s = (s >> 16) + (s & 0xFFFFu);
+    s = (s >> 16) + (s & 0xFFFFu);
+    return s;
+}
+
+template <int G, int P, int FPG>
 __global__ __launch_bounds__(256) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
-    constexpr uint32_t GPB = 256 / G;  // frame groups per block
-    constexpr int32_t STEP = 16 * G;   // bytes one group pass covers
+    constexpr uint32_t GPB = 256 / G;     // frame groups per block
+    constexpr uint32_t TILE = GPB * FPG;  // frames per block per trip
+    constexpr int32_t STEP = 16 * G;      // bytes one group pass covers
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t gbase = lane & ~(uint32_t)(G - 1);
     const uint32_t grp = tid / G;
+    const int32_t s0 = 16 * (int32_t)gl;
 
     if (lds_bins) {
         for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
         __syncthreads();
     }
 
-    const uint64_t stride = (uint64_t)gridDim.x * GPB;
-    for (uint64_t p = (uint64_t)blockIdx.x * GPB + grp; p < n; p += stride) {
-        const uint8_t *f = pkts + ((uint64_t)off[p] << unit_log2);
-        const int32_t cap = (int32_t)len[p];
-
-        // ---- pass 0: chunk gl, header fields broadcast from lanes 0..3
-        const int32_t s0 = 16 * (int32_t)gl;
-        uint4 c0 = make_uint4(0, 0, 0, 0);
-        if (s0 < cap) c0 = mask_chunk(*reinterpret_cast<const uint4 *>(f + s0), s0, cap);
-
-        const uint32_t h03 = __shfl(c0.w, gbase + 0); // bytes 12..15
-        const uint32_t h10 = __shfl(c0.x, gbase + 1); // 16..19
-        const uint32_t h11 = __shfl(c0.y, gbase + 1); // 20..23
-        const uint32_t h12 = __shfl(c0.z, gbase + 1); // 24..27
-        const uint32_t h13 = __shfl(c0.w, gbase + 1); // 28..31
-        const uint32_t h20 = __shfl(c0.x, gbase + 2); // 32..35
-        const uint32_t h21 = __shfl(c0.y, gbase + 2); // 36..39
-        const uint32_t h22 = __shfl(c0.z, gbase + 2); // 40..43
-        const uint32_t h23 = __shfl(c0.w, gbase + 2); // 44..47
-        const uint32_t h30 = __shfl(c0.x, gbase + 3); // 48..51
-
-        const uint32_t et = h03 & 0xFFFFu; // LE view of bytes 12,13
-        const uint32_t tl = rx_bswap16(h10 & 0xFFFFu);
-        const uint32_t proto = h11 >> 24;
-        const uint32_t sip = (h12 >> 16) | (h13 << 16);
-        const uint32_t dip = (h13 >> 16) | (h20 << 16);
-        const uint32_t sport = h20 >> 16;
-        const uint32_t dport = h21 & 0xFFFFu;
-        const uint32_t dgram_len = rx_bswap16(h21 >> 16);
-
-        uint32_t cls, need;
-        int32_t hole = -64;
-        if (et == 0x0608u) {
-            cls = RXG_CLS_ARP;
-            need = 42;
-        } else if (et != 0x0008u) {
-            cls = RXG_CLS_NON_IP;
-            need = 14;
-        } else if (proto == 17u) {
-            cls = RXG_CLS_UDP;
-            hole = 40;
-            need = 42;
-        } else if (proto == 6u) {
-            cls = RXG_CLS_TCP;
-            hole = 50;
-            need = 54;
-        } else {
-            cls = RXG_CLS_IPV4_OTHER;
-            need = 24;
-        }
-        const bool l4 = cls == RXG_CLS_UDP || cls == RXG_CLS_TCP;
-        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-        const bool do_sum = l4 && tl >= 20u;
-        if (l4 && 34u + l4n > need) need = 34u + l4n;
-
-        // ---- checksum over [26, 34 + l4n) ∩ [0, cap) (pseudo src/dst + L4)
-        const int32_t lo = 26;
-        int32_t hi = do_sum ? 34 + (int32_t)l4n : 0;
-        if (hi > cap) hi = cap;
-        uint32_t sum = do_sum ? chunk_sum(c0, s0, lo, hi, hole) : 0u;
-        for (int32_t sb = STEP; sb < hi; sb += 4 * STEP) { // group-uniform trip count
-            uint4 c[4];
+    for (uint64_t tile = blockIdx.x; tile * TILE < n; tile += gridDim.x) {
+        // ---- phase A: descriptors of the FPG frames
+        uint64_t pf[FPG];
+        bool valid[FPG];
+        const uint8_t *fb[FPG];
+        int32_t cap[FPG];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int32_t s = s0 + sb + u * STEP;
-                c[u] = make_uint4(0, 0, 0, 0);
-                if (s < hi) c[u] = *reinterpret_cast<const uint4 *>(f + s);
+        for (int f = 0; f < FPG; ++f) {
+            pf[f] = tile * TILE + (uint64_t)f * GPB + grp;
+            valid[f] = pf[f] < n;
+            const uint64_t q = valid[f] ? pf[f] : 0;
+            fb[f] = pkts + ((uint64_t)off[q] << unit_log2);
+            cap[f] = valid[f] ? (int32_t)len[q] : 0;
+        }
+        // ---- phase B: the first P passes of every frame, all in flight
+        uint4 c[FPG][P];
+#pragma unroll
+        for (int f = 0; f < FPG; ++f)
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const int32_t s = s0 + q * STEP;
+                c[f][q] = make_uint4(0, 0, 0, 0);
+                if (s < cap[f]) c[f][q] = ldg16(fb[f] + s);
             }
+
+        // ---- phase C: parse + checksum per frame
+        uint32_t cls[FPG], ck[FPG], stored[FPG], tl[FPG], dgl[FPG], hl[FPG], need[FPG];
+        uint32_t ka[FPG], kb[FPG], kc[FPG], dport[FPG];
+        bool ok[FPG];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) sum += chunk_sum(c[u], s0 + sb + u * STEP, lo, hi, hole);
+        for (int f = 0; f < FPG; ++f) {
+            const int32_t cp = cap[f];
+            uint4 x0 = c[f][0];
+            if (s0 < cp && s0 + 16 > cp) x0 = chunk_below(x0, s0, cp); // bytes past caplen read 0
+            const uint32_t h03 = gbcast<G, 0>(x0.w); // bytes 12..15
+            const uint32_t h10 = gbcast<G, 1>(x0.x); // 16..19
+            const uint32_t h11 = gbcast<G, 1>(x0.y); // 20..23
+            const uint32_t h12 = gbcast<G, 1>(x0.z); // 24..27
+            const uint32_t h13 = gbcast<G, 1>(x0.w); // 28..31
+            const uint32_t h20 = gbcast<G, 2>(x0.x); // 32..35
+            const uint32_t h21 = gbcast<G, 2>(x0.y); // 36..39
+            const uint32_t h22 = gbcast<G, 2>(x0.z); // 40..43
+            const uint32_t h23 = gbcast<G, 2>(x0.w); // 44..47
+            const uint32_t h30 = gbcast<G, 3>(x0.x); // 48..51
+
+            const uint32_t et = h03 & 0xFFFFu; // LE view of bytes 12,13
+            tl[f] = rx_bswap16(h10 & 0xFFFFu);
+            const uint32_t proto = h11 >> 24;
+            const uint32_t sip = (h12 >> 16) | (h13 << 16);
+            const uint32_t dip = (h13 >> 16) | (h20 << 16);
+            const uint32_t sport = h20 >> 16;
+            dport[f] = h21 & 0xFFFFu;
+            dgl[f] = rx_bswap16(h21 >> 16);
+            hl[f] = ((h23 >> 16) & 0xFFu) >> 4;
+
+            uint32_t cl, nd;
+            if (et == 0x0608u) {
+                cl = RXG_CLS_ARP;
+                nd = 42;
+            } else if (et != 0x0008u) {
+                cl = RXG_CLS_NON_IP;
+                nd = 14;
+            } else if (proto == 17u) {
+                cl = RXG_CLS_UDP;
+                nd = 42;
+            } else if (proto == 6u) {
+                cl = RXG_CLS_TCP;
+                nd = 54;
+            } else {
+                cl = RXG_CLS_IPV4_OTHER;
+                nd = 24;
+            }
+            const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+            const bool l4 = is_udp || is_tcp;
+            const uint32_t l4n = tl[f] >= 20u ? tl[f] - 20u : 0u;
+            const bool do_sum = l4 && tl[f] >= 20u;
+            if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+            cls[f] = cl;
+            need[f] = nd;
+
+            // checksum region [26, e): e = min(34 + l4n, caplen)
+            int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+            if (e > cp) e = cp;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const int32_t s = s0 + q * STEP;
+                uint4 v = c[f][q];
+                if (s + 16 > e) v = chunk_below(v, s, e);
+                if (q == 0) { // header bytes [0,26) and the checksum field are not summed
+                    if (gl == 0) v = make_uint4(0, 0, 0, 0);
+                    if (gl == 1) {
+                        v.x = 0;
+                        v.y = 0;
+                        v.z &= 0xFFFF0000u;
+                    }
+                    if (gl == 2 && is_udp) v.z &= 0xFFFF0000u; // UDP cksum at 40..41
+                    if (gl == 3 && is_tcp) v.x &= 0x0000FFFFu; // TCP cksum at 50..51
+                }
+                acc = add_halves(acc, v.x);
+                acc = add_halves(acc, v.y);
+                acc = add_halves(acc, v.z);
+                acc = add_halves(acc, v.w);
+            }
+            // frames longer than P passes: the rest in batches of 4 passes
+            for (int32_t sb = P * STEP; sb < e; sb += 4 * STEP) { // group-uniform
+                uint4 r[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int32_t s = s0 + sb + u * STEP;
+                    r[u] = make_uint4(0, 0, 0, 0);
+                    if (s < e) r[u] = ldg16(fb[f] + s);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int32_t s = s0 + sb + u * STEP;
+                    uint4 v = r[u];
+                    if (s + 16 > e) v = chunk_below(v, s, e);
+                    acc = add_halves(acc, v.x);
+                    acc = add_halves(acc, v.y);
+                    acc = add_halves(acc, v.z);
+                    acc = add_halves(acc, v.w);
+                }
+            }
+            uint32_t sum = gsum<G>(acc);
+            uint32_t k = 0;
+            if (do_sum) {
+                sum += proto << 8;       // psd {zero, proto}
+                sum += rx_bswap16(l4n);  // psd be16(l4_len)
+                k = (~fold16(sum)) & 0xFFFFu;
+                if (k == 0u && proto == 17u) k = 0xFFFFu;
+            }
+            ck[f] = k;
+            stored[f] = is_udp ? (h22 & 0xFFFFu) : (is_tcp ? (h30 >> 16) : 0u);
+            ok[f] = l4 && stored[f] == k;
+            ka[f] = is_udp ? dip : sip;
+            kb[f] = is_udp ? dport[f] : dip;
+            kc[f] = is_udp ? 17u : (sport | (dport[f] << 16));
+        }
+
+        // ---- phase D: flow probes (first bucket of every frame in flight)
+        uint32_t flow[FPG], bkt[FPG];
+        uint4 sl[FPG];
+        bool probe[FPG];
+#pragma unroll
+        for (int f = 0; f < FPG; ++f) {
+            probe[f] = valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
+            const bool udp = cls[f] == RXG_CLS_UDP;
+            bkt[f] = rx_hash3(ka[f], kb[f], kc[f]) & (udp ? ft.udp_mask : ft.tcp_mask);
+            sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
+            if (probe[f] && gl < RX_BUCKET_SLOTS) sl[f] = (udp ? ft.udp : ft.tcp)[(bkt[f] << 2) + gl];
+            flow[f] = RXG_FLOW_NONE;
         }
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-
-        uint32_t ck = 0;
-        if (do_sum) {
-            sum += proto << 8;          // psd {zero, proto}
-            sum += rx_bswap16(l4n);     // psd be16(l4_len)
-            ck = (~rx_fold(sum)) & 0xFFFFu;
-            if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-        }
-        const uint32_t stored = cls == RXG_CLS_UDP ? (h22 & 0xFFFFu)
-                                                   : (cls == RXG_CLS_TCP ? (h30 >> 16) : 0u);
-        const bool ok = l4 && stored == ck;
-
-        // ---- flow probe
-        const bool do_udp = cls == RXG_CLS_UDP;
-        const bool do_tcp = cls == RXG_CLS_TCP && ok;
-        uint32_t flow = RXG_FLOW_NONE;
-        if (do_udp || do_tcp) {
-            const uint4 *tbl = do_udp ? ft.udp : ft.tcp;
-            const uint32_t mask = do_udp ? ft.udp_mask : ft.tcp_mask;
-            const uint32_t maxp = do_udp ? ft.udp_probe : ft.tcp_probe;
-            const uint32_t ka = do_udp ? dip : sip;
-            const uint32_t kb = do_udp ? dport : dip;
-            const uint32_t kc = do_udp ? 17u : (sport | (dport << 16));
-            uint32_t b = rx_hash3(ka, kb, kc) & mask;
-            for (uint32_t pr = 0; pr < maxp; ++pr) {
-                uint4 sl = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-                if (gl < RX_BUCKET_SLOTS) sl = tbl[(b << 2) + gl];
-                const bool hit = gl < RX_BUCKET_SLOTS && sl.w != RX_SLOT_EMPTY && sl.x == ka &&
-                                 sl.y == kb && sl.z == kc;
-                const bool emp = gl < RX_BUCKET_SLOTS && sl.w == RX_SLOT_EMPTY;
-                const uint32_t gh = (uint32_t)(__ballot(hit) >> gbase) & 0xFu;
-                const uint32_t ge = (uint32_t)(__ballot(emp) >> gbase) & 0xFu;
-                const uint32_t v = __shfl(sl.w, gbase + (gh ? (uint32_t)(__ffs(gh) - 1) : 0u));
+        for (int f = 0; f < FPG; ++f) {
+            const bool udp = cls[f] == RXG_CLS_UDP;
+            const uint4 *tbl = udp ? ft.udp : ft.tcp;
+            const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
+            const uint32_t maxp = udp ? ft.udp_probe : ft.tcp_probe;
+            uint4 s = sl[f];
+            uint32_t b = bkt[f];
+            for (uint32_t pr = 0; pr < maxp; ++pr) { // trips are group-uniform
+                const bool hit = probe[f] && gl < RX_BUCKET_SLOTS && s.w != RX_SLOT_EMPTY &&
+                                 s.x == ka[f] && s.y == kb[f] && s.z == kc[f];
+                const bool emp = probe[f] && gl < RX_BUCKET_SLOTS && s.w == RX_SLOT_EMPTY;
+                const uint64_t hm = __ballot(hit), em = __ballot(emp);
+                const uint32_t gh = (uint32_t)(hm >> gbase) & 0xFu;
+                const uint32_t ge = (uint32_t)(em >> gbase) & 0xFu;
+                const uint32_t lanesrc = gbase + (gh ? (uint32_t)(__ffs(gh) - 1) : 0u);
+                const uint32_t v = __shfl(s.w, lanesrc);
+                if (!probe[f]) break; // probe[f], gh, ge are uniform across the group
                 if (gh) {
-                    flow = v;
+                    flow[f] = v;
                     break;
                 }
                 if (ge) break;
                 b = (b + 1) & mask;
+                s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
+                if (gl < RX_BUCKET_SLOTS) s = tbl[(b << 2) + gl];
             }
-            if (do_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
+            if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
+                flow[f] = ft.listen[dport[f]];
         }
 
-        // ---- verdict (reference return codes)
-        int32_t rc;
-        uint32_t poff = 0, plen = 0, flags = 0;
-        if (cls == RXG_CLS_UDP) {
-            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                       : (dgram_len <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-            poff = 42;
-            plen = dgram_len > 8u ? dgram_len - 8u : 0u;
-            if (dgram_len <= 8u) flags |= RXG_F_UDP_SHORT;
-            if (rc == RXG_RC_OK && 42u + plen > need) need = 42u + plen;
-        } else if (cls == RXG_CLS_TCP) {
-            const uint32_t hl = ((h23 >> 16) & 0xFFu) >> 4;
-            const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-            poff = 34u + 4u * hl;
-            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-            plen = pl < 0 ? 0u : (uint32_t)pl;
-            rc = !ok ? RXG_RC_TCP_BAD_CKSUM
-                     : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-        } else {
-            rc = RXG_RC_KNI;
-        }
-        if ((int32_t)need > cap) flags |= RXG_F_TRUNC;
-
-        if (gl == 0) {
-            uint4 v;
-            v.x = flow;
-            v.y = (poff & 0xFFFFu) | (plen << 16);
-            v.z = ck | (cls << 16) | (((uint32_t)rc & 0xFFu) << 24);
-            v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-            out[p] = v;
-            if (counts && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) {
-                const uint32_t idx = (cls == RXG_CLS_TCP ? ft.nu : 0u) + flow;
-                if (lds_bins)
-                    atomicAdd(&hist[idx], 1u);
-                else
-                    atomicAdd(&counts[idx], 1ull);
+        // ---- phase E: verdicts (reference return codes) + counts
+#pragma unroll
+        for (int f = 0; f < FPG; ++f) {
+            int32_t rc;
+            uint32_t poff = 0, plen = 0, flags = 0, nd = need[f];
+            if (cls[f] == RXG_CLS_UDP) {
+                rc = flow[f] == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                              : (dgl[f] <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+                poff = 42;
+                plen = dgl[f] > 8u ? dgl[f] - 8u : 0u;
+                if (dgl[f] <= 8u) flags |= RXG_F_UDP_SHORT;
+                if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+            } else if (cls[f] == RXG_CLS_TCP) {
+                const int32_t pl = (int32_t)tl[f] - 20 - 4 * (int32_t)hl[f];
+                poff = 34u + 4u * hl[f];
+                if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+                plen = pl < 0 ? 0u : (uint32_t)pl;
+                rc = !ok[f] ? RXG_RC_TCP_BAD_CKSUM
+                            : (flow[f] == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+            } else {
+                rc = RXG_RC_KNI;
+            }
+            if ((int32_t)nd > cap[f]) flags |= RXG_F_TRUNC;
+            if (gl == 0 && valid[f]) {
+                uint4 v;
+                v.x = flow[f];
+                v.y = (poff & 0xFFFFu) | (plen << 16);
+                v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
+                v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
+                stg16(&out[pf[f]], v);
+                if (counts && rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE) {
+                    const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
+                    if (lds_bins)
+                        atomicAdd(&hist[idx], 1u);
+                    else
+                        atomicAdd(&counts[idx], 1ull);
+                }
             }
         }
     }
@@ -253,52 +366,81 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     }
 }
 
-template <int G>
-hipError_t launch_g(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+template <int G, int P, int FPG>
+hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
-                    uint32_t lds_bins, uint32_t max_blocks, hipStream_t s) {
-    constexpr uint32_t GPB = 256 / G;
-    uint64_t blocks = (n + GPB - 1) / GPB;
-    if (blocks > max_blocks) blocks = max_blocks;
+                    uint32_t lds_bins, hipStream_t s) {
+    constexpr uint32_t TILE = (256 / G) * FPG;
+    const size_t lds = (size_t)lds_bins * 4u;
+    // resident blocks: one wave of blocks, equal shares, no tail (cached per LDS size)
+    static int cu = 0;
+    static int cached_occ[2] = {0, 0};
+    static size_t cached_lds[2] = {~(size_t)0, ~(size_t)0};
+    if (cu == 0) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        e = hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+    }
+    const int slot = lds ? 1 : 0;
+    if (cached_lds[slot] != lds) {
+        int occ = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG>), 256, lds);
+        if (e != hipSuccess) return e;
+        cached_occ[slot] = occ > 0 ? occ : 1;
+        cached_lds[slot] = lds;
+    }
+    const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
+    uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
+    if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    size_t lds = (size_t)lds_bins * 4u;
-    hipLaunchKernelGGL((rx_classify_kernel<G>), dim3((uint32_t)blocks), dim3(256), lds, s, pkts, off,
-                       len, n, unit_log2, ft, out, counts, lds_bins);
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG>), dim3((uint32_t)blocks), dim3(256), lds, s,
+                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
 
+typedef hipError_t (*launch_fn)(const uint8_t *, const uint32_t *, const uint16_t *, uint32_t,
+                                uint32_t, const rx_ft_dev &, uint4 *, unsigned long long *,
+                                uint32_t, hipStream_t);
+struct variant_entry {
+    uint32_t g, p, fpg;
+    launch_fn fn;
+};
+// every compiled variant; the first entry per G is its default
+static const variant_entry k_variants[] = {
+    {4, 1, 2, launch_v<4, 1, 2>},   {4, 1, 1, launch_v<4, 1, 1>},   {4, 1, 4, launch_v<4, 1, 4>},
+    {8, 2, 2, launch_v<8, 2, 2>},   {8, 2, 1, launch_v<8, 2, 1>},   {16, 2, 2, launch_v<16, 2, 2>},
+    {16, 2, 1, launch_v<16, 2, 1>}, {32, 3, 2, launch_v<32, 3, 2>}, {32, 3, 1, launch_v<32, 3, 1>},
+    {32, 2, 1, launch_v<32, 2, 1>}, {64, 4, 1, launch_v<64, 4, 1>}, {64, 2, 1, launch_v<64, 2, 1>},
+};
+
 } // namespace
 
-// Lanes per frame from a typical frame length: about two to three group
-// passes per frame, at least 4 lanes (the 64-B header spans 4 chunks).
+// Lanes per frame (G) from the typical frame length.  Any frame length works
+// with any variant (frames longer than P passes take the remainder loop); the
+// choice only moves speed.
 uint32_t rx_pick_group(uint32_t len_hint) {
     if (len_hint == 0) len_hint = 1518;
-    uint32_t chunks = (len_hint + 15) / 16;
-    uint32_t g = 4;
-    while (g < 64 && g * 2 <= chunks / 2) g *= 2;
-    return g;
+    if (len_hint <= 64) return 4;
+    if (len_hint <= 256) return 8;
+    if (len_hint <= 512) return 16;
+    if (len_hint <= 1536) return 32;
+    return 64;
 }
 
+// variant = (g, p, fpg); p == 0 / fpg == 0 pick the default for g.
 // LDS histogram when the flow count fits comfortably (<= 8192 bins = 32 KiB).
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
-                              uint32_t n, uint32_t unit_log2, uint32_t group, const rx_ft_dev &ft,
-                              uint4 *out, unsigned long long *counts, hipStream_t s) {
+                              uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
+                              const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
+                              hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t nflows = ft.nu + ft.nt;
     const uint32_t lds_bins = (counts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
-    const uint32_t max_blocks = 256u * 8u; // 256 CUs x 8 resident 256-thread blocks
-    switch (group) {
-    case 4:
-        return launch_g<4>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, max_blocks, s);
-    case 8:
-        return launch_g<8>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, max_blocks, s);
-    case 16:
-        return launch_g<16>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, max_blocks, s);
-    case 32:
-        return launch_g<32>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, max_blocks, s);
-    case 64:
-        return launch_g<64>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, max_blocks, s);
-    default:
-        return hipErrorInvalidValue;
-    }
+    for (const variant_entry &v : k_variants)
+        if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg))
+            return v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s);
+    return hipErrorInvalidValue;
 }

@@ -43,6 +43,9 @@ RC_OK, RC_TCP_BAD_CKSUM, RC_TCP_NO_TCB, RC_UDP_NOMEM, RC_UDP_NO_SOCKET, RC_KNI =
 F_TRUNC, F_TCP_NEGLEN, F_UDP_SHORT = 0x1, 0x2, 0x4
 TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
 HOST_ONLY = -1
+# (lanes per frame, passes up front, frames per group) compiled in rx_classify.hip
+KERNEL_VARIANTS = [(4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
+                   (32, 3, 2), (32, 3, 1), (32, 2, 1), (64, 4, 1), (64, 2, 1)]
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -96,6 +99,7 @@ _process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
 _flow_counts = _sig("rxg_flow_counts", _i32, _vp, _vp, _u32)
 _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
 _num_flows = _sig("rxg_num_flows", _u32, _vp)
+_tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32)
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
 _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
@@ -105,7 +109,7 @@ _gen_dev = _sig("rxg_gen_dev", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _v
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev"]
 
 
@@ -178,6 +182,10 @@ class Context:
         _check(_flows_sync(self._h, _ptr(udp) if len(udp) else None, len(udp),
                            _ptr(tcb) if len(tcb) else None, len(tcb)), "rxg_flows_sync")
         self.nu, self.nt = len(udp), len(tcb)
+
+    def tune(self, lanes_per_frame: int = 0, passes: int = 0, frames_per_group: int = 0):
+        """force a kernel variant (0 = automatic); see KERNEL_VARIANTS"""
+        _check(_tune(self._h, lanes_per_frame, passes, frames_per_group), "rxg_tune")
 
     @property
     def num_flows(self) -> int:

@@ -135,6 +135,28 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
         assert np.array_equal(cnt, wcnt), (name, hint)
 
 
+@pytest.mark.parametrize("variant", R.KERNEL_VARIANTS)
+def test_every_kernel_variant(ctx, torch_dev, variant):
+    """each compiled (lanes, passes, frames-per-group) variant, on mixed sizes"""
+    fl = np.load(os.path.join(GOLD, "edge_flows.npz"))
+    frames = F.read_pcap(os.path.join(GOLD, "edge.pcap"))
+    cfg = rxdist.gen_cfg("cfg4", n_udp=64, n_tcp=64)
+    pk, off, ln = R.gen_host(cfg, 0, 700, 6)
+    frames = frames + [pk[i * 1536:i * 1536 + ln[i]].tobytes() for i in range(700)]
+    udp, tcb = R.gen_flows(cfg)
+    udp = np.concatenate([fl["udp"], udp])
+    tcb = np.concatenate([fl["tcb"], tcb])
+    ctx.flows_sync(udp, tcb)
+    buf, off, lens = F.pack_frames(frames, 4)
+    want = O.Tables(udp, tcb).classify(buf, off, lens, 4)
+    ctx.tune(*variant)
+    try:
+        got = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 0)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
+
+
 def test_fuzzed_frames_match_oracle(ctx, torch_dev):
     """random header mutations, random total_length / dgram_len / data offset,
     random capture lengths: every verdict byte must match"""

@@ -20,6 +20,9 @@ step() { # name timeout cmd...
 
 step pytest_gpu 420 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -n "${SWEEP:-}" ]; then
+  step sweep 300 python bench.py --sweep "$SWEEP" --steps 10 --warmup 3 || exit $?
+fi
 step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 300 python bench.py --steps $STEPS --warmup 5 || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
