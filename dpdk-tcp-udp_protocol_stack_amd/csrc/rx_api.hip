@@ -275,7 +275,7 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group) {
     if (!c) return RXG_EINVAL;
-    if (lanes_per_frame && (lanes_per_frame < 4 || lanes_per_frame > 64 ||
+    if (lanes_per_frame && (lanes_per_frame == 2 || lanes_per_frame > 64 ||
                             (lanes_per_frame & (lanes_per_frame - 1))))
         return RXG_EINVAL;
     c->tune_g = lanes_per_frame;

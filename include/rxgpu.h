@@ -168,7 +168,7 @@ int rxg_classify(rxg_ctx *ctx, const uint8_t *pkts, const uint32_t *off, const u
  * netfamily.c:147.  Frames are gathered into the context's staging buffer. */
 int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
 
-/* Tuning hook: force the kernel variant (lanes per frame 4..64, passes
+/* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
  * loaded up front, frames per lane group); 0 = automatic from len_hint.
  * Unknown combinations make the next burst fail with RXG_EHIP. */
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group);

@@ -142,7 +142,7 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     frames = F.read_pcap(os.path.join(GOLD, "edge.pcap"))
     cfg = rxdist.gen_cfg("cfg4", n_udp=64, n_tcp=64)
     pk, off, ln = R.gen_host(cfg, 0, 700, 6)
-    frames = frames + [pk[i * 1536:i * 1536 + ln[i]].tobytes() for i in range(700)]
+    frames = frames + [pk[i * 1536:i * 1536 + int(ln[i])].tobytes() for i in range(700)]
     udp, tcb = R.gen_flows(cfg)
     udp = np.concatenate([fl["udp"], udp])
     tcb = np.concatenate([fl["tcb"], tcb])
