@@ -33,6 +33,7 @@ import torch  # noqa: E402
 import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
+COUNTS = True
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 
 
@@ -67,7 +68,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
             step_counts.zero_()
         if ev is not None:
             ev[0].record(stream)
-        ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, tgt, stream=sh)
+        ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out,
+                         tgt if COUNTS else None, stream=sh)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -100,7 +102,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     n_ok = int((rc == 0).sum().item())
     total_steps = warmup + steps
     counted = int(counts.sum().item())
-    expect = n_ok * total_steps if world == 1 else None
+    expect = n_ok * total_steps if (world == 1 and COUNTS) else None
     kavg = float(np.mean(kms))
     res = dict(
         workload=name, desc=w["desc"], n_per_gpu=n, nflows=nflows,
@@ -183,6 +185,8 @@ def main():
     ap.add_argument("--workload", default="cfg2,cfg3")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
+    ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
@@ -198,6 +202,10 @@ def main():
     torch.cuda.set_device(dev)
 
     ctx = R.Context(local)
+    global COUNTS
+    COUNTS = not a.no_counts
+    if a.variant:
+        ctx.tune(*[int(x) for x in a.variant.split(",")])
     if a.sweep:
         for nm in a.sweep.split(","):
             for var in R.KERNEL_VARIANTS:

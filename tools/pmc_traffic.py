@@ -34,7 +34,7 @@ def collect(workload, counter, outdir):
     vals = []
     for f in files:
         for row in csv.DictReader(open(f)):
-            if "rx_classify_kernel" in row.get("Kernel_Name", "") and \
+            if "rx_classify" in row.get("Kernel_Name", "") and \
                     row.get("Counter_Name") == counter:
                 vals.append(float(row["Counter_Value"]))
     return vals, files
