@@ -417,8 +417,186 @@ __device__ __forceinline__ uint32_t lane_chunk_sum(uint32_t acc, uint4 v, int32_
     return add_halves(acc, v.w);
 }
 
-template <int FPL>
-__global__ __launch_bounds__(256) void rx_classify_lane_kernel(
+// Per-lane frame state between the load and the verdict.
+struct lane_frame {
+    uint64_t p;
+    const uint8_t *fb;
+    int32_t cap;
+    bool valid;
+    uint4 c[4];
+};
+
+__device__ __forceinline__ void lane_desc(lane_frame &L, uint64_t p, uint32_t n,
+                                          const uint8_t *__restrict__ pkts,
+                                          const uint32_t *__restrict__ off,
+                                          const uint16_t *__restrict__ len, uint32_t unit_log2) {
+    L.p = p;
+    L.valid = p < n;
+    const uint64_t q = L.valid ? p : 0;
+    L.fb = pkts + ((uint64_t)off[q] << unit_log2);
+    L.cap = L.valid ? (int32_t)len[q] : 0;
+}
+
+__device__ __forceinline__ void lane_load(lane_frame &L) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        L.c[j] = make_uint4(0, 0, 0, 0);
+        if (16 * j < L.cap) L.c[j] = ldg16(L.fb + 16 * j);
+    }
+}
+
+// Parse + checksum + probe + verdict of one lane-owned frame.  `next` (may be
+// null) is the following trip's frame: its loads are issued here, after the
+// current frame's arithmetic and before the current frame's bucket probe, so
+// the bulk bytes of trip t+1 are in flight across the probe latency of trip t.
+__device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
+                                             const rx_ft_dev &ft, uint4 *__restrict__ out,
+                                             unsigned long long *__restrict__ counts,
+                                             uint32_t *hist, uint32_t lds_bins) {
+    const int32_t cp = L.cap;
+    if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.c[j] = chunk_below(L.c[j], 16 * j, cp);
+    }
+    const uint4 c0 = L.c[0], c1 = L.c[1], c2 = L.c[2], c3 = L.c[3];
+    const uint32_t et = c0.w & 0xFFFFu;
+    const uint32_t tl = rx_bswap16(c1.x & 0xFFFFu);
+    const uint32_t proto = c1.y >> 24;
+    const uint32_t sip = (c1.z >> 16) | (c1.w << 16);
+    const uint32_t dip = (c1.w >> 16) | (c2.x << 16);
+    const uint32_t sport = c2.x >> 16;
+    const uint32_t dport = c2.y & 0xFFFFu;
+    const uint32_t dgl = rx_bswap16(c2.y >> 16);
+    const uint32_t hl = ((c2.w >> 16) & 0xFFu) >> 4;
+
+    uint32_t cl, nd;
+    if (et == 0x0608u) {
+        cl = RXG_CLS_ARP;
+        nd = 42;
+    } else if (et != 0x0008u) {
+        cl = RXG_CLS_NON_IP;
+        nd = 14;
+    } else if (proto == 17u) {
+        cl = RXG_CLS_UDP;
+        nd = 42;
+    } else if (proto == 6u) {
+        cl = RXG_CLS_TCP;
+        nd = 54;
+    } else {
+        cl = RXG_CLS_IPV4_OTHER;
+        nd = 24;
+    }
+    const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+    const bool l4 = is_udp || is_tcp;
+    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+    const bool do_sum = l4 && tl >= 20u;
+    if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+
+    // checksum over [26, e), field at 40 (UDP) / 50 (TCP) read as 0
+    int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+    if (e > cp) e = cp;
+    uint4 h1 = c1, h2 = c2, h3 = c3;
+    h1.x = 0;
+    h1.y = 0;
+    h1.z &= 0xFFFF0000u;
+    if (is_udp) h2.z &= 0xFFFF0000u;
+    if (is_tcp) h3.x &= 0x0000FFFFu;
+    uint32_t acc = 0;
+    acc = lane_chunk_sum(acc, h1, 16, e);
+    acc = lane_chunk_sum(acc, h2, 32, e);
+    acc = lane_chunk_sum(acc, h3, 48, e);
+    for (int32_t s = 64; s < e; s += 64) { // longer frames: per-lane loop
+        uint4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            r[u] = make_uint4(0, 0, 0, 0);
+            if (s + 16 * u < e) r[u] = ldg16(L.fb + s + 16 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = lane_chunk_sum(acc, r[u], s + 16 * u, e);
+    }
+    uint32_t ck = 0;
+    if (do_sum) {
+        acc += proto << 8;
+        acc += rx_bswap16(l4n);
+        ck = (~fold16(acc)) & 0xFFFFu;
+        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+    }
+    const uint32_t stored = is_udp ? (c2.z & 0xFFFFu) : (is_tcp ? (c3.x >> 16) : 0u);
+    const bool ok = l4 && stored == ck;
+
+    if (next) lane_load(*next); // trip t+1 bytes in flight from here on
+
+    // flow probe: the whole 64-B bucket per lane
+    uint32_t flow = RXG_FLOW_NONE;
+    const bool probe = L.valid && (is_udp || (is_tcp && ok));
+    if (probe) {
+        const uint32_t ka = is_udp ? dip : sip;
+        const uint32_t kb = is_udp ? dport : dip;
+        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+        const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
+        const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
+        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        uint32_t b = rx_hash3(ka, kb, kc) & mask;
+        for (uint32_t pr = 0; pr < maxp; ++pr) {
+            bool done = false;
+#pragma unroll
+            for (int k = 0; k < RX_BUCKET_SLOTS; ++k) {
+                const uint4 sl = tbl[(b << 2) + k];
+                if (!done && sl.w == RX_SLOT_EMPTY) done = true;
+                if (!done && sl.x == ka && sl.y == kb && sl.z == kc) {
+                    flow = sl.w;
+                    done = true;
+                }
+            }
+            if (done) break;
+            b = (b + 1) & mask;
+        }
+        if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
+    }
+
+    int32_t rc;
+    uint32_t poff = 0, plen = 0, flags = 0;
+    if (is_udp) {
+        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                   : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        poff = 42;
+        plen = dgl > 8u ? dgl - 8u : 0u;
+        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+    } else if (is_tcp) {
+        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+        poff = 34u + 4u * hl;
+        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+        plen = pl < 0 ? 0u : (uint32_t)pl;
+        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+    } else {
+        rc = RXG_RC_KNI;
+    }
+    if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
+    if (L.valid) {
+        uint4 v;
+        v.x = flow;
+        v.y = (poff & 0xFFFFu) | (plen << 16);
+        v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+        v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+        stg16(&out[L.p], v);
+        if (counts && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) {
+            const uint32_t idx = (is_tcp ? ft.nu : 0u) + flow;
+            if (lds_bins)
+                atomicAdd(&hist[idx], 1u);
+            else
+                atomicAdd(&counts[idx], 1ull);
+        }
+    }
+}
+
+// PIPE = 0: load, process, repeat.  PIPE = 1: trip t+1's descriptors are
+// fetched at the top of trip t and its frame bytes are issued mid-trip.
+// PIPE = 2: as 1, register budget capped for 6 waves per SIMD.  PIPE = 3:
+// only the descriptors are prefetched (frame bytes loaded at the top).
+template <int PIPE>
+__global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
@@ -428,165 +606,59 @@ __global__ __launch_bounds__(256) void rx_classify_lane_kernel(
         for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
         __syncthreads();
     }
-    constexpr uint32_t TILE = 256 * FPL;
-    for (uint64_t tile = blockIdx.x; tile * TILE < n; tile += gridDim.x) {
-        uint64_t pf[FPL];
-        bool valid[FPL];
-        const uint8_t *fb[FPL];
-        int32_t cap[FPL];
-        uint4 c[FPL][4];
-#pragma unroll
-        for (int f = 0; f < FPL; ++f) {
-            pf[f] = tile * TILE + (uint64_t)f * 256 + tid;
-            valid[f] = pf[f] < n;
-            const uint64_t q = valid[f] ? pf[f] : 0;
-            fb[f] = pkts + ((uint64_t)off[q] << unit_log2);
-            cap[f] = valid[f] ? (int32_t)len[q] : 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
+    if constexpr (PIPE == 0) {
+        for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
+            lane_frame L;
+            lane_desc(L, p, n, pkts, off, len, unit_log2);
+            lane_load(L);
+            lane_process(L, nullptr, ft, out, counts, hist, lds_bins);
         }
-#pragma unroll
-        for (int f = 0; f < FPL; ++f)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                c[f][j] = make_uint4(0, 0, 0, 0);
-                if (16 * j < cap[f]) c[f][j] = ldg16(fb[f] + 16 * j);
-            }
-#pragma unroll
-        for (int f = 0; f < FPL; ++f) {
-            const int32_t cp = cap[f];
-            if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) c[f][j] = chunk_below(c[f][j], 16 * j, cp);
-            }
-            const uint4 c0 = c[f][0], c1 = c[f][1], c2 = c[f][2], c3 = c[f][3];
-            const uint32_t et = c0.w & 0xFFFFu;
-            const uint32_t tl = rx_bswap16(c1.x & 0xFFFFu);
-            const uint32_t proto = c1.y >> 24;
-            const uint32_t sip = (c1.z >> 16) | (c1.w << 16);
-            const uint32_t dip = (c1.w >> 16) | (c2.x << 16);
-            const uint32_t sport = c2.x >> 16;
-            const uint32_t dport = c2.y & 0xFFFFu;
-            const uint32_t dgl = rx_bswap16(c2.y >> 16);
-            const uint32_t hl = ((c2.w >> 16) & 0xFFu) >> 4;
-
-            uint32_t cl, nd;
-            if (et == 0x0608u) {
-                cl = RXG_CLS_ARP;
-                nd = 42;
-            } else if (et != 0x0008u) {
-                cl = RXG_CLS_NON_IP;
-                nd = 14;
-            } else if (proto == 17u) {
-                cl = RXG_CLS_UDP;
-                nd = 42;
-            } else if (proto == 6u) {
-                cl = RXG_CLS_TCP;
-                nd = 54;
-            } else {
-                cl = RXG_CLS_IPV4_OTHER;
-                nd = 24;
-            }
-            const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
-            const bool l4 = is_udp || is_tcp;
-            const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-            const bool do_sum = l4 && tl >= 20u;
-            if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-
-            // checksum over [26, e), field at 40 (UDP) / 50 (TCP) read as 0
-            int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
-            if (e > cp) e = cp;
-            uint4 h1 = c1, h2 = c2, h3 = c3;
-            h1.x = 0;
-            h1.y = 0;
-            h1.z &= 0xFFFF0000u;
-            if (is_udp) h2.z &= 0xFFFF0000u;
-            if (is_tcp) h3.x &= 0x0000FFFFu;
-            uint32_t acc = 0;
-            acc = lane_chunk_sum(acc, h1, 16, e);
-            acc = lane_chunk_sum(acc, h2, 32, e);
-            acc = lane_chunk_sum(acc, h3, 48, e);
-            for (int32_t s = 64; s < e; s += 64) { // longer frames: per-lane loop
-                uint4 r[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    r[u] = make_uint4(0, 0, 0, 0);
-                    if (s + 16 * u < e) r[u] = ldg16(fb[f] + s + 16 * u);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) acc = lane_chunk_sum(acc, r[u], s + 16 * u, e);
-            }
-            uint32_t ck = 0;
-            if (do_sum) {
-                acc += proto << 8;
-                acc += rx_bswap16(l4n);
-                ck = (~fold16(acc)) & 0xFFFFu;
-                if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-            }
-            const uint32_t stored = is_udp ? (c2.z & 0xFFFFu) : (is_tcp ? (c3.x >> 16) : 0u);
-            const bool ok = l4 && stored == ck;
-
-            // flow probe: the whole 64-B bucket per lane
-            uint32_t flow = RXG_FLOW_NONE;
-            const bool probe = valid[f] && (is_udp || (is_tcp && ok));
-            if (probe) {
-                const uint32_t ka = is_udp ? dip : sip;
-                const uint32_t kb = is_udp ? dport : dip;
-                const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-                const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
-                const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
-                const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-                uint32_t b = rx_hash3(ka, kb, kc) & mask;
-                for (uint32_t pr = 0; pr < maxp; ++pr) {
-                    bool done = false;
-#pragma unroll
-                    for (int k = 0; k < RX_BUCKET_SLOTS; ++k) {
-                        const uint4 sl = tbl[(b << 2) + k];
-                        if (!done && sl.w == RX_SLOT_EMPTY) done = true;
-                        if (!done && sl.x == ka && sl.y == kb && sl.z == kc) {
-                            flow = sl.w;
-                            done = true;
-                        }
-                    }
-                    if (done) break;
-                    b = (b + 1) & mask;
-                }
-                if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
-            }
-
-            int32_t rc;
-            uint32_t poff = 0, plen = 0, flags = 0;
-            if (is_udp) {
-                rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                           : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-                poff = 42;
-                plen = dgl > 8u ? dgl - 8u : 0u;
-                if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-                if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
-            } else if (is_tcp) {
-                const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-                poff = 34u + 4u * hl;
-                if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-                plen = pl < 0 ? 0u : (uint32_t)pl;
-                rc = !ok ? RXG_RC_TCP_BAD_CKSUM
-                         : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-            } else {
-                rc = RXG_RC_KNI;
-            }
-            if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
-            if (valid[f]) {
-                uint4 v;
-                v.x = flow;
-                v.y = (poff & 0xFFFFu) | (plen << 16);
-                v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-                v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-                stg16(&out[pf[f]], v);
-                if (counts && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) {
-                    const uint32_t idx = (is_tcp ? ft.nu : 0u) + flow;
-                    if (lds_bins)
-                        atomicAdd(&hist[idx], 1u);
-                    else
-                        atomicAdd(&counts[idx], 1ull);
-                }
-            }
+    } else if constexpr (PIPE == 3) {
+        lane_frame L;
+        uint64_t base = (uint64_t)blockIdx.x * 256;
+        uint64_t nq = 0;
+        const uint8_t *nfb = pkts;
+        int32_t ncap = 0;
+        if (base < n) {
+            lane_desc(L, p, n, pkts, off, len, unit_log2);
+            nfb = L.fb;
+            ncap = L.cap;
+        }
+        for (; base < n; base += stride, p += stride) {
+            L.p = p;
+            L.valid = p < n;
+            L.fb = nfb;
+            L.cap = ncap;
+            lane_load(L);
+            nq = p + stride; // descriptors of the next trip, in flight during this one
+            const uint64_t q = nq < n ? nq : 0;
+            nfb = pkts + ((uint64_t)off[q] << unit_log2);
+            ncap = nq < n ? (int32_t)len[q] : 0;
+            lane_process(L, nullptr, ft, out, counts, hist, lds_bins);
+        }
+    } else {
+        lane_frame A, B;
+        uint64_t base = (uint64_t)blockIdx.x * 256;
+        if (base < n) {
+            lane_desc(A, p, n, pkts, off, len, unit_log2);
+            lane_load(A);
+        }
+        // two frames alternate roles; the loop body is unrolled twice so that
+        // A and B stay in fixed registers
+        while (base < n) {
+            uint64_t nb = base + stride;
+            lane_desc(B, p + stride, n, pkts, off, len, unit_log2);
+            lane_process(A, nb < n ? &B : nullptr, ft, out, counts, hist, lds_bins);
+            base = nb;
+            p += stride;
+            if (base >= n) break;
+            nb = base + stride;
+            lane_desc(A, p + stride, n, pkts, off, len, unit_log2);
+            lane_process(B, nb < n ? &A : nullptr, ft, out, counts, hist, lds_bins);
+            base = nb;
+            p += stride;
         }
     }
     if (lds_bins) {
@@ -598,7 +670,7 @@ __global__ __launch_bounds__(256) void rx_classify_lane_kernel(
     }
 }
 
-template <int FPL>
+template <int PIPE>
 hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s) {
@@ -617,16 +689,16 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<FPL>), 256, lds);
+            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE>), 256, lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
     }
-    const uint64_t tiles = ((uint64_t)n + 256 * FPL - 1) / (256 * FPL);
+    const uint64_t tiles = ((uint64_t)n + 255) / 256;
     uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_lane_kernel<FPL>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
@@ -640,7 +712,8 @@ struct variant_entry {
 };
 // every compiled variant; the first entry per G is its default
 static const variant_entry k_variants[] = {
-    {1, 4, 1, launch_lane<1>},      {1, 4, 2, launch_lane<2>},
+    {1, 1, 1, launch_lane<1>},      {1, 0, 1, launch_lane<0>},      {1, 2, 1, launch_lane<2>},
+    {1, 3, 1, launch_lane<3>},
     {4, 1, 2, launch_v<4, 1, 2>},   {4, 1, 1, launch_v<4, 1, 1>},   {4, 1, 4, launch_v<4, 1, 4>},
     {8, 2, 2, launch_v<8, 2, 2>},   {8, 2, 1, launch_v<8, 2, 1>},   {16, 2, 2, launch_v<16, 2, 2>},
     {16, 2, 1, launch_v<16, 2, 1>}, {32, 3, 2, launch_v<32, 3, 2>}, {32, 3, 1, launch_v<32, 3, 1>},

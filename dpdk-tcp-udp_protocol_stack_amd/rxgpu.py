@@ -43,8 +43,9 @@ RC_OK, RC_TCP_BAD_CKSUM, RC_TCP_NO_TCB, RC_UDP_NOMEM, RC_UDP_NO_SOCKET, RC_KNI =
 F_TRUNC, F_TCP_NEGLEN, F_UDP_SHORT = 0x1, 0x2, 0x4
 TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
 HOST_ONLY = -1
-# (lanes per frame, passes up front, frames per group) compiled in rx_classify.hip
-KERNEL_VARIANTS = [(1, 4, 1), (1, 4, 2), (4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
+# (lanes per frame, passes up front, frames per group) compiled in rx_classify.hip;
+# for lanes per frame = 1 the second field is the prefetch depth (0 or 1 trip)
+KERNEL_VARIANTS = [(1, 1, 1), (1, 0, 1), (1, 2, 1), (1, 3, 1), (4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
                    (32, 3, 2), (32, 3, 1), (32, 2, 1), (64, 4, 1), (64, 2, 1)]
 
 VERDICT_DTYPE = np.dtype([
