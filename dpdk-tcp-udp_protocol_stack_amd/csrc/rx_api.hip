@@ -39,47 +39,37 @@ struct ft_host {
     std::vector<uint4> slots;
     uint32_t mask = 0, probe = 1;
 
-    void build(const std::vector<uint4> &entries /* x,y,z key; w value; creation order */) {
+    // entries: x,y,z = key, w = value, in creation order (newest wins)
+    void build(const std::vector<uint4> &entries) {
         const uint64_t n = entries.size();
-        uint64_t nb = 1;
-        while (nb * RX_BUCKET_SLOTS < 2 * n) nb <<= 1; // load factor <= 1/2: always an empty slot
-        slots.assign(nb * RX_BUCKET_SLOTS, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
-        mask = (uint32_t)(nb - 1);
+        uint64_t ns = 16;
+        while (ns < 4 * n) ns <<= 1; // load factor <= 1/4: always an empty slot
+        slots.assign(ns, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
+        mask = (uint32_t)(ns - 1);
         probe = 1;
         for (const uint4 &e : entries) {
-            uint32_t b = rx_hash3(e.x, e.y, e.z) & mask;
-            for (uint32_t d = 0;; ++d, b = (b + 1) & mask) {
-                bool placed = false;
-                for (uint32_t s = 0; s < RX_BUCKET_SLOTS && !placed; ++s) {
-                    uint4 &sl = slots[(uint64_t)b * RX_BUCKET_SLOTS + s];
-                    if (sl.w == RX_SLOT_EMPTY) {
-                        sl = e;
-                        placed = true;
-                    } else if (sl.x == e.x && sl.y == e.y && sl.z == e.z) {
-                        sl.w = e.w; // a newer control block with the same key wins
-                        placed = true;
-                    }
+            uint32_t i = rx_hash3(e.x, e.y, e.z) & mask;
+            for (uint32_t d = 0;; ++d, i = (i + 1) & mask) {
+                uint4 &sl = slots[i];
+                if (sl.w == RX_SLOT_EMPTY) {
+                    sl = e;
+                } else if (sl.x == e.x && sl.y == e.y && sl.z == e.z) {
+                    sl.w = e.w; // a newer control block with the same key wins
+                } else {
+                    continue;
                 }
-                if (placed) {
-                    probe = std::max(probe, d + 1);
-                    break;
-                }
+                probe = std::max(probe, d + 1);
+                break;
             }
         }
     }
 
-    uint32_t lookup(uint32_t a, uint32_t b_, uint32_t c) const {
-        uint32_t b = rx_hash3(a, b_, c) & mask;
-        for (uint32_t d = 0; d < probe; ++d, b = (b + 1) & mask) {
-            bool empty = false;
-            for (uint32_t s = 0; s < RX_BUCKET_SLOTS; ++s) {
-                const uint4 &sl = slots[(uint64_t)b * RX_BUCKET_SLOTS + s];
-                if (sl.w == RX_SLOT_EMPTY)
-                    empty = true;
-                else if (sl.x == a && sl.y == b_ && sl.z == c)
-                    return sl.w;
-            }
-            if (empty) break;
+    uint32_t lookup(uint32_t a, uint32_t b, uint32_t c) const {
+        uint32_t i = rx_hash3(a, b, c) & mask;
+        for (uint32_t d = 0; d < probe; ++d, i = (i + 1) & mask) {
+            const uint4 &sl = slots[i];
+            if (sl.w == RX_SLOT_EMPTY) break;
+            if (sl.x == a && sl.y == b && sl.z == c) return sl.w;
         }
         return RXG_FLOW_NONE;
     }

@@ -272,17 +272,19 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
             kc[f] = is_udp ? 17u : (sport | (dport[f] << 16));
         }
 
-        // ---- phase D: flow probes (first bucket of every frame in flight)
-        uint32_t flow[FPG], bkt[FPG];
+        // ---- phase D: flow probes, a 4-slot window per lane group, the first
+        // window of every frame in flight
+        uint32_t flow[FPG], slot[FPG];
         uint4 sl[FPG];
         bool probe[FPG];
 #pragma unroll
         for (int f = 0; f < FPG; ++f) {
             probe[f] = valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
             const bool udp = cls[f] == RXG_CLS_UDP;
-            bkt[f] = rx_hash3(ka[f], kb[f], kc[f]) & (udp ? ft.udp_mask : ft.tcp_mask);
+            const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
+            slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
             sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-            if (probe[f] && gl < RX_BUCKET_SLOTS) sl[f] = (udp ? ft.udp : ft.tcp)[(bkt[f] << 2) + gl];
+            if (probe[f] && gl < RX_WINDOW) sl[f] = (udp ? ft.udp : ft.tcp)[(slot[f] + gl) & mask];
             flow[f] = RXG_FLOW_NONE;
         }
 #pragma unroll
@@ -292,25 +294,24 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
             const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
             const uint32_t maxp = udp ? ft.udp_probe : ft.tcp_probe;
             uint4 s = sl[f];
-            uint32_t b = bkt[f];
-            for (uint32_t pr = 0; pr < maxp; ++pr) { // trips are group-uniform
-                const bool hit = probe[f] && gl < RX_BUCKET_SLOTS && s.w != RX_SLOT_EMPTY &&
+            uint32_t b = slot[f];
+            for (uint32_t pr = 0; pr < maxp; pr += RX_WINDOW) { // trips are group-uniform
+                const bool hit = probe[f] && gl < RX_WINDOW && s.w != RX_SLOT_EMPTY &&
                                  s.x == ka[f] && s.y == kb[f] && s.z == kc[f];
-                const bool emp = probe[f] && gl < RX_BUCKET_SLOTS && s.w == RX_SLOT_EMPTY;
-                const uint64_t hm = __ballot(hit), em = __ballot(emp);
-                const uint32_t gh = (uint32_t)(hm >> gbase) & 0xFu;
-                const uint32_t ge = (uint32_t)(em >> gbase) & 0xFu;
-                const uint32_t lanesrc = gbase + (gh ? (uint32_t)(__ffs(gh) - 1) : 0u);
-                const uint32_t v = __shfl(s.w, lanesrc);
+                const bool emp = probe[f] && gl < RX_WINDOW && s.w == RX_SLOT_EMPTY;
+                const uint32_t gh = (uint32_t)(__ballot(hit) >> gbase) & 0xFu;
+                const uint32_t ge = (uint32_t)(__ballot(emp) >> gbase) & 0xFu;
+                // linear probing: the first hit-or-empty slot of the window decides
+                const uint32_t first = (uint32_t)__ffs(gh | ge) - 1u; // 31 if neither (ffs 0)
+                const uint32_t v = __shfl(s.w, gbase + (first & 3u));
                 if (!probe[f]) break; // probe[f], gh, ge are uniform across the group
-                if (gh) {
-                    flow[f] = v;
+                if ((gh | ge) != 0u) {
+                    if (gh & (1u << first)) flow[f] = v;
                     break;
                 }
-                if (ge) break;
-                b = (b + 1) & mask;
+                b = (b + RX_WINDOW) & mask;
                 s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-                if (gl < RX_BUCKET_SLOTS) s = tbl[(b << 2) + gl];
+                if (gl < RX_WINDOW) s = tbl[(b + gl) & mask];
             }
             if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
                 flow[f] = ft.listen[dport[f]];
@@ -449,6 +450,9 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 // null) is the following trip's frame: its loads are issued here, after the
 // current frame's arithmetic and before the current frame's bucket probe, so
 // the bulk bytes of trip t+1 are in flight across the probe latency of trip t.
+// ABL (diagnostic builds only, never selected automatically): 1 = no bucket
+// probe, 4 = no verdict store, 8 = no checksum arithmetic.
+template <int ABL = 0, bool ST_NT = true>
 __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
                                              const rx_ft_dev &ft, uint4 *__restrict__ out,
                                              unsigned long long *__restrict__ counts,
@@ -502,10 +506,12 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
     if (is_udp) h2.z &= 0xFFFF0000u;
     if (is_tcp) h3.x &= 0x0000FFFFu;
     uint32_t acc = 0;
+    if (!(ABL & 8)) {
     acc = lane_chunk_sum(acc, h1, 16, e);
     acc = lane_chunk_sum(acc, h2, 32, e);
     acc = lane_chunk_sum(acc, h3, 48, e);
-    for (int32_t s = 64; s < e; s += 64) { // longer frames: per-lane loop
+    }
+    for (int32_t s = 64; s < e && !(ABL & 8); s += 64) { // longer frames: per-lane loop
         uint4 r[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -530,27 +536,23 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
     // flow probe: the whole 64-B bucket per lane
     uint32_t flow = RXG_FLOW_NONE;
     const bool probe = L.valid && (is_udp || (is_tcp && ok));
-    if (probe) {
+    if (ABL & 1) {
+        flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+    } else if (probe) {
         const uint32_t ka = is_udp ? dip : sip;
         const uint32_t kb = is_udp ? dport : dip;
         const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
         const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
         const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
         const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-        uint32_t b = rx_hash3(ka, kb, kc) & mask;
-        for (uint32_t pr = 0; pr < maxp; ++pr) {
-            bool done = false;
-#pragma unroll
-            for (int k = 0; k < RX_BUCKET_SLOTS; ++k) {
-                const uint4 sl = tbl[(b << 2) + k];
-                if (!done && sl.w == RX_SLOT_EMPTY) done = true;
-                if (!done && sl.x == ka && sl.y == kb && sl.z == kc) {
-                    flow = sl.w;
-                    done = true;
-                }
+        uint32_t i = rx_hash3(ka, kb, kc) & mask;
+        for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) { // ~1.2 trips expected
+            const uint4 sl = tbl[i];
+            if (sl.w == RX_SLOT_EMPTY) break;
+            if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                flow = sl.w;
+                break;
             }
-            if (done) break;
-            b = (b + 1) & mask;
         }
         if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
     }
@@ -580,7 +582,12 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         v.y = (poff & 0xFFFFu) | (plen << 16);
         v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-        stg16(&out[L.p], v);
+        if (ABL & 4)
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+        else if (ST_NT)
+            stg16(&out[L.p], v);
+        else
+            out[L.p] = v;
         if (counts && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) {
             const uint32_t idx = (is_tcp ? ft.nu : 0u) + flow;
             if (lds_bins)
@@ -595,7 +602,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
 // fetched at the top of trip t and its frame bytes are issued mid-trip.
 // PIPE = 2: as 1, register budget capped for 6 waves per SIMD.  PIPE = 3:
 // only the descriptors are prefetched (frame bytes loaded at the top).
-template <int PIPE>
+template <int PIPE, int ABL = 0, bool ST_NT = true>
 __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -613,7 +620,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2);
             lane_load(L);
-            lane_process(L, nullptr, ft, out, counts, hist, lds_bins);
+            lane_process<ABL, ST_NT>(L, nullptr, ft, out, counts, hist, lds_bins);
         }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
@@ -670,7 +677,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     }
 }
 
-template <int PIPE>
+template <int PIPE, int ABL = 0, bool ST_NT = true>
 hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s) {
@@ -689,7 +696,8 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE>), 256, lds);
+            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT>), 256,
+            lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
@@ -698,7 +706,7 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
@@ -713,7 +721,10 @@ struct variant_entry {
 // every compiled variant; the first entry per G is its default
 static const variant_entry k_variants[] = {
     {1, 1, 1, launch_lane<1>},      {1, 0, 1, launch_lane<0>},      {1, 2, 1, launch_lane<2>},
-    {1, 3, 1, launch_lane<3>},
+    {1, 3, 1, launch_lane<3>},      {1, 4, 1, launch_lane<0, 0, false>},
+    // diagnostic ablations (wrong verdicts by construction; tuning only)
+    {1, 101, 1, launch_lane<0, 1>}, {1, 104, 1, launch_lane<0, 4>}, {1, 108, 1, launch_lane<0, 8>},
+    {1, 113, 1, launch_lane<0, 13>},
     {4, 1, 2, launch_v<4, 1, 2>},   {4, 1, 1, launch_v<4, 1, 1>},   {4, 1, 4, launch_v<4, 1, 4>},
     {8, 2, 2, launch_v<8, 2, 2>},   {8, 2, 1, launch_v<8, 2, 1>},   {16, 2, 2, launch_v<16, 2, 2>},
     {16, 2, 1, launch_v<16, 2, 1>}, {32, 3, 2, launch_v<32, 3, 2>}, {32, 3, 1, launch_v<32, 3, 1>},

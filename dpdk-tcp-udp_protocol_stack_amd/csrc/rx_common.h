@@ -11,24 +11,25 @@
 #define RX_HD __host__ __device__ __forceinline__
 
 // ---------------------------------------------------------------------------
-// Flow table (device image).  Exact-key tables are bucketised open addressing:
-// one bucket = 4 slots x 16 B = one 64-B line, probed by 4 lanes of a frame's
-// lane group in a single coalesced load + ballot.  Slot = {a, b, c, flow};
-// flow == RX_SLOT_EMPTY marks a free slot.  Keys are the raw network-order
-// values the reference compares (common.c:101-103, 36-38):
+// Flow table (device image).  Exact-key tables use linear probing over 16-B
+// slots {a, b, c, flow} at a load factor <= 1/4 (expected ~1.2 slot reads per
+// lookup); flow == RX_SLOT_EMPTY marks a free slot.  A one-frame-per-lane
+// kernel reads slots one by one; a lane group reads a window of 4 consecutive
+// slots (one 64-B access) and __ballots the compare.  Keys are the raw
+// network-order values the reference compares (common.c:101-103, 36-38):
 //   UDP:  a = dst ip, b = dst port, c = 17           (get_hostinfo_fromip_port)
 //   TCP:  a = src ip, b = dst ip, c = sport | dport<<16   (tcp_stream_search pass 1)
 // Listeners (tcp_stream_search pass 2: dport + LISTEN, dst ip ignored) are a
 // direct u32[65536] table indexed by the raw dport.
 #define RX_SLOT_EMPTY 0xFFFFFFFFu
-#define RX_BUCKET_SLOTS 4
+#define RX_WINDOW 4
 
 struct rx_ft_dev {
-    const uint4 *udp;   // (udp_mask + 1) * 4 slots
-    const uint4 *tcp;   // (tcp_mask + 1) * 4 slots
+    const uint4 *udp;   // udp_mask + 1 slots
+    const uint4 *tcp;   // tcp_mask + 1 slots
     const uint32_t *listen; // 65536 entries
-    uint32_t udp_mask, tcp_mask;
-    uint32_t udp_probe, tcp_probe; // max buckets any present key needed
+    uint32_t udp_mask, tcp_mask;   // slots - 1 (power of two)
+    uint32_t udp_probe, tcp_probe; // longest probe sequence (slots) of any present key
     uint32_t nu, nt;
 };
 

@@ -45,7 +45,7 @@ TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
 HOST_ONLY = -1
 # (lanes per frame, passes up front, frames per group) compiled in rx_classify.hip;
 # for lanes per frame = 1 the second field is the prefetch depth (0 or 1 trip)
-KERNEL_VARIANTS = [(1, 1, 1), (1, 0, 1), (1, 2, 1), (1, 3, 1), (4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
+KERNEL_VARIANTS = [(1, 1, 1), (1, 0, 1), (1, 2, 1), (1, 3, 1), (1, 4, 1), (4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
                    (32, 3, 2), (32, 3, 1), (32, 2, 1), (64, 4, 1), (64, 2, 1)]
 
 VERDICT_DTYPE = np.dtype([
