@@ -16,8 +16,8 @@
 uint32_t rx_pick_group(uint32_t len_hint);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
-                              const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
-                              hipStream_t s);
+                              uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
+                              unsigned long long *counts, hipStream_t s);
 
 static thread_local std::string g_last_hip;
 
@@ -85,7 +85,7 @@ struct rxg_ctx {
     size_t d_udp_cap = 0, d_tcp_cap = 0;
     uint32_t *d_listen = nullptr;
     rx_ft_dev ft{};
-    uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0; // rxg_tune override (0 = auto)
+    uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
     uint32_t counts_cap = 0;
@@ -263,7 +263,8 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
     return RXG_OK;
 }
 
-int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group) {
+int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
+             uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
     if (lanes_per_frame && (lanes_per_frame == 2 || lanes_per_frame > 64 ||
                             (lanes_per_frame & (lanes_per_frame - 1))))
@@ -271,6 +272,7 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
     c->tune_g = lanes_per_frame;
     c->tune_p = lanes_per_frame ? passes : 0;
     c->tune_fpg = lanes_per_frame ? frames_per_group : 0;
+    c->tune_pipe = lanes_per_frame ? pipeline : ~0u;
     return RXG_OK;
 }
 
@@ -303,7 +305,7 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     HIPCHK(hipSetDevice(c->device));
     const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group(len_hint);
     HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, c->tune_p, c->tune_fpg,
-                              c->ft, reinterpret_cast<uint4 *>(d_out),
+                              c->tune_pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
                               reinterpret_cast<unsigned long long *>(d_counts),
                               (hipStream_t)stream));
     return RXG_OK;
@@ -331,7 +333,7 @@ int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uin
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
     const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group((uint32_t)(sumlen / n));
     HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, c->tune_p,
-                              c->tune_fpg, c->ft, c->d_out, c->d_counts, c->stream));
+                              c->tune_fpg, c->tune_pipe, c->ft, c->d_out, c->d_counts, c->stream));
     HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;

@@ -109,7 +109,257 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
     return s;
 }
 
+// Frames of one lane group for one trip: descriptors and the first P passes.
+template <int FPG, int P>
+struct group_frames {
+    uint64_t pf[FPG];
+    bool valid[FPG];
+    const uint8_t *fb[FPG];
+    int32_t cap[FPG];
+    uint4 c[FPG][P];
+};
+
+template <int G, int FPG, int P>
+__device__ __forceinline__ void group_desc(group_frames<FPG, P> &S, uint64_t tile, uint32_t n,
+                                           uint32_t grp, const uint8_t *__restrict__ pkts,
+                                           const uint32_t *__restrict__ off,
+                                           const uint16_t *__restrict__ len, uint32_t unit_log2) {
+    constexpr uint32_t GPB = 256 / G;
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        S.pf[f] = tile * (GPB * FPG) + (uint64_t)f * GPB + grp;
+        S.valid[f] = S.pf[f] < n;
+        const uint64_t q = S.valid[f] ? S.pf[f] : 0;
+        S.fb[f] = pkts + ((uint64_t)off[q] << unit_log2);
+        S.cap[f] = S.valid[f] ? (int32_t)len[q] : 0;
+    }
+}
+
+template <int G, int FPG, int P>
+__device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) {
+#pragma unroll
+    for (int f = 0; f < FPG; ++f)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const int32_t s = s0 + q * 16 * G;
+            S.c[f][q] = make_uint4(0, 0, 0, 0);
+            if (s < S.cap[f]) S.c[f][q] = ldg16(S.fb[f] + s);
+        }
+}
+
+// parse + checksum + probe + verdict for the FPG frames of S
 template <int G, int P, int FPG>
+__device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t gl, uint32_t gbase,
+                                              int32_t s0, const rx_ft_dev &ft,
+                                              uint4 *__restrict__ out,
+                                              unsigned long long *__restrict__ counts,
+                                              uint32_t *hist, uint32_t lds_bins) {
+    constexpr int32_t STEP = 16 * G;
+    // ---- phase C: parse + checksum per frame
+    uint32_t cls[FPG], ck[FPG], stored[FPG], tl[FPG], dgl[FPG], hl[FPG], need[FPG];
+    uint32_t ka[FPG], kb[FPG], kc[FPG], dport[FPG];
+    bool ok[FPG];
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        const int32_t cp = S.cap[f];
+        uint4 x0 = S.c[f][0];
+        if (s0 < cp && s0 + 16 > cp) x0 = chunk_below(x0, s0, cp); // bytes past caplen read 0
+        const uint32_t h03 = gbcast<G, 0>(x0.w); // bytes 12..15
+        const uint32_t h10 = gbcast<G, 1>(x0.x); // 16..19
+        const uint32_t h11 = gbcast<G, 1>(x0.y); // 20..23
+        const uint32_t h12 = gbcast<G, 1>(x0.z); // 24..27
+        const uint32_t h13 = gbcast<G, 1>(x0.w); // 28..31
+        const uint32_t h20 = gbcast<G, 2>(x0.x); // 32..35
+        const uint32_t h21 = gbcast<G, 2>(x0.y); // 36..39
+        const uint32_t h22 = gbcast<G, 2>(x0.z); // 40..43
+        const uint32_t h23 = gbcast<G, 2>(x0.w); // 44..47
+        const uint32_t h30 = gbcast<G, 3>(x0.x); // 48..51
+
+        const uint32_t et = h03 & 0xFFFFu; // LE view of bytes 12,13
+        tl[f] = rx_bswap16(h10 & 0xFFFFu);
+        const uint32_t proto = h11 >> 24;
+        const uint32_t sip = (h12 >> 16) | (h13 << 16);
+        const uint32_t dip = (h13 >> 16) | (h20 << 16);
+        const uint32_t sport = h20 >> 16;
+        dport[f] = h21 & 0xFFFFu;
+        dgl[f] = rx_bswap16(h21 >> 16);
+        hl[f] = ((h23 >> 16) & 0xFFu) >> 4;
+
+        uint32_t cl, nd;
+        if (et == 0x0608u) {
+            cl = RXG_CLS_ARP;
+            nd = 42;
+        } else if (et != 0x0008u) {
+            cl = RXG_CLS_NON_IP;
+            nd = 14;
+        } else if (proto == 17u) {
+            cl = RXG_CLS_UDP;
+            nd = 42;
+        } else if (proto == 6u) {
+            cl = RXG_CLS_TCP;
+            nd = 54;
+        } else {
+            cl = RXG_CLS_IPV4_OTHER;
+            nd = 24;
+        }
+        const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+        const bool l4 = is_udp || is_tcp;
+        const uint32_t l4n = tl[f] >= 20u ? tl[f] - 20u : 0u;
+        const bool do_sum = l4 && tl[f] >= 20u;
+        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+        cls[f] = cl;
+        need[f] = nd;
+
+        // checksum region [26, e): e = min(34 + l4n, caplen)
+        int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+        if (e > cp) e = cp;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const int32_t s = s0 + q * STEP;
+            uint4 v = S.c[f][q];
+            if (s + 16 > e) v = chunk_below(v, s, e);
+            if (q == 0) { // header bytes [0,26) and the checksum field are not summed
+                if (gl == 0) v = make_uint4(0, 0, 0, 0);
+                if (gl == 1) {
+                    v.x = 0;
+                    v.y = 0;
+                    v.z &= 0xFFFF0000u;
+                }
+                if (gl == 2 && is_udp) v.z &= 0xFFFF0000u; // UDP cksum at 40..41
+                if (gl == 3 && is_tcp) v.x &= 0x0000FFFFu; // TCP cksum at 50..51
+            }
+            acc = add_halves(acc, v.x);
+            acc = add_halves(acc, v.y);
+            acc = add_halves(acc, v.z);
+            acc = add_halves(acc, v.w);
+        }
+        // frames longer than P passes: the rest in batches of 4 passes
+        for (int32_t sb = P * STEP; sb < e; sb += 4 * STEP) { // group-uniform
+            uint4 r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t s = s0 + sb + u * STEP;
+                r[u] = make_uint4(0, 0, 0, 0);
+                if (s < e) r[u] = ldg16(S.fb[f] + s);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t s = s0 + sb + u * STEP;
+                uint4 v = r[u];
+                if (s + 16 > e) v = chunk_below(v, s, e);
+                acc = add_halves(acc, v.x);
+                acc = add_halves(acc, v.y);
+                acc = add_halves(acc, v.z);
+                acc = add_halves(acc, v.w);
+            }
+        }
+        uint32_t sum = gsum<G>(acc);
+        uint32_t k = 0;
+        if (do_sum) {
+            sum += proto << 8;       // psd {zero, proto}
+            sum += rx_bswap16(l4n);  // psd be16(l4_len)
+            k = (~fold16(sum)) & 0xFFFFu;
+            if (k == 0u && proto == 17u) k = 0xFFFFu;
+        }
+        ck[f] = k;
+        stored[f] = is_udp ? (h22 & 0xFFFFu) : (is_tcp ? (h30 >> 16) : 0u);
+        ok[f] = l4 && stored[f] == k;
+        ka[f] = is_udp ? dip : sip;
+        kb[f] = is_udp ? dport[f] : dip;
+        kc[f] = is_udp ? 17u : (sport | (dport[f] << 16));
+    }
+
+    // ---- phase D: flow probes, a 4-slot window per lane group, the first
+    // window of every frame in flight
+    uint32_t flow[FPG], slot[FPG];
+    uint4 sl[FPG];
+    bool probe[FPG];
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        probe[f] = S.valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
+        const bool udp = cls[f] == RXG_CLS_UDP;
+        const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
+        slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
+        sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
+        if (probe[f] && gl < RX_WINDOW) sl[f] = (udp ? ft.udp : ft.tcp)[(slot[f] + gl) & mask];
+        flow[f] = RXG_FLOW_NONE;
+    }
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        const bool udp = cls[f] == RXG_CLS_UDP;
+        const uint4 *tbl = udp ? ft.udp : ft.tcp;
+        const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
+        const uint32_t maxp = udp ? ft.udp_probe : ft.tcp_probe;
+        uint4 s = sl[f];
+        uint32_t b = slot[f];
+        for (uint32_t pr = 0; pr < maxp; pr += RX_WINDOW) { // trips are group-uniform
+            const bool hit = probe[f] && gl < RX_WINDOW && s.w != RX_SLOT_EMPTY &&
+                             s.x == ka[f] && s.y == kb[f] && s.z == kc[f];
+            const bool emp = probe[f] && gl < RX_WINDOW && s.w == RX_SLOT_EMPTY;
+            const uint32_t gh = (uint32_t)(__ballot(hit) >> gbase) & 0xFu;
+            const uint32_t ge = (uint32_t)(__ballot(emp) >> gbase) & 0xFu;
+            // linear probing: the first hit-or-empty slot of the window decides
+            const uint32_t first = (uint32_t)__ffs(gh | ge) - 1u; // 31 if neither (ffs 0)
+            const uint32_t v = __shfl(s.w, gbase + (first & 3u));
+            if (!probe[f]) break; // probe[f], gh, ge are uniform across the group
+            if ((gh | ge) != 0u) {
+                if (gh & (1u << first)) flow[f] = v;
+                break;
+            }
+            b = (b + RX_WINDOW) & mask;
+            s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
+            if (gl < RX_WINDOW) s = tbl[(b + gl) & mask];
+        }
+        if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
+            flow[f] = ft.listen[dport[f]];
+    }
+
+    // ---- phase E: verdicts (reference return codes) + counts
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        int32_t rc;
+        uint32_t poff = 0, plen = 0, flags = 0, nd = need[f];
+        if (cls[f] == RXG_CLS_UDP) {
+            rc = flow[f] == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                          : (dgl[f] <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+            poff = 42;
+            plen = dgl[f] > 8u ? dgl[f] - 8u : 0u;
+            if (dgl[f] <= 8u) flags |= RXG_F_UDP_SHORT;
+            if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+        } else if (cls[f] == RXG_CLS_TCP) {
+            const int32_t pl = (int32_t)tl[f] - 20 - 4 * (int32_t)hl[f];
+            poff = 34u + 4u * hl[f];
+            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+            plen = pl < 0 ? 0u : (uint32_t)pl;
+            rc = !ok[f] ? RXG_RC_TCP_BAD_CKSUM
+                        : (flow[f] == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+        } else {
+            rc = RXG_RC_KNI;
+        }
+        if ((int32_t)nd > S.cap[f]) flags |= RXG_F_TRUNC;
+        if (gl == 0 && S.valid[f]) {
+            uint4 v;
+            v.x = flow[f];
+            v.y = (poff & 0xFFFFu) | (plen << 16);
+            v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
+            v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
+            stg16(&out[S.pf[f]], v);
+            if (counts && rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE) {
+                const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
+                if (lds_bins)
+                    atomicAdd(&hist[idx], 1u);
+                else
+                    atomicAdd(&counts[idx], 1ull);
+            }
+        }
+    }
+}
+
+// PIPE = 1: trip t+1's descriptors are fetched one trip ahead and its frame
+// bytes are issued before trip t is processed (one extra frame set of
+// registers), so both HBM round trips overlap the previous trip's work.
+template <int G, int P, int FPG, int PIPE>
 __global__ __launch_bounds__(256) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -118,7 +368,6 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
     constexpr uint32_t GPB = 256 / G;     // frame groups per block
     constexpr uint32_t TILE = GPB * FPG;  // frames per block per trip
-    constexpr int32_t STEP = 16 * G;      // bytes one group pass covers
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -132,229 +381,26 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
         __syncthreads();
     }
 
-    for (uint64_t tile = blockIdx.x; tile * TILE < n; tile += gridDim.x) {
-        // ---- phase A: descriptors of the FPG frames
-        uint64_t pf[FPG];
-        bool valid[FPG];
-        const uint8_t *fb[FPG];
-        int32_t cap[FPG];
-#pragma unroll
-        for (int f = 0; f < FPG; ++f) {
-            pf[f] = tile * TILE + (uint64_t)f * GPB + grp;
-            valid[f] = pf[f] < n;
-            const uint64_t q = valid[f] ? pf[f] : 0;
-            fb[f] = pkts + ((uint64_t)off[q] << unit_log2);
-            cap[f] = valid[f] ? (int32_t)len[q] : 0;
+    uint64_t tile = blockIdx.x;
+    group_frames<FPG, P> A;
+    if (tile * TILE < n) {
+        group_desc<G>(A, tile, n, grp, pkts, off, len, unit_log2);
+        group_load<G>(A, s0);
+    }
+    if constexpr (PIPE) {
+        group_frames<FPG, P> B;
+        group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
+        for (; tile * TILE < n; tile += gridDim.x) {
+            group_load<G>(B, s0); // no-op lanes past the end (cap 0)
+            group_process<G, P, FPG>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            A = B;
+            group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2);
         }
-        // ---- phase B: the first P passes of every frame, all in flight
-        uint4 c[FPG][P];
-#pragma unroll
-        for (int f = 0; f < FPG; ++f)
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const int32_t s = s0 + q * STEP;
-                c[f][q] = make_uint4(0, 0, 0, 0);
-                if (s < cap[f]) c[f][q] = ldg16(fb[f] + s);
-            }
-
-        // ---- phase C: parse + checksum per frame
-        uint32_t cls[FPG], ck[FPG], stored[FPG], tl[FPG], dgl[FPG], hl[FPG], need[FPG];
-        uint32_t ka[FPG], kb[FPG], kc[FPG], dport[FPG];
-        bool ok[FPG];
-#pragma unroll
-        for (int f = 0; f < FPG; ++f) {
-            const int32_t cp = cap[f];
-            uint4 x0 = c[f][0];
-            if (s0 < cp && s0 + 16 > cp) x0 = chunk_below(x0, s0, cp); // bytes past caplen read 0
-            const uint32_t h03 = gbcast<G, 0>(x0.w); // bytes 12..15
-            const uint32_t h10 = gbcast<G, 1>(x0.x); // 16..19
-            const uint32_t h11 = gbcast<G, 1>(x0.y); // 20..23
-            const uint32_t h12 = gbcast<G, 1>(x0.z); // 24..27
-            const uint32_t h13 = gbcast<G, 1>(x0.w); // 28..31
-            const uint32_t h20 = gbcast<G, 2>(x0.x); // 32..35
-            const uint32_t h21 = gbcast<G, 2>(x0.y); // 36..39
-            const uint32_t h22 = gbcast<G, 2>(x0.z); // 40..43
-            const uint32_t h23 = gbcast<G, 2>(x0.w); // 44..47
-            const uint32_t h30 = gbcast<G, 3>(x0.x); // 48..51
-
-            const uint32_t et = h03 & 0xFFFFu; // LE view of bytes 12,13
-            tl[f] = rx_bswap16(h10 & 0xFFFFu);
-            const uint32_t proto = h11 >> 24;
-            const uint32_t sip = (h12 >> 16) | (h13 << 16);
-            const uint32_t dip = (h13 >> 16) | (h20 << 16);
-            const uint32_t sport = h20 >> 16;
-            dport[f] = h21 & 0xFFFFu;
-            dgl[f] = rx_bswap16(h21 >> 16);
-            hl[f] = ((h23 >> 16) & 0xFFu) >> 4;
-
-            uint32_t cl, nd;
-            if (et == 0x0608u) {
-                cl = RXG_CLS_ARP;
-                nd = 42;
-            } else if (et != 0x0008u) {
-                cl = RXG_CLS_NON_IP;
-                nd = 14;
-            } else if (proto == 17u) {
-                cl = RXG_CLS_UDP;
-                nd = 42;
-            } else if (proto == 6u) {
-                cl = RXG_CLS_TCP;
-                nd = 54;
-            } else {
-                cl = RXG_CLS_IPV4_OTHER;
-                nd = 24;
-            }
-            const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
-            const bool l4 = is_udp || is_tcp;
-            const uint32_t l4n = tl[f] >= 20u ? tl[f] - 20u : 0u;
-            const bool do_sum = l4 && tl[f] >= 20u;
-            if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-            cls[f] = cl;
-            need[f] = nd;
-
-            // checksum region [26, e): e = min(34 + l4n, caplen)
-            int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
-            if (e > cp) e = cp;
-            uint32_t acc = 0;
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const int32_t s = s0 + q * STEP;
-                uint4 v = c[f][q];
-                if (s + 16 > e) v = chunk_below(v, s, e);
-                if (q == 0) { // header bytes [0,26) and the checksum field are not summed
-                    if (gl == 0) v = make_uint4(0, 0, 0, 0);
-                    if (gl == 1) {
-                        v.x = 0;
-                        v.y = 0;
-                        v.z &= 0xFFFF0000u;
-                    }
-                    if (gl == 2 && is_udp) v.z &= 0xFFFF0000u; // UDP cksum at 40..41
-                    if (gl == 3 && is_tcp) v.x &= 0x0000FFFFu; // TCP cksum at 50..51
-                }
-                acc = add_halves(acc, v.x);
-                acc = add_halves(acc, v.y);
-                acc = add_halves(acc, v.z);
-                acc = add_halves(acc, v.w);
-            }
-            // frames longer than P passes: the rest in batches of 4 passes
-            for (int32_t sb = P * STEP; sb < e; sb += 4 * STEP) { // group-uniform
-                uint4 r[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int32_t s = s0 + sb + u * STEP;
-                    r[u] = make_uint4(0, 0, 0, 0);
-                    if (s < e) r[u] = ldg16(fb[f] + s);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int32_t s = s0 + sb + u * STEP;
-                    uint4 v = r[u];
-                    if (s + 16 > e) v = chunk_below(v, s, e);
-                    acc = add_halves(acc, v.x);
-                    acc = add_halves(acc, v.y);
-                    acc = add_halves(acc, v.z);
-                    acc = add_halves(acc, v.w);
-                }
-            }
-            uint32_t sum = gsum<G>(acc);
-            uint32_t k = 0;
-            if (do_sum) {
-                sum += proto << 8;       // psd {zero, proto}
-                sum += rx_bswap16(l4n);  // psd be16(l4_len)
-                k = (~fold16(sum)) & 0xFFFFu;
-                if (k == 0u && proto == 17u) k = 0xFFFFu;
-            }
-            ck[f] = k;
-            stored[f] = is_udp ? (h22 & 0xFFFFu) : (is_tcp ? (h30 >> 16) : 0u);
-            ok[f] = l4 && stored[f] == k;
-            ka[f] = is_udp ? dip : sip;
-            kb[f] = is_udp ? dport[f] : dip;
-            kc[f] = is_udp ? 17u : (sport | (dport[f] << 16));
-        }
-
-        // ---- phase D: flow probes, a 4-slot window per lane group, the first
-        // window of every frame in flight
-        uint32_t flow[FPG], slot[FPG];
-        uint4 sl[FPG];
-        bool probe[FPG];
-#pragma unroll
-        for (int f = 0; f < FPG; ++f) {
-            probe[f] = valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
-            const bool udp = cls[f] == RXG_CLS_UDP;
-            const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
-            slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
-            sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-            if (probe[f] && gl < RX_WINDOW) sl[f] = (udp ? ft.udp : ft.tcp)[(slot[f] + gl) & mask];
-            flow[f] = RXG_FLOW_NONE;
-        }
-#pragma unroll
-        for (int f = 0; f < FPG; ++f) {
-            const bool udp = cls[f] == RXG_CLS_UDP;
-            const uint4 *tbl = udp ? ft.udp : ft.tcp;
-            const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
-            const uint32_t maxp = udp ? ft.udp_probe : ft.tcp_probe;
-            uint4 s = sl[f];
-            uint32_t b = slot[f];
-            for (uint32_t pr = 0; pr < maxp; pr += RX_WINDOW) { // trips are group-uniform
-                const bool hit = probe[f] && gl < RX_WINDOW && s.w != RX_SLOT_EMPTY &&
-                                 s.x == ka[f] && s.y == kb[f] && s.z == kc[f];
-                const bool emp = probe[f] && gl < RX_WINDOW && s.w == RX_SLOT_EMPTY;
-                const uint32_t gh = (uint32_t)(__ballot(hit) >> gbase) & 0xFu;
-                const uint32_t ge = (uint32_t)(__ballot(emp) >> gbase) & 0xFu;
-                // linear probing: the first hit-or-empty slot of the window decides
-                const uint32_t first = (uint32_t)__ffs(gh | ge) - 1u; // 31 if neither (ffs 0)
-                const uint32_t v = __shfl(s.w, gbase + (first & 3u));
-                if (!probe[f]) break; // probe[f], gh, ge are uniform across the group
-                if ((gh | ge) != 0u) {
-                    if (gh & (1u << first)) flow[f] = v;
-                    break;
-                }
-                b = (b + RX_WINDOW) & mask;
-                s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-                if (gl < RX_WINDOW) s = tbl[(b + gl) & mask];
-            }
-            if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
-                flow[f] = ft.listen[dport[f]];
-        }
-
-        // ---- phase E: verdicts (reference return codes) + counts
-#pragma unroll
-        for (int f = 0; f < FPG; ++f) {
-            int32_t rc;
-            uint32_t poff = 0, plen = 0, flags = 0, nd = need[f];
-            if (cls[f] == RXG_CLS_UDP) {
-                rc = flow[f] == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                              : (dgl[f] <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-                poff = 42;
-                plen = dgl[f] > 8u ? dgl[f] - 8u : 0u;
-                if (dgl[f] <= 8u) flags |= RXG_F_UDP_SHORT;
-                if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
-            } else if (cls[f] == RXG_CLS_TCP) {
-                const int32_t pl = (int32_t)tl[f] - 20 - 4 * (int32_t)hl[f];
-                poff = 34u + 4u * hl[f];
-                if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-                plen = pl < 0 ? 0u : (uint32_t)pl;
-                rc = !ok[f] ? RXG_RC_TCP_BAD_CKSUM
-                            : (flow[f] == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-            } else {
-                rc = RXG_RC_KNI;
-            }
-            if ((int32_t)nd > cap[f]) flags |= RXG_F_TRUNC;
-            if (gl == 0 && valid[f]) {
-                uint4 v;
-                v.x = flow[f];
-                v.y = (poff & 0xFFFFu) | (plen << 16);
-                v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
-                v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
-                stg16(&out[pf[f]], v);
-                if (counts && rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE) {
-                    const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
-                    if (lds_bins)
-                        atomicAdd(&hist[idx], 1u);
-                    else
-                        atomicAdd(&counts[idx], 1ull);
-                }
-            }
+    } else {
+        for (; tile * TILE < n; tile += gridDim.x) {
+            group_process<G, P, FPG>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
+            group_load<G>(A, s0);
         }
     }
 
@@ -367,7 +413,7 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     }
 }
 
-template <int G, int P, int FPG>
+template <int G, int P, int FPG, int PIPE = 0>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s) {
@@ -388,7 +434,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG>), 256, lds);
+            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE>), 256, lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
@@ -397,7 +443,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
@@ -715,20 +761,30 @@ typedef hipError_t (*launch_fn)(const uint8_t *, const uint32_t *, const uint16_
                                 uint32_t, const rx_ft_dev &, uint4 *, unsigned long long *,
                                 uint32_t, hipStream_t);
 struct variant_entry {
-    uint32_t g, p, fpg;
+    uint32_t g, p, fpg, pipe;
     launch_fn fn;
 };
-// every compiled variant; the first entry per G is its default
+// every compiled variant; the first entry per lanes-per-frame g is its default.
+// g = 1 (one frame per lane): p = 4 chunks up front, pipe = prefetch mode
+// (0 none, 1 descriptors + frame one trip ahead, 2 = 1 capped at 6 waves/SIMD,
+// 3 descriptors only, 4 = 0 with plain verdict stores); pipe >= 100 are
+// diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
-    {1, 1, 1, launch_lane<1>},      {1, 0, 1, launch_lane<0>},      {1, 2, 1, launch_lane<2>},
-    {1, 3, 1, launch_lane<3>},      {1, 4, 1, launch_lane<0, 0, false>},
-    // diagnostic ablations (wrong verdicts by construction; tuning only)
-    {1, 101, 1, launch_lane<0, 1>}, {1, 104, 1, launch_lane<0, 4>}, {1, 108, 1, launch_lane<0, 8>},
-    {1, 113, 1, launch_lane<0, 13>},
-    {4, 1, 2, launch_v<4, 1, 2>},   {4, 1, 1, launch_v<4, 1, 1>},   {4, 1, 4, launch_v<4, 1, 4>},
-    {8, 2, 2, launch_v<8, 2, 2>},   {8, 2, 1, launch_v<8, 2, 1>},   {16, 2, 2, launch_v<16, 2, 2>},
-    {16, 2, 1, launch_v<16, 2, 1>}, {32, 3, 2, launch_v<32, 3, 2>}, {32, 3, 1, launch_v<32, 3, 1>},
-    {32, 2, 1, launch_v<32, 2, 1>}, {64, 4, 1, launch_v<64, 4, 1>}, {64, 2, 1, launch_v<64, 2, 1>},
+    {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
+    {1, 4, 1, 2, launch_lane<2>},          {1, 4, 1, 3, launch_lane<3>},
+    {1, 4, 1, 4, launch_lane<0, 0, false>},
+    {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
+    {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
+    {4, 1, 1, 1, launch_v<4, 1, 1, 1>},    {4, 1, 1, 0, launch_v<4, 1, 1, 0>},
+    {4, 1, 2, 0, launch_v<4, 1, 2, 0>},    {4, 1, 2, 1, launch_v<4, 1, 2, 1>},
+    {4, 1, 4, 0, launch_v<4, 1, 4, 0>},
+    {8, 2, 2, 0, launch_v<8, 2, 2, 0>},    {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
+    {8, 2, 1, 0, launch_v<8, 2, 1, 0>},    {8, 2, 1, 1, launch_v<8, 2, 1, 1>},
+    {16, 2, 2, 0, launch_v<16, 2, 2, 0>},  {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
+    {16, 2, 1, 1, launch_v<16, 2, 1, 1>},  {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
+    {32, 3, 1, 0, launch_v<32, 3, 1, 0>},  {32, 2, 1, 1, launch_v<32, 2, 1, 1>},
+    {64, 4, 1, 0, launch_v<64, 4, 1, 0>},  {64, 2, 1, 0, launch_v<64, 2, 1, 0>},
+    {64, 2, 1, 1, launch_v<64, 2, 1, 1>},
 };
 
 } // namespace
@@ -745,17 +801,18 @@ uint32_t rx_pick_group(uint32_t len_hint) {
     return 64;
 }
 
-// variant = (g, p, fpg); p == 0 / fpg == 0 pick the default for g.
+// variant = (g, p, fpg, pipe); p == 0 / fpg == 0 / pipe == ~0 pick the default for g.
 // LDS histogram when the flow count fits comfortably (<= 8192 bins = 32 KiB).
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
-                              const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
-                              hipStream_t s) {
+                              uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
+                              unsigned long long *counts, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t nflows = ft.nu + ft.nt;
     const uint32_t lds_bins = (counts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
     for (const variant_entry &v : k_variants)
-        if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg))
+        if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
+            (pipe == 0xFFFFFFFFu || v.pipe == pipe))
             return v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s);
     return hipErrorInvalidValue;
 }

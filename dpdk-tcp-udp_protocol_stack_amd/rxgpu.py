@@ -43,10 +43,13 @@ RC_OK, RC_TCP_BAD_CKSUM, RC_TCP_NO_TCB, RC_UDP_NOMEM, RC_UDP_NO_SOCKET, RC_KNI =
 F_TRUNC, F_TCP_NEGLEN, F_UDP_SHORT = 0x1, 0x2, 0x4
 TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
 HOST_ONLY = -1
-# (lanes per frame, passes up front, frames per group) compiled in rx_classify.hip;
-# for lanes per frame = 1 the second field is the prefetch depth (0 or 1 trip)
-KERNEL_VARIANTS = [(1, 1, 1), (1, 0, 1), (1, 2, 1), (1, 3, 1), (1, 4, 1), (4, 1, 2), (4, 1, 1), (4, 1, 4), (8, 2, 2), (8, 2, 1), (16, 2, 2), (16, 2, 1),
-                   (32, 3, 2), (32, 3, 1), (32, 2, 1), (64, 4, 1), (64, 2, 1)]
+# (lanes per frame, passes up front, frames per group, pipeline) compiled in
+# rx_classify.hip (verdict-exact ones; the >= 100 pipeline ids are ablations)
+KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4, 1, 4),
+                   (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
+                   (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
+                   (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
+                   (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1)]
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -100,7 +103,7 @@ _process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
 _flow_counts = _sig("rxg_flow_counts", _i32, _vp, _vp, _u32)
 _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
 _num_flows = _sig("rxg_num_flows", _u32, _vp)
-_tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32)
+_tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
 _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
@@ -184,9 +187,10 @@ class Context:
                            _ptr(tcb) if len(tcb) else None, len(tcb)), "rxg_flows_sync")
         self.nu, self.nt = len(udp), len(tcb)
 
-    def tune(self, lanes_per_frame: int = 0, passes: int = 0, frames_per_group: int = 0):
-        """force a kernel variant (0 = automatic); see KERNEL_VARIANTS"""
-        _check(_tune(self._h, lanes_per_frame, passes, frames_per_group), "rxg_tune")
+    def tune(self, lanes_per_frame: int = 0, passes: int = 0, frames_per_group: int = 0,
+             pipeline: int = 0xFFFFFFFF):
+        """force a kernel variant (lanes_per_frame 0 = automatic); see KERNEL_VARIANTS"""
+        _check(_tune(self._h, lanes_per_frame, passes, frames_per_group, pipeline), "rxg_tune")
 
     @property
     def num_flows(self) -> int:

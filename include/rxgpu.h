@@ -169,9 +169,11 @@ int rxg_classify(rxg_ctx *ctx, const uint8_t *pkts, const uint32_t *off, const u
 int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
 
 /* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
- * loaded up front, frames per lane group); 0 = automatic from len_hint.
- * Unknown combinations make the next burst fail with RXG_EHIP. */
-int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group);
+ * loaded up front, frames per lane group, pipeline mode; 0xFFFFFFFF = the
+ * default pipeline); lanes_per_frame = 0 = automatic from len_hint.  Unknown
+ * combinations make the next burst fail with RXG_EHIP. */
+int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
+             uint32_t pipeline);
 
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
