@@ -177,6 +177,54 @@ def cpu_baseline(name, budget_s):
 
 
 # ---------------------------------------------------------------------------
+def sweep(ctx, names, steps, warmup, dev, only=""):
+    """Tuning: every kernel variant, interleaved over rounds in one process
+    (same data, same device), median and min of the per-round kernel time."""
+    variants = [tuple(int(x) for x in v.split(",")) for v in only.split(";") if v] or \
+        R.KERNEL_VARIANTS
+    # a 5th field = resident blocks per CU cap
+    variants = [v if len(v) == 5 else v + (0,) for v in variants]
+    for nm in names:
+        w = rxdist.WORKLOADS[nm]
+        cfg = rxdist.gen_cfg(nm)
+        n = w["n"]
+        udp, tcb = R.gen_flows(cfg)
+        ctx.flows_sync(udp, tcb)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
+        off = torch.empty(n, dtype=torch.int32, device=dev)
+        ln = torch.empty(n, dtype=torch.int16, device=dev)
+        out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
+        torch.cuda.synchronize(dev)
+        alg = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item()) + 22 * n
+        times = {v: [] for v in variants}
+        for rnd in range(5):
+            for v in variants:
+                ctx.tune(*v[:4])
+                ctx.tune_grid(v[4])
+                for _ in range(warmup):
+                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                                     stream=sh)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(steps):
+                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                                     stream=sh)
+                b.record()
+                torch.cuda.synchronize(dev)
+                times[v].append(a.elapsed_time(b) / steps)
+        ctx.tune(0)
+        ctx.tune_grid(0)
+        for v in variants:
+            t = sorted(times[v])
+            med = t[len(t) // 2]
+            log(f"sweep {nm} variant={v}: median {med:.4f} ms min {t[0]:.4f} ms "
+                f"-> {n / med / 1e3:.0f} Mpps, {alg / med / 1e6:.0f} GB/s")
+        del pk, off, ln, out
+        torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,6 +235,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
@@ -207,14 +256,7 @@ def main():
     if a.variant:
         ctx.tune(*[int(x) for x in a.variant.split(",")])
     if a.sweep:
-        for nm in a.sweep.split(","):
-            for var in R.KERNEL_VARIANTS:
-                ctx.tune(*var)
-                r = run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev)
-                log(f"sweep {nm} variant={var}: kernel {r['kernel_ms_avg']:.4f} ms "
-                    f"(min {r['kernel_ms_min']:.4f}), {r['mpps']:.1f} Mpps, "
-                    f"{r['roofline']['achieved']:.0f} GB/s")
-            ctx.tune(0)
+        sweep(ctx, a.sweep.split(","), a.steps, a.warmup, dev, a.sweep_variants)
         return
     names = [s.strip() for s in a.workload.split(",") if s.strip()]
     results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}

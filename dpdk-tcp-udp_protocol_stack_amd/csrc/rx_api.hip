@@ -14,6 +14,7 @@
 #include "rx_common.h"
 
 uint32_t rx_pick_group(uint32_t len_hint);
+void rx_set_bpc_cap(uint32_t cap);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
@@ -86,6 +87,7 @@ struct rxg_ctx {
     uint32_t *d_listen = nullptr;
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
+    uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
     uint32_t counts_cap = 0;
@@ -276,6 +278,12 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
     return RXG_OK;
 }
 
+int rxg_tune_grid(rxg_ctx *c, uint32_t blocks_per_cu) {
+    if (!c || blocks_per_cu > 32) return RXG_EINVAL;
+    c->tune_bpc = blocks_per_cu;
+    return RXG_OK;
+}
+
 uint32_t rxg_num_flows(const rxg_ctx *c) { return c ? c->ft.nu + c->ft.nt : 0; }
 
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *c, uint32_t dip, uint16_t dport) {
@@ -304,6 +312,7 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     HIPCHK(hipSetDevice(c->device));
     const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group(len_hint);
+    rx_set_bpc_cap(c->tune_bpc);
     HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, c->tune_p, c->tune_fpg,
                               c->tune_pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
                               reinterpret_cast<unsigned long long *>(d_counts),
@@ -332,6 +341,7 @@ int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uin
     HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
     const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group((uint32_t)(sumlen / n));
+    rx_set_bpc_cap(c->tune_bpc);
     HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, c->tune_p,
                               c->tune_fpg, c->tune_pipe, c->ft, c->d_out, c->d_counts, c->stream));
     HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));

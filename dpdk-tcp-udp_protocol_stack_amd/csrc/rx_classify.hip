@@ -93,10 +93,20 @@ __device__ __forceinline__ uint4 chunk_below(uint4 c, int32_t s, int32_t end) {
 
 typedef unsigned int rx_u32x4 __attribute__((ext_vector_type(4)));
 
-// streaming 16-B load / store (frames and verdicts are touched once: nt)
+// resident blocks per CU the launchers use: min(occupancy, cap); 0 = no cap
+static thread_local uint32_t g_bpc_cap = 0;
+
+// streaming 16-B load / store.  nt (non-temporal) pays for coalesced 1-KiB
+// wave accesses and costs for 16-B-per-lane strided ones (tools/membw.hip), so
+// the policy is a template choice of each kernel.
+template <bool NT = true>
 __device__ __forceinline__ uint4 ldg16(const uint8_t *p) {
-    const rx_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rx_u32x4 *>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
+    if constexpr (NT) {
+        const rx_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rx_u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
 }
 __device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
     const rx_u32x4 w = {v.x, v.y, v.z, v.w};
@@ -135,7 +145,7 @@ __device__ __forceinline__ void group_desc(group_frames<FPG, P> &S, uint64_t til
     }
 }
 
-template <int G, int FPG, int P>
+template <int G, int FPG, int P, bool NTL = true>
 __device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) {
 #pragma unroll
     for (int f = 0; f < FPG; ++f)
@@ -143,12 +153,12 @@ __device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) 
         for (int q = 0; q < P; ++q) {
             const int32_t s = s0 + q * 16 * G;
             S.c[f][q] = make_uint4(0, 0, 0, 0);
-            if (s < S.cap[f]) S.c[f][q] = ldg16(S.fb[f] + s);
+            if (s < S.cap[f]) S.c[f][q] = ldg16<NTL>(S.fb[f] + s);
         }
 }
 
 // parse + checksum + probe + verdict for the FPG frames of S
-template <int G, int P, int FPG>
+template <int G, int P, int FPG, bool NTL = true>
 __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t gl, uint32_t gbase,
                                               int32_t s0, const rx_ft_dev &ft,
                                               uint4 *__restrict__ out,
@@ -359,7 +369,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
 // PIPE = 1: trip t+1's descriptors are fetched one trip ahead and its frame
 // bytes are issued before trip t is processed (one extra frame set of
 // registers), so both HBM round trips overlap the previous trip's work.
-template <int G, int P, int FPG, int PIPE>
+template <int G, int P, int FPG, int PIPE, bool NTL = true>
 __global__ __launch_bounds__(256) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -385,22 +395,22 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     group_frames<FPG, P> A;
     if (tile * TILE < n) {
         group_desc<G>(A, tile, n, grp, pkts, off, len, unit_log2);
-        group_load<G>(A, s0);
+        group_load<G, FPG, P, NTL>(A, s0);
     }
     if constexpr (PIPE) {
         group_frames<FPG, P> B;
         group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
         for (; tile * TILE < n; tile += gridDim.x) {
-            group_load<G>(B, s0); // no-op lanes past the end (cap 0)
-            group_process<G, P, FPG>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_load<G, FPG, P, NTL>(B, s0); // no-op lanes past the end (cap 0)
+            group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             A = B;
             group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2);
         }
     } else {
         for (; tile * TILE < n; tile += gridDim.x) {
-            group_process<G, P, FPG>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
-            group_load<G>(A, s0);
+            group_load<G, FPG, P, NTL>(A, s0);
         }
     }
 
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     }
 }
 
-template <int G, int P, int FPG, int PIPE = 0>
+template <int G, int P, int FPG, int PIPE = 0, bool NTL = true>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s) {
@@ -434,16 +444,18 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE>), 256, lds);
+            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL>), 256, lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
     }
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
-    uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
+    uint64_t occ = (uint64_t)cached_occ[slot];
+    if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
+    uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
@@ -484,11 +496,12 @@ __device__ __forceinline__ void lane_desc(lane_frame &L, uint64_t p, uint32_t n,
     L.cap = L.valid ? (int32_t)len[q] : 0;
 }
 
+template <bool NTL>
 __device__ __forceinline__ void lane_load(lane_frame &L) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         L.c[j] = make_uint4(0, 0, 0, 0);
-        if (16 * j < L.cap) L.c[j] = ldg16(L.fb + 16 * j);
+        if (16 * j < L.cap) L.c[j] = ldg16<NTL>(L.fb + 16 * j);
     }
 }
 
@@ -498,7 +511,7 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 // the bulk bytes of trip t+1 are in flight across the probe latency of trip t.
 // ABL (diagnostic builds only, never selected automatically): 1 = no bucket
 // probe, 4 = no verdict store, 8 = no checksum arithmetic.
-template <int ABL = 0, bool ST_NT = true>
+template <int ABL = 0, bool ST_NT = true, bool NTL = true>
 __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
                                              const rx_ft_dev &ft, uint4 *__restrict__ out,
                                              unsigned long long *__restrict__ counts,
@@ -562,7 +575,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             r[u] = make_uint4(0, 0, 0, 0);
-            if (s + 16 * u < e) r[u] = ldg16(L.fb + s + 16 * u);
+            if (s + 16 * u < e) r[u] = ldg16<NTL>(L.fb + s + 16 * u);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc = lane_chunk_sum(acc, r[u], s + 16 * u, e);
@@ -577,7 +590,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
     const uint32_t stored = is_udp ? (c2.z & 0xFFFFu) : (is_tcp ? (c3.x >> 16) : 0u);
     const bool ok = l4 && stored == ck;
 
-    if (next) lane_load(*next); // trip t+1 bytes in flight from here on
+    if (next) lane_load<NTL>(*next); // trip t+1 bytes in flight from here on
 
     // flow probe: the whole 64-B bucket per lane
     uint32_t flow = RXG_FLOW_NONE;
@@ -648,7 +661,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
 // fetched at the top of trip t and its frame bytes are issued mid-trip.
 // PIPE = 2: as 1, register budget capped for 6 waves per SIMD.  PIPE = 3:
 // only the descriptors are prefetched (frame bytes loaded at the top).
-template <int PIPE, int ABL = 0, bool ST_NT = true>
+template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
 __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -665,8 +678,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
         for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2);
-            lane_load(L);
-            lane_process<ABL, ST_NT>(L, nullptr, ft, out, counts, hist, lds_bins);
+            lane_load<NTL>(L);
+            lane_process<ABL, ST_NT, NTL>(L, nullptr, ft, out, counts, hist, lds_bins);
         }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
@@ -684,32 +697,32 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             L.valid = p < n;
             L.fb = nfb;
             L.cap = ncap;
-            lane_load(L);
+            lane_load<NTL>(L);
             nq = p + stride; // descriptors of the next trip, in flight during this one
             const uint64_t q = nq < n ? nq : 0;
             nfb = pkts + ((uint64_t)off[q] << unit_log2);
             ncap = nq < n ? (int32_t)len[q] : 0;
-            lane_process(L, nullptr, ft, out, counts, hist, lds_bins);
+            lane_process<0, ST_NT, NTL>(L, nullptr, ft, out, counts, hist, lds_bins);
         }
     } else {
         lane_frame A, B;
         uint64_t base = (uint64_t)blockIdx.x * 256;
         if (base < n) {
             lane_desc(A, p, n, pkts, off, len, unit_log2);
-            lane_load(A);
+            lane_load<NTL>(A);
         }
         // two frames alternate roles; the loop body is unrolled twice so that
         // A and B stay in fixed registers
         while (base < n) {
             uint64_t nb = base + stride;
             lane_desc(B, p + stride, n, pkts, off, len, unit_log2);
-            lane_process(A, nb < n ? &B : nullptr, ft, out, counts, hist, lds_bins);
+            lane_process<0, ST_NT, NTL>(A, nb < n ? &B : nullptr, ft, out, counts, hist, lds_bins);
             base = nb;
             p += stride;
             if (base >= n) break;
             nb = base + stride;
             lane_desc(A, p + stride, n, pkts, off, len, unit_log2);
-            lane_process(B, nb < n ? &A : nullptr, ft, out, counts, hist, lds_bins);
+            lane_process<0, ST_NT, NTL>(B, nb < n ? &A : nullptr, ft, out, counts, hist, lds_bins);
             base = nb;
             p += stride;
         }
@@ -723,7 +736,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     }
 }
 
-template <int PIPE, int ABL = 0, bool ST_NT = true>
+template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
 hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s) {
@@ -742,17 +755,19 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT>), 256,
+            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL>), 256,
             lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
     }
     const uint64_t tiles = ((uint64_t)n + 255) / 256;
-    uint64_t blocks = (uint64_t)cu * (uint64_t)cached_occ[slot];
+    uint64_t occ = (uint64_t)cached_occ[slot];
+    if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
+    uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
     return hipGetLastError();
 }
@@ -763,22 +778,31 @@ typedef hipError_t (*launch_fn)(const uint8_t *, const uint32_t *, const uint16_
 struct variant_entry {
     uint32_t g, p, fpg, pipe;
     launch_fn fn;
+    uint32_t bpc; // default resident blocks per CU (0 = occupancy), from measurement
 };
 // every compiled variant; the first entry per lanes-per-frame g is its default.
 // g = 1 (one frame per lane): p = 4 chunks up front, pipe = prefetch mode
 // (0 none, 1 descriptors + frame one trip ahead, 2 = 1 capped at 6 waves/SIMD,
-// 3 descriptors only, 4 = 0 with plain verdict stores); pipe >= 100 are
+// 3 descriptors only, 4 = 0 with plain verdict stores, 5/6 = 0/4 with plain
+// frame loads, 7/8 = 1/2 with plain frame loads); g >= 4: pipe 0/1 = no /
+// one-trip pipeline, 2/3 = 0/1 with plain frame loads; pipe >= 100 are
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
+    // defaults first (measured on MI355X, bench.py --sweep)
+    {1, 4, 1, 5, launch_lane<0, 0, true, false>, 6},
+    {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
     {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
     {1, 4, 1, 2, launch_lane<2>},          {1, 4, 1, 3, launch_lane<3>},
     {1, 4, 1, 4, launch_lane<0, 0, false>},
+    {1, 4, 1, 6, launch_lane<0, 0, false, false>},
+    {1, 4, 1, 7, launch_lane<1, 0, true, false>}, {1, 4, 1, 8, launch_lane<2, 0, true, false>},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {4, 1, 1, 1, launch_v<4, 1, 1, 1>},    {4, 1, 1, 0, launch_v<4, 1, 1, 0>},
+    {4, 1, 1, 3, launch_v<4, 1, 1, 1, false>}, {4, 1, 2, 2, launch_v<4, 1, 2, 0, false>},
     {4, 1, 2, 0, launch_v<4, 1, 2, 0>},    {4, 1, 2, 1, launch_v<4, 1, 2, 1>},
     {4, 1, 4, 0, launch_v<4, 1, 4, 0>},
-    {8, 2, 2, 0, launch_v<8, 2, 2, 0>},    {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
+    {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
     {8, 2, 1, 0, launch_v<8, 2, 1, 0>},    {8, 2, 1, 1, launch_v<8, 2, 1, 1>},
     {16, 2, 2, 0, launch_v<16, 2, 2, 0>},  {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
     {16, 2, 1, 1, launch_v<16, 2, 1, 1>},  {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
@@ -794,15 +818,15 @@ static const variant_entry k_variants[] = {
 // choice only moves speed.
 uint32_t rx_pick_group(uint32_t len_hint) {
     if (len_hint == 0) len_hint = 1518;
-    if (len_hint <= 64) return 1;
-    if (len_hint <= 256) return 8;
-    if (len_hint <= 512) return 16;
-    if (len_hint <= 1536) return 32;
+    if (len_hint <= 64) return 1;  // one frame per lane
+    if (len_hint <= 1536) return 8; // 8 lanes x 16 B: 128 B per pass
     return 64;
 }
 
 // variant = (g, p, fpg, pipe); p == 0 / fpg == 0 / pipe == ~0 pick the default for g.
 // LDS histogram when the flow count fits comfortably (<= 8192 bins = 32 KiB).
+void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
+
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
@@ -812,7 +836,12 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
     const uint32_t lds_bins = (counts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
     for (const variant_entry &v : k_variants)
         if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
-            (pipe == 0xFFFFFFFFu || v.pipe == pipe))
-            return v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s);
+            (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
+            const uint32_t user_cap = g_bpc_cap;
+            if (!user_cap) g_bpc_cap = v.bpc;
+            hipError_t e = v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s);
+            g_bpc_cap = user_cap;
+            return e;
+        }
     return hipErrorInvalidValue;
 }

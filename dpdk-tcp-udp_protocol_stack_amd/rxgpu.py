@@ -46,7 +46,8 @@ HOST_ONLY = -1
 # (lanes per frame, passes up front, frames per group, pipeline) compiled in
 # rx_classify.hip (verdict-exact ones; the >= 100 pipeline ids are ablations)
 KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4, 1, 4),
-                   (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
+                   (1, 4, 1, 5), (1, 4, 1, 6), (1, 4, 1, 7), (1, 4, 1, 8),
+                   (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 1, 3), (4, 1, 2, 2), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
                    (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
                    (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1)]
@@ -104,6 +105,7 @@ _flow_counts = _sig("rxg_flow_counts", _i32, _vp, _vp, _u32)
 _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
 _num_flows = _sig("rxg_num_flows", _u32, _vp)
 _tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
+_tune_grid = _sig("rxg_tune_grid", _i32, _vp, _u32)
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
 _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
@@ -113,7 +115,7 @@ _gen_dev = _sig("rxg_gen_dev", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _v
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev"]
 
 
@@ -191,6 +193,10 @@ class Context:
              pipeline: int = 0xFFFFFFFF):
         """force a kernel variant (lanes_per_frame 0 = automatic); see KERNEL_VARIANTS"""
         _check(_tune(self._h, lanes_per_frame, passes, frames_per_group, pipeline), "rxg_tune")
+
+    def tune_grid(self, blocks_per_cu: int = 0):
+        """cap resident blocks per CU (0 = occupancy)"""
+        _check(_tune_grid(self._h, blocks_per_cu), "rxg_tune_grid")
 
     @property
     def num_flows(self) -> int:

@@ -175,6 +175,10 @@ int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict 
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline);
 
+/* Tuning hook: cap the resident 256-thread blocks per CU the launch uses
+ * (0 = as many as the occupancy allows). */
+int rxg_tune_grid(rxg_ctx *ctx, uint32_t blocks_per_cu);
+
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);
