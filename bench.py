@@ -177,6 +177,40 @@ def cpu_baseline(name, budget_s):
 
 
 # ---------------------------------------------------------------------------
+def e2e(name, local, batch, reps=20):
+    """PCIe-inclusive rate of the host-buffer path (rxg_classify_span):
+    pinned host frames + descriptors -> H2D -> K1 -> verdicts D2H, synchronous
+    per burst (no overlap between bursts).  Reported in DESIGN.md, never as value."""
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name)
+    span = batch * cfg.slot_bytes
+    pk = torch.empty(span + 64, dtype=torch.uint8).pin_memory()
+    off = torch.empty(batch, dtype=torch.int32).pin_memory()
+    ln = torch.empty(batch, dtype=torch.int16).pin_memory()
+    out = torch.empty(batch * 16, dtype=torch.uint8).pin_memory()
+    hp, ho, hl = R.gen_host(cfg, 0, batch, w["unit_log2"])
+    pk.numpy()[:span] = hp
+    off.numpy().view(np.uint32)[:] = ho
+    ln.numpy().view(np.uint16)[:] = hl
+    ctx = R.Context(local, max_pkts=batch, max_bytes=span + 64)
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    args = (pk.data_ptr(), span, off.data_ptr(), ln.data_ptr(), batch, w["unit_log2"],
+            out.data_ptr())
+    for _ in range(3):
+        ctx.classify_span(*args)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.classify_span(*args)
+    el = (time.perf_counter() - t0) / reps
+    frame_bytes = int(hl.astype(np.int64).sum())
+    ctx.close()
+    return dict(workload=name, frames_per_burst=batch, ms_per_burst=round(el * 1e3, 3),
+                mpps=round(batch / el / 1e6, 1),
+                h2d_gb_per_s=round((span + 6 * batch) / el / 1e9, 2),
+                alg_gb_per_s=round((frame_bytes + 22 * batch) / el / 1e9, 2))
+
+
 def sweep(ctx, names, steps, warmup, dev, only=""):
     """Tuning: every kernel variant, interleaved over rounds in one process
     (same data, same device), median and min of the per-round kernel time."""
@@ -235,6 +269,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
@@ -268,6 +303,12 @@ def main():
         for nm in names[1:]:
             results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget / 2)
 
+    if a.e2e and rank == 0:
+        for nm in names:
+            r = e2e(nm, local, {"cfg2": 1 << 20, "cfg3": 1 << 16}.get(nm, 1 << 16))
+            log("e2e", json.dumps(r))
+            results[nm]["e2e_pcie"] = r
+
     if rank == 0:
         line = {
             "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
@@ -290,6 +331,8 @@ def main():
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
         }
+        if "e2e_pcie" in head:
+            line["e2e_pcie"] = head["e2e_pcie"]
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}

@@ -320,6 +320,29 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     return RXG_OK;
 }
 
+int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                      const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n == 0) return RXG_OK;
+    if (!pkts || !off || !len || !out) return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    if (n > c->max_pkts || !c->d_pkts) return RXG_ERANGE;
+    const uint64_t span = (span_bytes + 15) & ~15ull;
+    if (span > c->max_bytes) return RXG_ERANGE;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_pkts, pkts, span, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
+    const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group((uint32_t)(span / n));
+    rx_set_bpc_cap(c->tune_bpc);
+    HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, c->tune_p,
+                              c->tune_fpg, c->tune_pipe, c->ft, c->d_out, c->d_counts, c->stream));
+    HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RXG_OK;
+}
+
 int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                  uint32_t n, uint32_t off_unit_log2, rxg_verdict *out) {
     if (!c) return RXG_EINVAL;
@@ -327,26 +350,12 @@ int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uin
     if (n == 0) return RXG_OK;
     if (!pkts || !off || !len || !out) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    if (n > c->max_pkts || !c->d_pkts) return RXG_ERANGE;
-    uint64_t span = 0, sumlen = 0;
+    uint64_t span = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        uint64_t e = ((uint64_t)off[i] << off_unit_log2) + len[i];
+        const uint64_t e = ((uint64_t)off[i] << off_unit_log2) + len[i];
         span = std::max(span, e);
-        sumlen += len[i];
     }
-    span = (span + 15) & ~15ull;
-    if (span > c->max_bytes) return RXG_ERANGE;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpyAsync(c->d_pkts, pkts, span, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
-    const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group((uint32_t)(sumlen / n));
-    rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, c->tune_p,
-                              c->tune_fpg, c->tune_pipe, c->ft, c->d_out, c->d_counts, c->stream));
-    HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return RXG_OK;
+    return rxg_classify_span(c, pkts, span, off, len, n, off_unit_log2, out);
 }
 
 int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out) {

@@ -100,6 +100,7 @@ _last_hip = _sig("rxg_last_hip_error", C.c_char_p)
 _flows_sync = _sig("rxg_flows_sync", _i32, _vp, _vp, _u32, _vp, _u32)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify = _sig("rxg_classify", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp)
+_classify_span = _sig("rxg_classify_span", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32, _vp)
 _process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
 _flow_counts = _sig("rxg_flow_counts", _i32, _vp, _vp, _u32)
 _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
@@ -114,7 +115,7 @@ _gen_host = _sig("rxg_gen_host", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, 
 _gen_dev = _sig("rxg_gen_dev", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32, _vp)
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
-            "rxg_classify_dev", "rxg_classify", "rxg_process_mbufs", "rxg_flow_counts",
+            "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev"]
 
@@ -218,6 +219,12 @@ class Context:
         _check(_classify(self._h, _ptr(pkts), _ptr(off), _ptr(lens), len(off), off_unit_log2,
                          _ptr(out)), "rxg_classify")
         return out
+
+    def classify_span(self, pkts_ptr: int, span: int, off_ptr: int, len_ptr: int, n: int,
+                      off_unit_log2: int, out_ptr: int):
+        """raw-pointer host burst (pinned buffers from the caller), PCIe-inclusive"""
+        _check(_classify_span(self._h, pkts_ptr, span, off_ptr, len_ptr, n, off_unit_log2,
+                              out_ptr), "rxg_classify_span")
 
     def classify_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
                      d_out, d_counts=None, stream=None):

@@ -164,6 +164,11 @@ int rxg_classify_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
 int rxg_classify(rxg_ctx *ctx, const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                  uint32_t n, uint32_t off_unit_log2, rxg_verdict *out);
 
+/* Same, with the caller stating how many bytes of `pkts` the burst spans
+ * (every frame end <= span_bytes); skips the O(n) scan rxg_classify makes. */
+int rxg_classify_span(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                      const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out);
+
 /* The reference's calling convention: a burst of mbuf pointers as dequeued at
  * netfamily.c:147.  Frames are gathered into the context's staging buffer. */
 int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
