@@ -13,7 +13,7 @@
 
 #include "rx_common.h"
 
-uint32_t rx_pick_group(uint32_t len_hint);
+void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
 void rx_set_bpc_cap(uint32_t cap);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
@@ -311,10 +311,10 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (!d_pkts || !d_off || !d_len || !d_out) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     HIPCHK(hipSetDevice(c->device));
-    const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group(len_hint);
+    uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
+    if (!g) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
     rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, c->tune_p, c->tune_fpg,
-                              c->tune_pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
+    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
                               reinterpret_cast<unsigned long long *>(d_counts),
                               (hipStream_t)stream));
     return RXG_OK;
@@ -334,10 +334,11 @@ int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, cons
     HIPCHK(hipMemcpyAsync(c->d_pkts, pkts, span, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
-    const uint32_t g = c->tune_g ? c->tune_g : rx_pick_group((uint32_t)(span / n));
+    uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
+    if (!g) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
     rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, c->tune_p,
-                              c->tune_fpg, c->tune_pipe, c->ft, c->d_out, c->d_counts, c->stream));
+    HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, p, fpg, pipe,
+                              c->ft, c->d_out, c->d_counts, c->stream));
     HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;

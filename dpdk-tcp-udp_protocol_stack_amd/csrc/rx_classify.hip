@@ -813,18 +813,23 @@ static const variant_entry k_variants[] = {
 
 } // namespace
 
-// Lanes per frame (G) from the typical frame length.  Any frame length works
+// Default variant per typical frame length (measured on MI355X with
+// bench.py --sweep, interleaved rounds).  Any frame length works
 // with any variant (frames longer than P passes take the remainder loop); the
 // choice only moves speed.
-uint32_t rx_pick_group(uint32_t len_hint) {
+void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
     if (len_hint == 0) len_hint = 1518;
-    if (len_hint <= 64) return 1;  // one frame per lane
-    if (len_hint <= 1536) return 8; // 8 lanes x 16 B: 128 B per pass
-    return 64;
+    if (len_hint <= 64) { // cfg2: 64 B
+        *g = 1, *p = 4, *fpg = 1, *pipe = 5;
+    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4)
+        *g = 8, *p = 2, *fpg = 1, *pipe = 1;
+    } else if (len_hint <= 1536) { // cfg3: 1500 B
+        *g = 8, *p = 2, *fpg = 2, *pipe = 0;
+    } else { // jumbo (cfg5: 9000 B)
+        *g = 16, *p = 2, *fpg = 2, *pipe = 0;
+    }
 }
 
-// variant = (g, p, fpg, pipe); p == 0 / fpg == 0 / pipe == ~0 pick the default for g.
-// LDS histogram when the flow count fits comfortably (<= 8192 bins = 32 KiB).
 void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
 
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
