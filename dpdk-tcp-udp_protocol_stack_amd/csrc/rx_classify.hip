@@ -108,6 +108,13 @@ __device__ __forceinline__ uint4 ldg16(const uint8_t *p) {
         return *reinterpret_cast<const uint4 *>(p);
     }
 }
+// one 16-B flow-table slot in a single dwordx4 load (a uint4 member-wise load
+// lets the compiler split off .w, test it, then load .xyz: two round trips)
+__device__ __forceinline__ uint4 ld_slot(const uint4 *p) {
+    const rx_u32x4 v = *reinterpret_cast<const rx_u32x4 *>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
     const rx_u32x4 w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(p));
@@ -292,7 +299,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
         const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
         slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
         sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-        if (probe[f] && gl < RX_WINDOW) sl[f] = (udp ? ft.udp : ft.tcp)[(slot[f] + gl) & mask];
+        if (probe[f] && gl < RX_WINDOW) sl[f] = ld_slot((udp ? ft.udp : ft.tcp) + ((slot[f] + gl) & mask));
         flow[f] = RXG_FLOW_NONE;
     }
 #pragma unroll
@@ -319,7 +326,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             }
             b = (b + RX_WINDOW) & mask;
             s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
-            if (gl < RX_WINDOW) s = tbl[(b + gl) & mask];
+            if (gl < RX_WINDOW) s = ld_slot(tbl + ((b + gl) & mask));
         }
         if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
             flow[f] = ft.listen[dport[f]];
@@ -606,7 +613,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
         uint32_t i = rx_hash3(ka, kb, kc) & mask;
         for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) { // ~1.2 trips expected
-            const uint4 sl = tbl[i];
+            const uint4 sl = ld_slot(tbl + i);
             if (sl.w == RX_SLOT_EMPTY) break;
             if (sl.x == ka && sl.y == kb && sl.z == kc) {
                 flow = sl.w;
