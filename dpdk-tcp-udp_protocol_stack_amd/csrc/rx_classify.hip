@@ -518,11 +518,11 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 // the bulk bytes of trip t+1 are in flight across the probe latency of trip t.
 // ABL (diagnostic builds only, never selected automatically): 1 = no bucket
 // probe, 4 = no verdict store, 8 = no checksum arithmetic.
-template <int ABL = 0, bool ST_NT = true, bool NTL = true>
-__device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
-                                             const rx_ft_dev &ft, uint4 *__restrict__ out,
-                                             unsigned long long *__restrict__ counts,
-                                             uint32_t *hist, uint32_t lds_bins) {
+// Verdict of one lane-owned frame (everything but the store): returns the
+// 16-B verdict and the per-flow count slot (~0u = not counted).
+template <int ABL = 0, bool NTL = true>
+__device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, const rx_ft_dev &ft,
+                                              uint32_t *count_idx) {
     const int32_t cp = L.cap;
     if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
 #pragma unroll
@@ -642,25 +642,49 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         rc = RXG_RC_KNI;
     }
     if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
+    uint4 v;
+    v.x = flow;
+    v.y = (poff & 0xFFFFu) | (plen << 16);
+    v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+    v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+    *count_idx = (L.valid && rc == RXG_RC_OK && flow != RXG_FLOW_NONE)
+                     ? (is_tcp ? ft.nu : 0u) + flow
+                     : 0xFFFFFFFFu;
+    return v;
+}
+
+__device__ __forceinline__ void lane_count(uint32_t idx, unsigned long long *__restrict__ counts,
+                                           uint32_t *hist, uint32_t lds_bins) {
+    if (counts && idx != 0xFFFFFFFFu) {
+        if (lds_bins)
+            atomicAdd(&hist[idx], 1u);
+        else
+            atomicAdd(&counts[idx], 1ull);
+    }
+}
+
+template <bool ST_NT>
+__device__ __forceinline__ void lane_store(uint4 *__restrict__ out, uint64_t p, uint4 v) {
+    if constexpr (ST_NT)
+        stg16(&out[p], v);
+    else
+        out[p] = v;
+}
+
+// the original one-shot form: verdict, store, count
+template <int ABL = 0, bool ST_NT = true, bool NTL = true>
+__device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
+                                             const rx_ft_dev &ft, uint4 *__restrict__ out,
+                                             unsigned long long *__restrict__ counts,
+                                             uint32_t *hist, uint32_t lds_bins) {
+    uint32_t idx;
+    const uint4 v = lane_verdict<ABL, NTL>(L, next, ft, &idx);
     if (L.valid) {
-        uint4 v;
-        v.x = flow;
-        v.y = (poff & 0xFFFFu) | (plen << 16);
-        v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-        v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
         if (ABL & 4)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-        else if (ST_NT)
-            stg16(&out[L.p], v);
         else
-            out[L.p] = v;
-        if (counts && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) {
-            const uint32_t idx = (is_tcp ? ft.nu : 0u) + flow;
-            if (lds_bins)
-                atomicAdd(&hist[idx], 1u);
-            else
-                atomicAdd(&counts[idx], 1ull);
-        }
+            lane_store<ST_NT>(out, L.p, v);
+        lane_count(idx, counts, hist, lds_bins);
     }
 }
 
@@ -681,7 +705,37 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     }
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
-    if constexpr (PIPE == 0) {
+    if constexpr (PIPE == 9) {
+        // issue order per trip t: frame(t) loads, descriptors(t+1), the
+        // deferred verdict store of t-1, then wait for frame(t) only.  The
+        // store ack and descriptor latency overlap the frame latency; the
+        // probe loop's waits drain everything before the next trip.
+        uint64_t base = (uint64_t)blockIdx.x * 256;
+        lane_frame L;
+        if (base < n) lane_desc(L, p, n, pkts, off, len, unit_log2);
+        uint4 pend = make_uint4(0, 0, 0, 0);
+        uint64_t pend_p = 0;
+        bool pend_valid = false;
+        for (; base < n; base += stride, p += stride) {
+            lane_load<NTL>(L);
+            const uint64_t np = p + stride;
+            const bool nvalid = np < n;
+            const uint64_t nq = nvalid ? np : 0;
+            const uint32_t noff = off[nq];
+            const uint16_t nlen = len[nq];
+            if (pend_valid) lane_store<ST_NT>(out, pend_p, pend);
+            uint32_t idx;
+            pend = lane_verdict<ABL, NTL>(L, nullptr, ft, &idx);
+            pend_p = L.p;
+            pend_valid = L.valid;
+            lane_count(idx, counts, hist, lds_bins);
+            L.p = np;
+            L.valid = nvalid;
+            L.fb = pkts + ((uint64_t)noff << unit_log2);
+            L.cap = nvalid ? (int32_t)nlen : 0;
+        }
+        if (pend_valid) lane_store<ST_NT>(out, pend_p, pend);
+    } else if constexpr (PIPE == 0) {
         for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2);
@@ -791,7 +845,8 @@ struct variant_entry {
 // g = 1 (one frame per lane): p = 4 chunks up front, pipe = prefetch mode
 // (0 none, 1 descriptors + frame one trip ahead, 2 = 1 capped at 6 waves/SIMD,
 // 3 descriptors only, 4 = 0 with plain verdict stores, 5/6 = 0/4 with plain
-// frame loads, 7/8 = 1/2 with plain frame loads); g >= 4: pipe 0/1 = no /
+// frame loads, 7/8 = 1/2 with plain frame loads, 9/10 = ordered one-trip
+// descriptor prefetch + deferred store, nt / plain store); g >= 4: pipe 0/1 = no /
 // one-trip pipeline, 2/3 = 0/1 with plain frame loads; pipe >= 100 are
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
@@ -803,6 +858,7 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 4, launch_lane<0, 0, false>},
     {1, 4, 1, 6, launch_lane<0, 0, false, false>},
     {1, 4, 1, 7, launch_lane<1, 0, true, false>}, {1, 4, 1, 8, launch_lane<2, 0, true, false>},
+    {1, 4, 1, 9, launch_lane<9, 0, true, false>}, {1, 4, 1, 10, launch_lane<9, 0, false, false>},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {4, 1, 1, 1, launch_v<4, 1, 1, 1>},    {4, 1, 1, 0, launch_v<4, 1, 1, 0>},
