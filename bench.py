@@ -269,6 +269,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; "
+                    "gloo only to rehearse N > 1 on one GPU)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
@@ -278,10 +280,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.backend != "nccl":  # rehearsal: ranks may share a GPU
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(a.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
