@@ -56,16 +56,29 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     ln = torch.empty(n, dtype=torch.int16, device=dev)
     out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     counts = torch.zeros(max(nflows, 1), dtype=torch.int64, device=dev)
-    step_counts = torch.zeros_like(counts)
+    # N > 1: per-step counts double-buffered; step k's all-reduce runs on the
+    # collective stream while step k+1's kernel runs (drained at step k+2)
+    step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)]
+    pending = [None, None]
     R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
     torch.cuda.synchronize(dev)
     frame_bytes = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item())
     alg_bytes = frame_bytes + 22 * n  # frame + off(4) + len(2) read + verdict(16) written
+    kstep = [0]
+
+    def drain(b):
+        if pending[b] is not None:
+            pending[b].wait()
+            counts.add_(step_counts[b])
+            pending[b] = None
 
     def step(ev=None):
-        tgt = counts if world == 1 else step_counts
+        b = kstep[0] & 1
+        kstep[0] += 1
         if world > 1:
-            step_counts.zero_()
+            drain(b)
+            step_counts[b].zero_()
+        tgt = counts if world == 1 else step_counts[b]
         if ev is not None:
             ev[0].record(stream)
         ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out,
@@ -73,11 +86,15 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            rxdist.allreduce_counts(step_counts, world)
-            counts.add_(step_counts)
+            pending[b] = rxdist.allreduce_counts(step_counts[b], world, async_op=True)
+
+    def drain_all():
+        drain(0)
+        drain(1)
 
     for _ in range(warmup):
         step()
+    drain_all()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     if world > 1:
@@ -86,6 +103,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     t0 = time.perf_counter()
     for k in range(steps):
         step(evs[k])
+    drain_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -102,7 +120,12 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     n_ok = int((rc == 0).sum().item())
     total_steps = warmup + steps
     counted = int(counts.sum().item())
-    expect = n_ok * total_steps if (world == 1 and COUNTS) else None
+    n_ok_all = n_ok
+    if world > 1:  # every rank holds the all-reduced histogram of all ranks' frames
+        t = torch.tensor([n_ok], dtype=torch.int64, device=dev)
+        torch.distributed.all_reduce(t)
+        n_ok_all = int(t.item())
+    expect = n_ok_all * total_steps if COUNTS else None
     kavg = float(np.mean(kms))
     res = dict(
         workload=name, desc=w["desc"], n_per_gpu=n, nflows=nflows,

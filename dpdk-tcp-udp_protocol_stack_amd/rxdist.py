@@ -41,9 +41,11 @@ def gen_cfg(name: str, rank: int = 0, world: int = 1, **over) -> R.GenCfg:
     return R.make_gen_cfg(**kw)
 
 
-def allreduce_counts(counts, world: int):
-    """The single collective of the rx path: per-flow count vector sum."""
+def allreduce_counts(counts, world: int, async_op: bool = False):
+    """The single collective of the rx path: per-flow count vector sum.
+    async_op=True returns the collective's work handle (overlap with the next
+    burst's kernel; .wait() before reusing the buffer), else None."""
     if world > 1:
         import torch.distributed as dist
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
-    return counts
+        return dist.all_reduce(counts, op=dist.ReduceOp.SUM, async_op=async_op)
+    return None

@@ -48,7 +48,8 @@ def _worker(rank, world, port, name, q):
             dp = int.from_bytes(b[36:38], "little") if l4 else 0
             bad += O.rss_hash(sip, dip, sp, dp) % world != rank
         t = torch.from_numpy(cnt.astype(np.int64))
-        rxdist.allreduce_counts(t, world)
+        work = rxdist.allreduce_counts(t, world, async_op=True)
+        work.wait()
         q.put((rank, bad, t.numpy().copy()))
     finally:
         dist.destroy_process_group()
