@@ -18,7 +18,7 @@ void rx_set_bpc_cap(uint32_t cap);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
-                              unsigned long long *counts, hipStream_t s);
+                              unsigned long long *counts, hipStream_t s, uint32_t *ws);
 
 static thread_local std::string g_last_hip;
 
@@ -88,6 +88,8 @@ struct rxg_ctx {
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
+    uint32_t *d_ws = nullptr; // binned-path workspace (16 B + 8 B per frame), grown on demand
+    size_t d_ws_cap = 0;
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
     uint32_t counts_cap = 0;
@@ -197,6 +199,7 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_tcp);
     (void)hipFree(c->d_listen);
     (void)hipFree(c->d_counts);
+    (void)hipFree(c->d_ws);
     (void)hipFree(c->d_pkts);
     (void)hipFree(c->d_off);
     (void)hipFree(c->d_len);
@@ -268,6 +271,12 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
+    if (lanes_per_frame == 0 && pipeline == 20) { // size-class binned path
+        c->tune_g = 0;
+        c->tune_p = c->tune_fpg = 0;
+        c->tune_pipe = 20;
+        return RXG_OK;
+    }
     if (lanes_per_frame && (lanes_per_frame == 2 || lanes_per_frame > 64 ||
                             (lanes_per_frame & (lanes_per_frame - 1))))
         return RXG_EINVAL;
@@ -312,11 +321,15 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     HIPCHK(hipSetDevice(c->device));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
-    if (!g) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
+    if (!g && pipe != 20) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
+    if (g == 0) { // binned path: workspace (sized once per burst size; not inside graph capture)
+        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
+        if (rc) return rc;
+    }
     rx_set_bpc_cap(c->tune_bpc);
     HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
                               reinterpret_cast<unsigned long long *>(d_counts),
-                              (hipStream_t)stream));
+                              (hipStream_t)stream, c->d_ws));
     return RXG_OK;
 }
 
@@ -335,10 +348,14 @@ int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, cons
     HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
-    if (!g) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
+    if (!g && pipe != 20) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
+    if (g == 0) {
+        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
+        if (rc) return rc;
+    }
     rx_set_bpc_cap(c->tune_bpc);
     HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, p, fpg, pipe,
-                              c->ft, c->d_out, c->d_counts, c->stream));
+                              c->ft, c->d_out, c->d_counts, c->stream, c->d_ws));
     HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;

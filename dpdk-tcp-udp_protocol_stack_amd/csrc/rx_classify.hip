@@ -129,7 +129,7 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
 // Frames of one lane group for one trip: descriptors and the first P passes.
 template <int FPG, int P>
 struct group_frames {
-    uint64_t pf[FPG];
+    uint64_t pf[FPG]; // frame index (the verdict slot)
     bool valid[FPG];
     const uint8_t *fb[FPG];
     int32_t cap[FPG];
@@ -140,13 +140,16 @@ template <int G, int FPG, int P>
 __device__ __forceinline__ void group_desc(group_frames<FPG, P> &S, uint64_t tile, uint32_t n,
                                            uint32_t grp, const uint8_t *__restrict__ pkts,
                                            const uint32_t *__restrict__ off,
-                                           const uint16_t *__restrict__ len, uint32_t unit_log2) {
+                                           const uint16_t *__restrict__ len, uint32_t unit_log2,
+                                           const uint32_t *__restrict__ idx = nullptr) {
     constexpr uint32_t GPB = 256 / G;
 #pragma unroll
     for (int f = 0; f < FPG; ++f) {
-        S.pf[f] = tile * (GPB * FPG) + (uint64_t)f * GPB + grp;
-        S.valid[f] = S.pf[f] < n;
-        const uint64_t q = S.valid[f] ? S.pf[f] : 0;
+        const uint64_t pos = tile * (GPB * FPG) + (uint64_t)f * GPB + grp;
+        S.valid[f] = pos < n;
+        const uint64_t pp = S.valid[f] ? pos : 0;
+        const uint64_t q = idx ? (uint64_t)idx[pp] : pp;
+        S.pf[f] = q;
         S.fb[f] = pkts + ((uint64_t)off[q] << unit_log2);
         S.cap[f] = S.valid[f] ? (int32_t)len[q] : 0;
     }
@@ -380,8 +383,10 @@ template <int G, int P, int FPG, int PIPE, bool NTL = true>
 __global__ __launch_bounds__(256) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
-    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
+    const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
     constexpr uint32_t GPB = 256 / G;     // frame groups per block
     constexpr uint32_t TILE = GPB * FPG;  // frames per block per trip
@@ -401,22 +406,22 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     uint64_t tile = blockIdx.x;
     group_frames<FPG, P> A;
     if (tile * TILE < n) {
-        group_desc<G>(A, tile, n, grp, pkts, off, len, unit_log2);
+        group_desc<G>(A, tile, n, grp, pkts, off, len, unit_log2, idx);
         group_load<G, FPG, P, NTL>(A, s0);
     }
     if constexpr (PIPE) {
         group_frames<FPG, P> B;
-        group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
+        group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         for (; tile * TILE < n; tile += gridDim.x) {
             group_load<G, FPG, P, NTL>(B, s0); // no-op lanes past the end (cap 0)
             group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             A = B;
-            group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2);
+            group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         }
     } else {
         for (; tile * TILE < n; tile += gridDim.x) {
             group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
-            group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2);
+            group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
             group_load<G, FPG, P, NTL>(A, s0);
         }
     }
@@ -433,7 +438,8 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
 template <int G, int P, int FPG, int PIPE = 0, bool NTL = true>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
-                    uint32_t lds_bins, hipStream_t s) {
+                    uint32_t lds_bins, hipStream_t s, const uint32_t *idx = nullptr,
+                    const uint32_t *n_dev = nullptr) {
     constexpr uint32_t TILE = (256 / G) * FPG;
     const size_t lds = (size_t)lds_bins * 4u;
     // resident blocks: one wave of blocks, equal shares, no tail (cached per LDS size)
@@ -463,7 +469,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
-                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
+                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
 
@@ -492,13 +498,17 @@ struct lane_frame {
     uint4 c[4];
 };
 
+// p = position in the burst (or in the index list idx, when given); L.p =
+// the frame index the verdict belongs to
 __device__ __forceinline__ void lane_desc(lane_frame &L, uint64_t p, uint32_t n,
                                           const uint8_t *__restrict__ pkts,
                                           const uint32_t *__restrict__ off,
-                                          const uint16_t *__restrict__ len, uint32_t unit_log2) {
-    L.p = p;
+                                          const uint16_t *__restrict__ len, uint32_t unit_log2,
+                                          const uint32_t *__restrict__ idx = nullptr) {
     L.valid = p < n;
-    const uint64_t q = L.valid ? p : 0;
+    const uint64_t pp = L.valid ? p : 0;
+    const uint64_t q = idx ? (uint64_t)idx[pp] : pp;
+    L.p = q;
     L.fb = pkts + ((uint64_t)off[q] << unit_log2);
     L.cap = L.valid ? (int32_t)len[q] : 0;
 }
@@ -696,8 +706,10 @@ template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
 __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
-    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
+    const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
     const uint32_t tid = threadIdx.x;
     if (lds_bins) {
         for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
@@ -738,7 +750,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     } else if constexpr (PIPE == 0) {
         for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
             lane_frame L;
-            lane_desc(L, p, n, pkts, off, len, unit_log2);
+            lane_desc(L, p, n, pkts, off, len, unit_log2, idx);
             lane_load<NTL>(L);
             lane_process<ABL, ST_NT, NTL>(L, nullptr, ft, out, counts, hist, lds_bins);
         }
@@ -800,7 +812,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
 template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
 hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
-                       unsigned long long *counts, uint32_t lds_bins, hipStream_t s) {
+                       unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                       const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
     const size_t lds = (size_t)lds_bins * 4u;
     static int cu = 0;
     static int cached_occ[2] = {0, 0};
@@ -829,13 +842,107 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
-                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
+                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// Size-class binning for mixed-size bursts (IMIX): frame indices split into a
+// small list (len <= thresh) and a large list, so each list runs on the
+// kernel shape that suits it.  Block b owns the contiguous chunk
+// [b*chunk, (b+1)*chunk): pass 1 counts its classes, one atomic per class
+// per block reserves output ranges, pass 2 (len re-read from L2) writes the
+// indices in order.  Lists: small at lists[0..), large at lists[n..) (2n
+// slots); lens[0] = small count, lens[1] = large count.
+__global__ __launch_bounds__(256) void rx_bin_kernel(const uint16_t *__restrict__ len, uint32_t n,
+                                                     uint32_t chunk, uint32_t thresh,
+                                                     uint32_t *__restrict__ lists,
+                                                     uint32_t *__restrict__ lens) {
+    __shared__ uint32_t wsum[2][4];
+    __shared__ uint32_t base[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t c1 = min((uint64_t)n, c0 + chunk);
+    uint32_t my_small = 0, my_large = 0;
+    for (uint64_t i = c0 + tid; i < c1; i += 256) {
+        const bool sm = len[i] <= thresh;
+        my_small += sm;
+        my_large += !sm;
+    }
+    // block totals
+    for (int o = 32; o > 0; o >>= 1) {
+        my_small += __shfl_xor(my_small, o);
+        my_large += __shfl_xor(my_large, o);
+    }
+    if (lane == 0) {
+        wsum[0][wave] = my_small;
+        wsum[1][wave] = my_large;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t ts = wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
+        const uint32_t tl = wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+        base[0] = ts ? atomicAdd(&lens[0], ts) : 0;
+        base[1] = tl ? n + atomicAdd(&lens[1], tl) : 0; // large list: lists[n ...]
+    }
+    __syncthreads();
+    uint32_t run_s = base[0], run_l = base[1];
+    for (uint64_t t0 = c0; t0 < c1; t0 += 256) {
+        const uint64_t i = t0 + tid;
+        const bool v = i < c1;
+        const bool sm = v && len[i] <= thresh;
+        const bool lg = v && !sm;
+        const uint64_t ms = __ballot(sm), ml = __ballot(lg);
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (lane == 0) {
+            wsum[0][wave] = __popcll(ms);
+            wsum[1][wave] = __popcll(ml);
+        }
+        __syncthreads();
+        uint32_t ps = run_s, pl = run_l;
+        for (uint32_t w = 0; w < wave; ++w) {
+            ps += wsum[0][w];
+            pl += wsum[1][w];
+        }
+        if (sm) lists[ps + __popcll(ms & below)] = (uint32_t)i;
+        if (lg) lists[pl + __popcll(ml & below)] = (uint32_t)i;
+        for (uint32_t w = 0; w < 4; ++w) {
+            run_s += wsum[0][w];
+            run_l += wsum[1][w];
+        }
+        __syncthreads();
+    }
+}
+
+// binned path: bin, then the lane kernel over the small list and the G=8
+// kernel over the large list (both read frame indices through the list)
+static hipError_t launch_binned(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                                uint32_t n, uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                                unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                                uint32_t *ws) {
+    if (!ws) return hipErrorInvalidValue;
+    uint32_t *lens = ws, *lists = ws + 4;
+    hipError_t e = hipMemsetAsync(lens, 0, 16, s);
+    if (e != hipSuccess) return e;
+    const uint32_t chunk = 16384;
+    const uint32_t blocks = (uint32_t)(((uint64_t)n + chunk - 1) / chunk);
+    hipLaunchKernelGGL(rx_bin_kernel, dim3(blocks), dim3(256), 0, s, len, n, chunk, 64u, lists,
+                       lens);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t user_cap = g_bpc_cap;
+    if (!user_cap) g_bpc_cap = 6;
+    e = launch_lane<0, 0, true, false>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
+                                        lists, lens);
+    g_bpc_cap = user_cap;
+    if (e != hipSuccess) return e;
+    return launch_v<8, 2, 1, 1>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
+                                lists + n, lens + 1);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t *, const uint32_t *, const uint16_t *, uint32_t,
                                 uint32_t, const rx_ft_dev &, uint4 *, unsigned long long *,
-                                uint32_t, hipStream_t);
+                                uint32_t, hipStream_t, const uint32_t *, const uint32_t *);
 struct variant_entry {
     uint32_t g, p, fpg, pipe;
     launch_fn fn;
@@ -884,8 +991,8 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B
         *g = 1, *p = 4, *fpg = 1, *pipe = 5;
-    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4)
-        *g = 8, *p = 2, *fpg = 1, *pipe = 1;
+    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): size-class binned
+        *g = 0, *p = 0, *fpg = 0, *pipe = 20;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B)
@@ -898,16 +1005,19 @@ void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
-                              unsigned long long *counts, hipStream_t s) {
+                              unsigned long long *counts, hipStream_t s, uint32_t *ws) {
     if (n == 0) return hipSuccess;
     const uint32_t nflows = ft.nu + ft.nt;
     const uint32_t lds_bins = (counts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
+    if (g == 0 && pipe == 20) // size-class binned (workspace: 16 B + 8 B per frame)
+        return launch_binned(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s, ws);
     for (const variant_entry &v : k_variants)
         if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
             (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
             const uint32_t user_cap = g_bpc_cap;
             if (!user_cap) g_bpc_cap = v.bpc;
-            hipError_t e = v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s);
+            hipError_t e = v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s, nullptr,
+                                nullptr);
             g_bpc_cap = user_cap;
             return e;
         }

@@ -50,7 +50,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 1, 3), (4, 1, 2, 2), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
                    (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
-                   (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1)]
+                   (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1),
+                   (0, 0, 0, 20)]  # size-class binned: lane kernel + G=8 kernel
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
