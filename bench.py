@@ -206,13 +206,15 @@ def e2e(name, local, batch, reps=20):
     per burst (no overlap between bursts).  Reported in DESIGN.md, never as value."""
     w = rxdist.WORKLOADS[name]
     cfg = rxdist.gen_cfg(name)
-    span = batch * cfg.slot_bytes
+    hp, ho, hl = R.gen_host(cfg, 0, batch, w["unit_log2"])
+    # bytes the burst occupies (the packed layout ends before batch * slot_bytes)
+    span = (int(ho[-1]) << w["unit_log2"]) + ((int(hl[-1]) + 63) & ~63) if cfg.packed \
+        else batch * cfg.slot_bytes
     pk = torch.empty(span + 64, dtype=torch.uint8).pin_memory()
     off = torch.empty(batch, dtype=torch.int32).pin_memory()
     ln = torch.empty(batch, dtype=torch.int16).pin_memory()
     out = torch.empty(batch * 16, dtype=torch.uint8).pin_memory()
-    hp, ho, hl = R.gen_host(cfg, 0, batch, w["unit_log2"])
-    pk.numpy()[:span] = hp
+    pk.numpy()[:span] = hp[:span]
     off.numpy().view(np.uint32)[:] = ho
     ln.numpy().view(np.uint16)[:] = hl
     ctx = R.Context(local, max_pkts=batch, max_bytes=span + 64)
@@ -255,6 +257,16 @@ def sweep(ctx, names, steps, warmup, dev, only=""):
         R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
         torch.cuda.synchronize(dev)
         alg = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item()) + 22 * n
+        ok = []
+        for v in variants:  # drop variants that are not compiled in
+            ctx.tune(*v[:4])
+            try:
+                ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                                 stream=sh)
+                ok.append(v)
+            except R.RxgError as e:
+                log(f"sweep {nm} variant={v}: skipped ({e})")
+        variants = ok
         times = {v: [] for v in variants}
         for rnd in range(5):
             for v in variants:

@@ -271,10 +271,10 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
-    if (lanes_per_frame == 0 && pipeline == 20) { // size-class binned path
-        c->tune_g = 0;
+    if (lanes_per_frame == 0 && (pipeline == 20 || (pipeline >= 30 && pipeline <= 32))) {
+        c->tune_g = 0; // size-class binned path (20) / stream kernel (30..32)
         c->tune_p = c->tune_fpg = 0;
-        c->tune_pipe = 20;
+        c->tune_pipe = pipeline;
         return RXG_OK;
     }
     if (lanes_per_frame && (lanes_per_frame == 2 || lanes_per_frame > 64 ||
@@ -321,8 +321,8 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     HIPCHK(hipSetDevice(c->device));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
-    if (!g && pipe != 20) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
-    if (g == 0) { // binned path: workspace (sized once per burst size; not inside graph capture)
+    if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
+    if (g == 0 && pipe == 20) { // binned path: workspace (sized once per burst size; not inside graph capture)
         int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
         if (rc) return rc;
     }
@@ -348,8 +348,8 @@ int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, cons
     HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
-    if (!g && pipe != 20) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
-    if (g == 0) {
+    if (!g && pipe == ~0u) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
+    if (g == 0 && pipe == 20) {
         int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
         if (rc) return rc;
     }

@@ -940,6 +940,313 @@ static hipError_t launch_binned(const uint8_t *pkts, const uint32_t *off, const 
                                 lists + n, lens + 1);
 }
 
+// ---------------------------------------------------------------------------
+// Stream kernel: frame heads lane-owned, frame tails streamed by the block.
+//   A block takes 256 consecutive frames, one per thread.  Head phase: thread
+//   t loads its descriptor and its frame's first 64 B, decodes, sums the
+//   checksum words of [26, min(e, 64)) (e = checksum end) and probes the flow
+//   table (speculatively for TCP: a bad checksum discards the hit, as the
+//   reference never looks one up).  Tail phase: the block streams the byte span
+//   that covers every frame's full tail chunks [64, e & ~15) as contiguous 16-B
+//   chunks (each wave instruction loads 1 KiB of consecutive bytes whatever
+//   the frame sizes), forms the exclusive prefix sum E(c) of the per-chunk word
+//   sums tile by tile (DPP wave scans + 16 wave totals through LDS), and each
+//   frame takes E(ce) - E(cs) from the tiles holding its boundary chunks, plus
+//   its last partial chunk loaded and masked by its own thread.  Prefix
+//   differences are exact mod 2^32 and a frame's tail sum is < 2^32, so bytes
+//   between frames cost bandwidth only, never correctness.  A block whose span
+//   is far larger than its tails (frames scattered over the buffer) falls back
+//   to per-thread tail loops: correct for any layout, fast for ordered ones
+//   (packed bursts, fixed slots).
+constexpr uint32_t ST_TILE = 1024; // chunks per block trip (16 KiB)
+
+// inclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true); // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true); // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true); // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true); // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1,3
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2,3
+    return x;
+}
+
+__device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
+    return add_halves(add_halves(add_halves(add_halves(0u, v.x), v.y), v.z), v.w);
+}
+
+// EARLY: the span comes from the descriptors (tails end before caplen), so
+// the first tile's loads are in flight while the heads are decoded and probed;
+// otherwise from the decoded checksum ends (tighter span, later start).
+template <bool NTS, bool EARLY>
+__global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
+    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
+    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][ST_TILE];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16]; // [row j][wave w]
+    __shared__ unsigned long long s_lo, s_hi;
+    __shared__ uint32_t s_tail;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (tid == 0) {
+        s_lo = ~0ull;
+        s_hi = 0;
+        s_tail = 0;
+    }
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
+    const bool valid = p < n;
+    const uint64_t q = valid ? p : 0;
+    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
+    const uint8_t *fb = pkts + fpos;
+    const int32_t cp = valid ? (int32_t)len[q] : 0;
+
+    // block span of the tail chunks; a span far larger than the tails means
+    // scattered frames (per-thread fallback below)
+    auto block_span = [&](bool t, uint64_t clo, uint64_t chi) {
+        __syncthreads(); // s_lo/s_hi/s_tail initialised
+        if (t) {
+            atomicMin(&s_lo, (unsigned long long)clo);
+            atomicMax(&s_hi, (unsigned long long)chi);
+            atomicAdd(&s_tail, (uint32_t)(chi - clo));
+        }
+        __syncthreads();
+    };
+    uint64_t lo = 0, hi = 0;
+    uint32_t span = 0;
+    bool streamed = false;
+    uint4 v[4];
+    if constexpr (EARLY) {
+        const int32_t cf = cp & ~15;
+        block_span(cf > 64, (fpos + 64) >> 4, (fpos + (uint32_t)cf) >> 4);
+        lo = s_lo, hi = s_hi;
+        const uint32_t tsum = s_tail;
+        streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
+        span = streamed ? (uint32_t)(hi - lo) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = j * 256 + tid;
+            v[j] = k < span ? ldg16<NTS>(pkts + ((lo + k) << 4)) : make_uint4(0, 0, 0, 0);
+        }
+    }
+
+    // ---- head phase -------------------------------------------------------
+    uint4 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        c[j] = make_uint4(0, 0, 0, 0);
+        if (16 * j < cp) c[j] = ldg16<false>(fb + 16 * j);
+    }
+    if (cp < 64) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp);
+    }
+    const uint32_t et = c[0].w & 0xFFFFu;
+    const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
+    const uint32_t proto = c[1].y >> 24;
+    const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
+    const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
+    const uint32_t sport = c[2].x >> 16;
+    const uint32_t dport = c[2].y & 0xFFFFu;
+    const uint32_t dgl = rx_bswap16(c[2].y >> 16);
+    const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+    uint32_t cl, nd;
+    if (et == 0x0608u) {
+        cl = RXG_CLS_ARP;
+        nd = 42;
+    } else if (et != 0x0008u) {
+        cl = RXG_CLS_NON_IP;
+        nd = 14;
+    } else if (proto == 17u) {
+        cl = RXG_CLS_UDP;
+        nd = 42;
+    } else if (proto == 6u) {
+        cl = RXG_CLS_TCP;
+        nd = 54;
+    } else {
+        cl = RXG_CLS_IPV4_OTHER;
+        nd = 24;
+    }
+    const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+    const bool l4 = is_udp || is_tcp;
+    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+    const bool do_sum = l4 && tl >= 20u;
+    if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+    int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+    if (e > cp) e = cp;
+    uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+    h1.x = 0;
+    h1.y = 0;
+    h1.z &= 0xFFFF0000u;
+    if (is_udp) h2.z &= 0xFFFF0000u;
+    if (is_tcp) h3.x &= 0x0000FFFFu;
+    uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
+    acc = lane_chunk_sum(acc, h2, 32, e);
+    acc = lane_chunk_sum(acc, h3, 48, e);
+    const int32_t ef = e & ~15; // full tail chunks: [64, ef)
+    if (ef < e && ef >= 64) acc = lane_chunk_sum(acc, ldg16<false>(fb + ef), ef, e);
+    const bool tail = ef > 64;
+    const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
+    if constexpr (!EARLY) {
+        block_span(tail, cs_abs, ce_abs);
+        lo = s_lo, hi = s_hi;
+        const uint32_t tsum = s_tail;
+        streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
+        span = streamed ? (uint32_t)(hi - lo) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = j * 256 + tid;
+            v[j] = k < span ? ldg16<NTS>(pkts + ((lo + k) << 4)) : make_uint4(0, 0, 0, 0);
+        }
+    }
+
+    // flow probe (UDP always, TCP speculatively)
+    uint32_t flow = RXG_FLOW_NONE;
+    if (valid && l4) {
+        const uint32_t ka = is_udp ? dip : sip;
+        const uint32_t kb = is_udp ? dport : dip;
+        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+        const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
+        const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
+        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        uint32_t i = rx_hash3(ka, kb, kc) & mask;
+        for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) {
+            const uint4 sl = ld_slot(tbl + i);
+            if (sl.w == RX_SLOT_EMPTY) break;
+            if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                flow = sl.w;
+                break;
+            }
+        }
+        if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
+    }
+
+    // ---- tail phase -------------------------------------------------------
+    if (streamed) {
+        const uint8_t *sb = pkts + (lo << 4);
+        const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
+        const uint32_t ce = tail ? (uint32_t)(ce_abs - lo) : 0xFFFFFFFFu;
+        uint32_t es = 0, ee = 0, carry = 0;
+        uint32_t buf = 0;
+        for (uint32_t c0 = 0; c0 < span; c0 += ST_TILE, buf ^= 1u) {
+            uint4 nv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { // next tile in flight across this one's scan
+                const uint32_t k = c0 + ST_TILE + j * 256 + tid;
+                nv[j] = k < span ? ldg16<NTS>(sb + ((uint64_t)k << 4)) : make_uint4(0, 0, 0, 0);
+            }
+            uint32_t sj[4], xj[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sj[j] = chunk_sum(v[j]);
+                xj[j] = wave_incl_scan(sj[j]);
+            }
+            if (lane == 63) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+            }
+            __syncthreads();
+            uint32_t wt[16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
+                wt[j * 4 + 0] = r.x, wt[j * 4 + 1] = r.y, wt[j * 4 + 2] = r.z, wt[j * 4 + 3] = r.w;
+            }
+            uint32_t base = carry;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t wb = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
+                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
+                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
+            }
+            carry = base;
+            __syncthreads();
+            if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
+            if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = nv[j];
+        }
+        if (ce == span) ee = carry;
+        if (tail) acc += ee - es;
+    } else if (tail) { // scattered frames: this thread sums its own tail
+        for (int32_t s = 64; s < ef; s += 64) {
+            uint4 r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                r[u] = make_uint4(0, 0, 0, 0);
+                if (s + 16 * u < ef) r[u] = ldg16<false>(fb + s + 16 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += chunk_sum(r[u]);
+        }
+    }
+
+    // ---- verdict ----------------------------------------------------------
+    uint32_t ck = 0;
+    if (do_sum) {
+        acc += proto << 8;
+        acc += rx_bswap16(l4n);
+        ck = (~fold16(acc)) & 0xFFFFu;
+        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+    }
+    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+    const bool ok = l4 && stored == ck;
+    if (is_tcp && !ok) flow = RXG_FLOW_NONE;
+    int32_t rc;
+    uint32_t poff = 0, plen = 0, flags = 0;
+    if (is_udp) {
+        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                   : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        poff = 42;
+        plen = dgl > 8u ? dgl - 8u : 0u;
+        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+    } else if (is_tcp) {
+        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+        poff = 34u + 4u * hl;
+        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+        plen = pl < 0 ? 0u : (uint32_t)pl;
+        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+    } else {
+        rc = RXG_RC_KNI;
+    }
+    if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
+    if (valid) {
+        uint4 vd;
+        vd.x = flow;
+        vd.y = (poff & 0xFFFFu) | (plen << 16);
+        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+        stg16(&out[p], vd);
+        if (rc == RXG_RC_OK && flow != RXG_FLOW_NONE)
+            lane_count((is_tcp ? ft.nu : 0u) + flow, counts, hist, lds_bins);
+    }
+    if (lds_bins) {
+        __syncthreads();
+        for (uint32_t i = tid; i < lds_bins; i += 256) {
+            const uint32_t cnt = hist[i];
+            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
+        }
+    }
+}
+
+template <bool NTS, bool EARLY = true>
+hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                         uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                         unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                         const uint32_t *, const uint32_t *) {
+    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, EARLY>), dim3((uint32_t)blocks), dim3(256),
+                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
+                       lds_bins);
+    return hipGetLastError();
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t *, const uint32_t *, const uint16_t *, uint32_t,
                                 uint32_t, const rx_ft_dev &, uint4 *, unsigned long long *,
                                 uint32_t, hipStream_t, const uint32_t *, const uint32_t *);
@@ -979,6 +1286,10 @@ static const variant_entry k_variants[] = {
     {32, 3, 1, 0, launch_v<32, 3, 1, 0>},  {32, 2, 1, 1, launch_v<32, 2, 1, 1>},
     {64, 4, 1, 0, launch_v<64, 4, 1, 0>},  {64, 2, 1, 0, launch_v<64, 2, 1, 0>},
     {64, 2, 1, 1, launch_v<64, 2, 1, 1>},
+    // g = 0: stream kernel (head per lane, tails streamed per block); pipe 30 nt
+    // tail loads, 31 plain, 32 = 30 with the span from the decoded heads
+    {0, 1, 1, 30, launch_stream<true>},    {0, 1, 1, 31, launch_stream<false>},
+    {0, 1, 1, 32, launch_stream<true, false>},
 };
 
 } // namespace
@@ -991,8 +1302,8 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B
         *g = 1, *p = 4, *fpg = 1, *pipe = 5;
-    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): size-class binned
-        *g = 0, *p = 0, *fpg = 0, *pipe = 20;
+    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel
+        *g = 0, *p = 0, *fpg = 0, *pipe = 30;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B)

@@ -3,6 +3,7 @@
 // and the device kernel call the same rx_common.h code, so any subset of a
 // device-generated burst can be regenerated on the CPU.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "rx_common.h"
@@ -21,15 +22,30 @@ RX_HD uint32_t gen_one(const rxg_gen_cfg &cfg, uint64_t i, uint32_t *dst, uint32
     return pl.len;
 }
 
+// frame t of the burst: written at the offset off_in[t] (packed layout) or
+// at t * slot_bytes
 __global__ void rx_gen_kernel(rxg_gen_cfg cfg, uint64_t first, uint32_t n, uint8_t *pkts,
-                              uint32_t *off, uint16_t *len, uint32_t unit_log2) {
+                              uint32_t *off, uint16_t *len, uint32_t unit_log2,
+                              const uint32_t *off_in) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const uint64_t base = t * (uint64_t)cfg.slot_bytes;
+    const uint64_t base = off_in ? ((uint64_t)off_in[t] << unit_log2) : t * (uint64_t)cfg.slot_bytes;
     const uint32_t l = gen_one(cfg, first + t, reinterpret_cast<uint32_t *>(pkts + base),
                                cfg.slot_bytes / 4);
     off[t] = (uint32_t)(base >> unit_log2);
     len[t] = (uint16_t)l;
+}
+
+// packed layout offsets (units of 1 << unit_log2, each frame 64-B aligned)
+static uint64_t packed_offsets(const rxg_gen_cfg &cfg, uint64_t first, uint32_t n,
+                               uint32_t unit_log2, uint32_t *off) {
+    uint64_t pos = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        off[t] = (uint32_t)(pos >> unit_log2);
+        const uint32_t l = rx_gen_len(cfg, first + t);
+        pos += ((uint64_t)(l < 60 ? 60 : l) + 63) & ~63ull;
+    }
+    return pos;
 }
 
 int check_cfg(const rxg_gen_cfg *cfg, uint32_t unit_log2) {
@@ -41,6 +57,7 @@ int check_cfg(const rxg_gen_cfg *cfg, uint32_t unit_log2) {
     if (maxlen < 64 || maxlen > 65535 || maxlen > cfg->slot_bytes) return RXG_EINVAL;
     if (cfg->n_udp == 0 && cfg->n_tcp == 0) return RXG_EINVAL;
     if (cfg->n_shards > 1 && cfg->shard >= cfg->n_shards) return RXG_EINVAL;
+    if (cfg->packed > 1 || (cfg->packed && unit_log2 > 6)) return RXG_EINVAL;
     if (cfg->n_udp && (uint32_t)cfg->udp_base_port + cfg->n_udp > 65536u) return RXG_EINVAL;
     if (cfg->n_udp && cfg->udp_base_port <= 7 && cfg->udp_base_port + cfg->n_udp > 7)
         return RXG_EINVAL; // :7 is the generator's "unknown flow" port
@@ -88,8 +105,10 @@ extern "C" int rxg_gen_host(const rxg_gen_cfg *cfg, uint64_t first, uint32_t n, 
     int rc = check_cfg(cfg, off_unit_log2);
     if (rc) return rc;
     if (n && (!pkts || !off || !len)) return RXG_EINVAL;
+    if (cfg->packed) packed_offsets(*cfg, first, n, off_unit_log2, off);
     for (uint32_t t = 0; t < n; ++t) {
-        const uint64_t base = (uint64_t)t * cfg->slot_bytes;
+        const uint64_t base =
+            cfg->packed ? ((uint64_t)off[t] << off_unit_log2) : (uint64_t)t * cfg->slot_bytes;
         uint32_t l = gen_one(*cfg, first + t, reinterpret_cast<uint32_t *>(pkts + base),
                              cfg->slot_bytes / 4);
         off[t] = (uint32_t)(base >> off_unit_log2);
@@ -108,7 +127,25 @@ extern "C" int rxg_gen_dev(const rxg_gen_cfg *cfg, uint64_t first, uint32_t n, u
     if (((uint64_t)n * cfg->slot_bytes - 1) >> off_unit_log2 > 0xFFFFFFFFull) return RXG_ERANGE;
     const uint32_t threads = 256;
     const uint32_t blocks = (n + threads - 1) / threads;
+    uint32_t *d_off_in = nullptr;
+    if (cfg->packed) { // offsets: host prefix sum of the (RNG-determined) frame sizes
+        uint32_t *h = (uint32_t *)malloc((size_t)n * 4);
+        if (!h) return RXG_ENOMEM;
+        packed_offsets(*cfg, first, n, off_unit_log2, h);
+        hipError_t e = hipMalloc(&d_off_in, (size_t)n * 4);
+        if (e == hipSuccess) e = hipMemcpy(d_off_in, h, (size_t)n * 4, hipMemcpyHostToDevice);
+        free(h);
+        if (e != hipSuccess) {
+            (void)hipFree(d_off_in);
+            return rx_set_hip_error(e);
+        }
+    }
     hipLaunchKernelGGL(rx_gen_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, *cfg,
-                       first, n, d_pkts, d_off, d_len, off_unit_log2);
+                       first, n, d_pkts, d_off, d_len, off_unit_log2, d_off_in);
+    if (d_off_in) {
+        hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+        (void)hipFree(d_off_in);
+        if (e != hipSuccess) return rx_set_hip_error(e);
+    }
     return rx_set_hip_error(hipGetLastError());
 }

@@ -21,10 +21,12 @@ WORKLOADS = {
     "cfg3": dict(desc="1500B TCP/IPv4, 4096 tcbs + listener, 4M frames/GPU", n=4 << 20,
                  unit_log2=6, len_hint=1500,
                  gen=dict(frame_len=1500, slot_bytes=1536, proto_mode=1, n_udp=0, n_tcp=4096)),
-    # BASELINE configs[3]: IMIX 64/576/1500 at 7:4:1, TCP/UDP 50/50, 64K flows
-    "cfg4": dict(desc="IMIX 64/576/1500 (7:4:1), TCP+UDP, 65536 flows, 16M frames/GPU",
+    # BASELINE configs[3]: IMIX 64/576/1500 at 7:4:1, TCP/UDP 50/50, 64K flows; frames
+    # packed at 64-B alignment (the layout the host staging path produces)
+    "cfg4": dict(desc="IMIX 64/576/1500 (7:4:1), TCP+UDP, 65536 flows, 16M frames/GPU, packed",
                  n=16 << 20, unit_log2=6, len_hint=354,
-                 gen=dict(size_mode=1, slot_bytes=1536, proto_mode=2, n_udp=32768, n_tcp=32767)),
+                 gen=dict(size_mode=1, slot_bytes=1536, proto_mode=2, n_udp=32768, n_tcp=32767,
+                          packed=1)),
     # BASELINE configs[4]: 10M x 9000 B TCP over 8 GPUs (1.25M/GPU), 1M tcbs
     "cfg5": dict(desc="9000B TCP jumbo, 1M tcbs, 1.25M frames/GPU (10M over 8 GPUs)",
                  n=1250000, unit_log2=6, len_hint=9000,

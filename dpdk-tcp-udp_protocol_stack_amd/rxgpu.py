@@ -51,7 +51,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
                    (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1),
-                   (0, 0, 0, 20)]  # size-class binned: lane kernel + G=8 kernel
+                   (0, 0, 0, 20),  # size-class binned: lane kernel + G=8 kernel
+                   (0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32)]  # stream kernel
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -72,7 +73,7 @@ class GenCfg(C.Structure):
         ("n_tcp", C.c_uint32), ("local_ip", C.c_uint32), ("udp_base_port", C.c_uint16),
         ("tcp_port", C.c_uint16), ("bad_cksum_per10k", C.c_uint32),
         ("unknown_per10k", C.c_uint32), ("other_per10k", C.c_uint32), ("shard", C.c_uint32),
-        ("n_shards", C.c_uint32),
+        ("n_shards", C.c_uint32), ("packed", C.c_uint32),
     ]
 
 
@@ -259,7 +260,8 @@ def rss_hash(sip: int, dip: int, sport: int, dport: int) -> int:
 def make_gen_cfg(**kw) -> GenCfg:
     d = dict(seed=0x5EED0001, size_mode=0, frame_len=64, slot_bytes=64, proto_mode=0, n_udp=1024,
              n_tcp=0, local_ip=ip_raw("192.168.100.77"), udp_base_port=20000, tcp_port=9999,
-             bad_cksum_per10k=100, unknown_per10k=50, other_per10k=50, shard=0, n_shards=1)
+             bad_cksum_per10k=100, unknown_per10k=50, other_per10k=50, shard=0, n_shards=1,
+             packed=0)
     d.update(kw)
     return GenCfg(**d)
 

@@ -201,8 +201,8 @@ uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport
 
 /* ---- synthetic traffic (pktgen) --------------------------------------- */
 /* Deterministic counter-based generator: frame i is a pure function of
- * (cfg, i), identical on host and device. Frames are written at
- * off[i] = i * (slot_bytes >> off_unit_log2). */
+ * (cfg, i), identical on host and device.  Frames are written at
+ * off[i] = i * (slot_bytes >> off_unit_log2), or packed (cfg.packed). */
 typedef struct rxg_gen_cfg {
     uint64_t seed;
     uint32_t size_mode;     /* 0 fixed frame_len, 1 IMIX 64/576/1500 at 7:4:1 */
@@ -219,11 +219,15 @@ typedef struct rxg_gen_cfg {
     uint32_t other_per10k;     /* ICMP or ARP frames */
     uint32_t shard;         /* keep only tuples whose rxg_rss_hash % n_shards == shard */
     uint32_t n_shards;      /* 1 = no sharding */
+    uint32_t packed;        /* 0: frame i in slot i (slot_bytes apart); 1: frames packed
+                               back to back at 64-B alignment (what rxg_process_mbufs
+                               staging produces); slot_bytes then bounds one frame */
 } rxg_gen_cfg;
 
 /* Flow set the generator assumes (the sockets/tcbs a test or bench binds). */
 int rxg_gen_flows(const rxg_gen_cfg *cfg, rxg_udp_sock *u, rxg_tcb *t);
-/* Host generation of frames [first, first+n) into caller buffers (slot i-first). */
+/* Host generation of frames [first, first+n) into caller buffers (slot i-first;
+ * the buffer must hold n * slot_bytes bytes in either layout). */
 int rxg_gen_host(const rxg_gen_cfg *cfg, uint64_t first, uint32_t n, uint8_t *pkts,
                  uint32_t *off, uint16_t *len, uint32_t off_unit_log2);
 /* Device generation (same frames), asynchronous on stream. */

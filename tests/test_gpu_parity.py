@@ -128,6 +128,7 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
     torch.cuda.synchronize(dev)
     assert np.array_equal(d_pk.cpu().numpy()[:len(pk)], pk)
     assert np.array_equal(d_ln.cpu().numpy().view(np.uint16), ln)
+    assert np.array_equal(d_off.cpu().numpy().view(np.uint32), off)
     want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, w["unit_log2"], counts=True)
     for hint in sorted({w["len_hint"], 64, 1500}):
         got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, w["unit_log2"], hint, counts=True)
@@ -142,7 +143,8 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     frames = F.read_pcap(os.path.join(GOLD, "edge.pcap"))
     cfg = rxdist.gen_cfg("cfg4", n_udp=64, n_tcp=64)
     pk, off, ln = R.gen_host(cfg, 0, 700, 6)
-    frames = frames + [pk[i * 1536:i * 1536 + int(ln[i])].tobytes() for i in range(700)]
+    frames = frames + [pk[(int(off[i]) << 6):(int(off[i]) << 6) + int(ln[i])].tobytes()
+                       for i in range(700)]
     udp, tcb = R.gen_flows(cfg)
     udp = np.concatenate([fl["udp"], udp])
     tcb = np.concatenate([fl["tcb"], tcb])
@@ -155,6 +157,46 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     finally:
         ctx.tune(0)
     assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
+
+
+@pytest.mark.parametrize("layout", ["packed", "block_shuffled", "scattered", "gapped"])
+@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 20),
+                                     (4, 1, 2, 0)])
+def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
+    """Descriptor orders the stream kernel must handle: packed (streamed),
+    frames shuffled inside each 256-frame block (streamed, unordered
+    boundaries), fully scattered (per-thread tail fallback), and frames with
+    random garbage between them (streamed: gap bytes must not leak in)."""
+    cfg = rxdist.gen_cfg("cfg4", n_udp=500, n_tcp=500)
+    n = 20000
+    pk, off, ln = R.gen_host(cfg, 5, n, 6)
+    rng = np.random.default_rng(3)
+    if layout == "block_shuffled":
+        perm = np.concatenate([rng.permutation(np.arange(b, min(b + 256, n)))
+                               for b in range(0, n, 256)])
+    elif layout == "scattered":
+        perm = rng.permutation(n)
+    else:
+        perm = np.arange(n)
+    off, ln = off[perm].copy(), ln[perm].copy()
+    if layout == "gapped":  # re-pack with 0..3 units of random bytes after each frame
+        frames = [pk[int(o) << 6:(int(o) << 6) + int(l)] for o, l in zip(off, ln)]
+        units = [(int(l) + 63) // 64 + int(rng.integers(0, 4)) for l in ln]
+        pos = np.concatenate([[0], np.cumsum(units)[:-1]]).astype(np.uint32)
+        pk = rng.integers(0, 256, int(sum(units)) * 64, dtype=np.uint8)
+        for f, o in zip(frames, pos):
+            pk[int(o) << 6:(int(o) << 6) + len(f)] = f
+        off = pos
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 354, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (layout, variant, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt)
 
 
 def test_fuzzed_frames_match_oracle(ctx, torch_dev):
@@ -218,7 +260,7 @@ def test_nstack_udp_echo_through_gpu(torch_dev):
         ns.fini()
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg3"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
 def test_full_size_properties(ctx, torch_dev, name):
     """BASELINE sizes (16M x 64 B, 4M x 1500 B): verdicts of a random sample of
     indices regenerate bit-exactly on the CPU (counter-based pktgen + oracle),

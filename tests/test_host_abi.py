@@ -129,6 +129,25 @@ def test_generator_deterministic_and_valid(name):
     assert (l4["cksum_ok"] == 1).mean() > 0.95
 
 
+def test_generator_packed_layout():
+    """packed=1: same frames as the slot layout, back to back at 64-B alignment."""
+    kw = dict(size_mode=1, slot_bytes=1536, proto_mode=2, n_udp=300, n_tcp=300)
+    n = 500
+    pk, off, ln = R.gen_host(R.make_gen_cfg(**kw), 77, n)
+    pq, oq, lq = R.gen_host(R.make_gen_cfg(**kw, packed=1), 77, n)
+    assert np.array_equal(ln, lq)
+    want = np.concatenate([[0], np.cumsum((np.maximum(ln.astype(np.int64), 60) + 63) // 64)[:-1]])
+    assert np.array_equal(oq.astype(np.int64), want)
+    for k in range(n):
+        a = int(off[k]) << 6
+        b = int(oq[k]) << 6
+        m = int(ln[k])
+        assert pk[a:a + m].tobytes() == pq[b:b + m].tobytes(), k
+    # coarser offset units cannot address 64-B aligned frames
+    with pytest.raises(R.RxgError):
+        R.gen_host(R.make_gen_cfg(**kw, packed=1), 0, 4, 7)
+
+
 @pytest.mark.parametrize("nsh", [2, 4, 8])
 def test_generator_rss_sharding(nsh):
     base = dict(frame_len=64, slot_bytes=64, proto_mode=2, n_udp=64, n_tcp=64)
