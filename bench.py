@@ -236,7 +236,7 @@ def e2e(name, local, batch, reps=20):
                 alg_gb_per_s=round((frame_bytes + 22 * batch) / el / 1e9, 2))
 
 
-def sweep(ctx, names, steps, warmup, dev, only=""):
+def sweep(ctx, names, steps, warmup, dev, only="", with_counts=False):
     """Tuning: every kernel variant, interleaved over rounds in one process
     (same data, same device), median and min of the per-round kernel time."""
     variants = [tuple(int(x) for x in v.split(",")) for v in only.split(";") if v] or \
@@ -254,6 +254,7 @@ def sweep(ctx, names, steps, warmup, dev, only=""):
         off = torch.empty(n, dtype=torch.int32, device=dev)
         ln = torch.empty(n, dtype=torch.int16, device=dev)
         out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(ctx.num_flows, dtype=torch.int64, device=dev) if with_counts else None
         R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
         torch.cuda.synchronize(dev)
         alg = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item()) + 22 * n
@@ -261,7 +262,7 @@ def sweep(ctx, names, steps, warmup, dev, only=""):
         for v in variants:  # drop variants that are not compiled in
             ctx.tune(*v[:4])
             try:
-                ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, cnt,
                                  stream=sh)
                 ok.append(v)
             except R.RxgError as e:
@@ -273,12 +274,12 @@ def sweep(ctx, names, steps, warmup, dev, only=""):
                 ctx.tune(*v[:4])
                 ctx.tune_grid(v[4])
                 for _ in range(warmup):
-                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, cnt,
                                      stream=sh)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for _ in range(steps):
-                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None,
+                    ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, cnt,
                                      stream=sh)
                 b.record()
                 torch.cuda.synchronize(dev)
@@ -288,9 +289,9 @@ def sweep(ctx, names, steps, warmup, dev, only=""):
         for v in variants:
             t = sorted(times[v])
             med = t[len(t) // 2]
-            log(f"sweep {nm} variant={v}: median {med:.4f} ms min {t[0]:.4f} ms "
+            log(f"sweep {nm}{' +counts' if with_counts else ''} variant={v}: median {med:.4f} ms min {t[0]:.4f} ms "
                 f"-> {n / med / 1e3:.0f} Mpps, {alg / med / 1e6:.0f} GB/s")
-        del pk, off, ln, out
+        del pk, off, ln, out, cnt
         torch.cuda.empty_cache()
 
 
@@ -308,6 +309,7 @@ def main():
                     "gloo only to rehearse N > 1 on one GPU)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
+    ap.add_argument("--sweep-counts", action="store_true", help="sweep with per-flow counts on")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
@@ -333,7 +335,7 @@ def main():
     if a.variant:
         ctx.tune(*[int(x) for x in a.variant.split(",")])
     if a.sweep:
-        sweep(ctx, a.sweep.split(","), a.steps, a.warmup, dev, a.sweep_variants)
+        sweep(ctx, a.sweep.split(","), a.steps, a.warmup, dev, a.sweep_variants, a.sweep_counts)
         return
     names = [s.strip() for s in a.workload.split(",") if s.strip()]
     results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}

@@ -19,6 +19,8 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
                               unsigned long long *counts, hipStream_t s, uint32_t *ws);
+size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
+                            bool counts);
 
 static thread_local std::string g_last_hip;
 
@@ -76,19 +78,43 @@ struct ft_host {
     }
 };
 
+// Compact UDP table for socket sets of <= RX_UDPC_MAX_FLOWS: the same keys and
+// flow ids as the main table (already deduplicated, newest wins), 8-B slots at
+// load <= 1/2 so the lane kernel can keep it in LDS.
+static void build_udpc(const ft_host &u, uint32_t nu, std::vector<uint2> *out, uint32_t *probe) {
+    out->clear();
+    *probe = 0;
+    if (nu == 0 || nu > RX_UDPC_MAX_FLOWS) return;
+    uint32_t ns = 16;
+    while (ns < 2 * nu) ns <<= 1;
+    out->assign(ns, make_uint2(0, 0xFFFFFFFFu));
+    const uint32_t mask = ns - 1;
+    for (const uint4 &sl : u.slots) {
+        if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> flow
+        uint32_t i = rx_hash3(sl.x, sl.y, sl.z) & mask;
+        uint32_t d = 0;
+        while ((*out)[i].y != 0xFFFFFFFFu) i = (i + 1) & mask, ++d;
+        (*out)[i] = make_uint2(sl.x, (sl.y & 0xFFFFu) | (sl.w << 16));
+        *probe = std::max(*probe, d + 1);
+    }
+}
+
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // flow tables
     ft_host h_udp, h_tcp;
     std::vector<uint32_t> h_listen;
+    std::vector<uint2> h_udpc; // compact UDP table (small socket sets), empty if none
+    uint32_t udpc_probe = 0;
     uint4 *d_udp = nullptr, *d_tcp = nullptr;
-    size_t d_udp_cap = 0, d_tcp_cap = 0;
+    uint2 *d_udpc = nullptr;
+    size_t d_udp_cap = 0, d_tcp_cap = 0, d_udpc_cap = 0;
     uint32_t *d_listen = nullptr;
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
-    uint32_t *d_ws = nullptr; // binned-path workspace (16 B + 8 B per frame), grown on demand
+    uint32_t *d_ws = nullptr; // launch workspace (binned lists, count slabs), grown on demand
     size_t d_ws_cap = 0;
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
@@ -200,6 +226,7 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_listen);
     (void)hipFree(c->d_counts);
     (void)hipFree(c->d_ws);
+    (void)hipFree(c->d_udpc);
     (void)hipFree(c->d_pkts);
     (void)hipFree(c->d_off);
     (void)hipFree(c->d_len);
@@ -227,6 +254,7 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
                                 (uint32_t)t[i].sport | ((uint32_t)t[i].dport << 16), i));
     c->h_udp.build(ue);
     c->h_tcp.build(te);
+    build_udpc(c->h_udp, nu, &c->h_udpc, &c->udpc_probe);
     c->h_listen.assign(65536, RXG_FLOW_NONE);
     for (uint32_t i = 0; i < nt; ++i)
         if (t[i].status == RXG_TCP_STATUS_LISTEN) c->h_listen[t[i].dport] = i;
@@ -248,6 +276,17 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
                      hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_listen, c->h_listen.data(), 65536 * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
+    c->ft.udpc = nullptr;
+    c->ft.udpc_mask = c->ft.udpc_probe = 0;
+    if (!c->h_udpc.empty()) {
+        if ((rc = ensure_dev((void **)&c->d_udpc, &c->d_udpc_cap, c->h_udpc.size() * sizeof(uint2))))
+            return rc;
+        HIPCHK(hipMemcpy(c->d_udpc, c->h_udpc.data(), c->h_udpc.size() * sizeof(uint2),
+                         hipMemcpyHostToDevice));
+        c->ft.udpc = c->d_udpc;
+        c->ft.udpc_mask = (uint32_t)c->h_udpc.size() - 1;
+        c->ft.udpc_probe = c->udpc_probe;
+    }
     c->ft.udp = c->d_udp;
     c->ft.tcp = c->d_tcp;
     c->ft.listen = c->d_listen;
@@ -271,8 +310,8 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
-    if (lanes_per_frame == 0 && (pipeline == 20 || (pipeline >= 30 && pipeline <= 32))) {
-        c->tune_g = 0; // size-class binned path (20) / stream kernel (30..32)
+    if (lanes_per_frame == 0 && (pipeline == 20 || pipeline == 30 || pipeline == 31 || pipeline == 130)) {
+        c->tune_g = 0; // size-class binned path (20) / stream kernel (30, 31)
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;
         return RXG_OK;
@@ -322,8 +361,10 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     HIPCHK(hipSetDevice(c->device));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
-    if (g == 0 && pipe == 20) { // binned path: workspace (sized once per burst size; not inside graph capture)
-        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
+    // workspace (binned lists, count slabs): grown on demand, so size it once
+    // per burst shape before any graph capture
+    if (size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr)) {
+        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
         if (rc) return rc;
     }
     rx_set_bpc_cap(c->tune_bpc);
@@ -349,8 +390,8 @@ int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, cons
     HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
-    if (g == 0 && pipe == 20) {
-        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, 16 + 8ull * n);
+    if (size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, c->d_counts != nullptr)) {
+        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
         if (rc) return rc;
     }
     rx_set_bpc_cap(c->tune_bpc);

@@ -530,9 +530,9 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 // probe, 4 = no verdict store, 8 = no checksum arithmetic.
 // Verdict of one lane-owned frame (everything but the store): returns the
 // 16-B verdict and the per-flow count slot (~0u = not counted).
-template <int ABL = 0, bool NTL = true>
+template <int ABL = 0, bool NTL = true, bool LDT = false>
 __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, const rx_ft_dev &ft,
-                                              uint32_t *count_idx) {
+                                              uint32_t *count_idx, const uint2 *lt = nullptr) {
     const int32_t cp = L.cap;
     if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
 #pragma unroll
@@ -614,6 +614,16 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
     const bool probe = L.valid && (is_udp || (is_tcp && ok));
     if (ABL & 1) {
         flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+    } else if (LDT && probe && is_udp) { // compact UDP table in LDS
+        uint32_t i = rx_hash3(dip, dport, 17u) & ft.udpc_mask;
+        for (uint32_t pr = 0; pr < ft.udpc_probe; ++pr, i = (i + 1) & ft.udpc_mask) {
+            const uint2 sl = lt[i];
+            if (sl.y == 0xFFFFFFFFu) break;
+            if (sl.x == dip && (sl.y & 0xFFFFu) == dport) {
+                flow = sl.y >> 16;
+                break;
+            }
+        }
     } else if (probe) {
         const uint32_t ka = is_udp ? dip : sip;
         const uint32_t kb = is_udp ? dport : dip;
@@ -682,13 +692,14 @@ __device__ __forceinline__ void lane_store(uint4 *__restrict__ out, uint64_t p, 
 }
 
 // the original one-shot form: verdict, store, count
-template <int ABL = 0, bool ST_NT = true, bool NTL = true>
+template <int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false>
 __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
                                              const rx_ft_dev &ft, uint4 *__restrict__ out,
                                              unsigned long long *__restrict__ counts,
-                                             uint32_t *hist, uint32_t lds_bins) {
+                                             uint32_t *hist, uint32_t lds_bins,
+                                             const uint2 *lt = nullptr) {
     uint32_t idx;
-    const uint4 v = lane_verdict<ABL, NTL>(L, next, ft, &idx);
+    const uint4 v = lane_verdict<ABL, NTL, LDT>(L, next, ft, &idx, lt);
     if (L.valid) {
         if (ABL & 4)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
@@ -702,19 +713,28 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
 // fetched at the top of trip t and its frame bytes are issued mid-trip.
 // PIPE = 2: as 1, register budget capped for 6 waves per SIMD.  PIPE = 3:
 // only the descriptors are prefetched (frame bytes loaded at the top).
-template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
+// LDT: the compact UDP table (ft.udpc) is copied into LDS after the histogram
+// and UDP frames probe it there (PIPE 0 only)
+template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false>
 __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
+    static_assert(!LDT || PIPE == 0, "LDS table: PIPE 0 only");
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
     const uint32_t tid = threadIdx.x;
+    if constexpr (LDT) {
+        const uint32_t q = (ft.udpc_mask + 1) / 2; // 16-B pieces
+        for (uint32_t i = tid; i < q; i += 256)
+            reinterpret_cast<uint4 *>(lt)[i] = reinterpret_cast<const uint4 *>(ft.udpc)[i];
+    }
     if (lds_bins) {
         for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
-        __syncthreads();
     }
+    if (LDT || lds_bins) __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
     if constexpr (PIPE == 9) {
@@ -752,7 +772,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2, idx);
             lane_load<NTL>(L);
-            lane_process<ABL, ST_NT, NTL>(L, nullptr, ft, out, counts, hist, lds_bins);
+            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
         }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
@@ -809,12 +829,13 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     }
 }
 
-template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
+template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false>
 hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
-    const size_t lds = (size_t)lds_bins * 4u;
+    const size_t lds =
+        (size_t)((lds_bins + 3u) & ~3u) * 4u + (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u);
     static int cu = 0;
     static int cached_occ[2] = {0, 0};
     static size_t cached_lds[2] = {~(size_t)0, ~(size_t)0};
@@ -829,7 +850,7 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL>), 256,
+            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
             lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
@@ -841,11 +862,24 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
 
+
+// the LDS-table instantiation when the flow set has a compact UDP table
+template <int PIPE, int ABL = 0, bool ST_NT = true, bool NTL = true>
+hipError_t launch_lane_udpc(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                            uint32_t n, uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                            unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                            const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
+    if (ft.udpc)
+        return launch_lane<PIPE, ABL, ST_NT, NTL, true>(pkts, off, len, n, unit_log2, ft, out,
+                                                         counts, lds_bins, s, idx, n_dev);
+    return launch_lane<PIPE, ABL, ST_NT, NTL, false>(pkts, off, len, n, unit_log2, ft, out, counts,
+                                                      lds_bins, s, idx, n_dev);
+}
 
 // ---------------------------------------------------------------------------
 // Size-class binning for mixed-size bursts (IMIX): frame indices split into a
@@ -932,7 +966,7 @@ static hipError_t launch_binned(const uint8_t *pkts, const uint32_t *off, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t user_cap = g_bpc_cap;
     if (!user_cap) g_bpc_cap = 6;
-    e = launch_lane<0, 0, true, false>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
+    e = launch_lane_udpc<0, 0, true, false>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
                                         lists, lens);
     g_bpc_cap = user_cap;
     if (e != hipSuccess) return e;
@@ -975,10 +1009,13 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
     return add_halves(add_halves(add_halves(add_halves(0u, v.x), v.y), v.z), v.w);
 }
 
-// EARLY: the span comes from the descriptors (tails end before caplen), so
-// the first tile's loads are in flight while the heads are decoded and probed;
-// otherwise from the decoded checksum ends (tighter span, later start).
-template <bool NTS, bool EARLY>
+// Every load below is issued unconditionally (out-of-range lanes load a
+// clamped, valid address and select zero) so that the compiler's wait counts
+// stay partial: a lane-dependent branch around a load makes it drain every
+// outstanding load (vmcnt(0)), which would serialise the tile prefetch.
+// ABL (diagnostic builds only, never selected automatically): 1 = no flow
+// table probe (flow id from the port: wrong verdicts by construction)
+template <bool NTS, int ABL = 0>
 __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1003,46 +1040,12 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     const uint8_t *fb = pkts + fpos;
     const int32_t cp = valid ? (int32_t)len[q] : 0;
 
-    // block span of the tail chunks; a span far larger than the tails means
-    // scattered frames (per-thread fallback below)
-    auto block_span = [&](bool t, uint64_t clo, uint64_t chi) {
-        __syncthreads(); // s_lo/s_hi/s_tail initialised
-        if (t) {
-            atomicMin(&s_lo, (unsigned long long)clo);
-            atomicMax(&s_hi, (unsigned long long)chi);
-            atomicAdd(&s_tail, (uint32_t)(chi - clo));
-        }
-        __syncthreads();
-    };
-    uint64_t lo = 0, hi = 0;
-    uint32_t span = 0;
-    bool streamed = false;
-    uint4 v[4];
-    if constexpr (EARLY) {
-        const int32_t cf = cp & ~15;
-        block_span(cf > 64, (fpos + 64) >> 4, (fpos + (uint32_t)cf) >> 4);
-        lo = s_lo, hi = s_hi;
-        const uint32_t tsum = s_tail;
-        streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
-        span = streamed ? (uint32_t)(hi - lo) : 0u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k = j * 256 + tid;
-            v[j] = k < span ? ldg16<NTS>(pkts + ((lo + k) << 4)) : make_uint4(0, 0, 0, 0);
-        }
-    }
-
     // ---- head phase -------------------------------------------------------
     uint4 c[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        c[j] = make_uint4(0, 0, 0, 0);
-        if (16 * j < cp) c[j] = ldg16<false>(fb + 16 * j);
-    }
-    if (cp < 64) {
+    for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp);
-    }
+    for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
     const uint32_t et = c[0].w & 0xFFFFu;
     const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
     const uint32_t proto = c[1].y >> 24;
@@ -1076,6 +1079,23 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     if (l4 && 34u + l4n > nd) nd = 34u + l4n;
     int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
     if (e > cp) e = cp;
+    const int32_t ef = e & ~15; // full tail chunks: [64, ef)
+    const bool part = ef < e && ef >= 64;
+    const bool tail = ef > 64;
+    const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
+    // the last partial chunk (consumed after the stream) and the first probe slot
+    const uint4 pc = ldg16<false>(fb + (part ? ef : 0));
+    const bool probe = valid && l4;
+    const uint32_t ka = is_udp ? dip : sip;
+    const uint32_t kb = is_udp ? dport : dip;
+    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+    const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
+    const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
+    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+    uint32_t pi = rx_hash3(ka, kb, kc) & mask;
+    const bool probe0 = probe && maxp > 0 && !(ABL & 1);
+    const uint4 sl0 = ld_slot(probe0 ? tbl + pi : reinterpret_cast<const uint4 *>(fb));
+
     uint4 h1 = c[1], h2 = c[2], h3 = c[3];
     h1.x = 0;
     h1.y = 0;
@@ -1085,62 +1105,85 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
     acc = lane_chunk_sum(acc, h2, 32, e);
     acc = lane_chunk_sum(acc, h3, 48, e);
-    const int32_t ef = e & ~15; // full tail chunks: [64, ef)
-    if (ef < e && ef >= 64) acc = lane_chunk_sum(acc, ldg16<false>(fb + ef), ef, e);
-    const bool tail = ef > 64;
-    const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
-    if constexpr (!EARLY) {
-        block_span(tail, cs_abs, ce_abs);
-        lo = s_lo, hi = s_hi;
-        const uint32_t tsum = s_tail;
-        streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
-        span = streamed ? (uint32_t)(hi - lo) : 0u;
+    if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
+    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+
+    // block span of the tail chunks; a span far larger than the tails means
+    // scattered frames (per-thread fallback below)
+    __syncthreads(); // s_lo/s_hi/s_tail initialised
+    if (tail) {
+        atomicMin(&s_lo, (unsigned long long)cs_abs);
+        atomicMax(&s_hi, (unsigned long long)ce_abs);
+        atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
+    }
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    const uint32_t tsum = s_tail;
+    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
+    const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
+    // (not streamed: loads of the thread's own frame head, never consumed)
+    const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
+    auto tile_load = [&](uint4 *v, uint32_t c0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = j * 256 + tid;
-            v[j] = k < span ? ldg16<NTS>(pkts + ((lo + k) << 4)) : make_uint4(0, 0, 0, 0);
+            const uint32_t k = c0 + j * 256 + tid;
+            v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
         }
-    }
+    };
+    if (part) acc = lane_chunk_sum(acc, pc, ef, e);
 
-    // flow probe (UDP always, TCP speculatively)
+    // flow probe (UDP always, TCP speculatively: a bad checksum drops the hit)
     uint32_t flow = RXG_FLOW_NONE;
-    if (valid && l4) {
-        const uint32_t ka = is_udp ? dip : sip;
-        const uint32_t kb = is_udp ? dport : dip;
-        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-        const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
-        const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
-        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-        uint32_t i = rx_hash3(ka, kb, kc) & mask;
-        for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) {
-            const uint4 sl = ld_slot(tbl + i);
+    if (probe0) {
+        uint4 sl = sl0;
+        for (uint32_t pr = 0;;) {
             if (sl.w == RX_SLOT_EMPTY) break;
             if (sl.x == ka && sl.y == kb && sl.z == kc) {
                 flow = sl.w;
                 break;
             }
+            if (++pr >= maxp) break;
+            pi = (pi + 1) & mask;
+            sl = ld_slot(tbl + pi);
         }
-        if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
     }
+    if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+    if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
+
+    // every verdict field but the checksum outcome, before the tail phase (so
+    // the header words are dead across the stream loop)
+    uint32_t poff = 0, plen = 0, flags = 0;
+    int32_t rc = RXG_RC_KNI;
+    if (is_udp) {
+        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                   : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        poff = 42;
+        plen = dgl > 8u ? dgl - 8u : 0u;
+        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+    } else if (is_tcp) {
+        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+        poff = 34u + 4u * hl;
+        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+        plen = pl < 0 ? 0u : (uint32_t)pl;
+    }
+    if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
+    const uint32_t vy = (poff & 0xFFFFu) | (plen << 16);
 
     // ---- tail phase -------------------------------------------------------
+    uint4 va[4], vb[4];
+    tile_load(va, 0);
     if (streamed) {
-        const uint8_t *sb = pkts + (lo << 4);
         const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
         const uint32_t ce = tail ? (uint32_t)(ce_abs - lo) : 0xFFFFFFFFu;
         uint32_t es = 0, ee = 0, carry = 0;
-        uint32_t buf = 0;
-        for (uint32_t c0 = 0; c0 < span; c0 += ST_TILE, buf ^= 1u) {
-            uint4 nv[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { // next tile in flight across this one's scan
-                const uint32_t k = c0 + ST_TILE + j * 256 + tid;
-                nv[j] = k < span ? ldg16<NTS>(sb + ((uint64_t)k << 4)) : make_uint4(0, 0, 0, 0);
-            }
+        // one tile: chunk sums, exclusive prefix (wave scans + wave totals via
+        // LDS), then each frame picks up its boundary values
+        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
             uint32_t sj[4], xj[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                sj[j] = chunk_sum(v[j]);
+                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
                 xj[j] = wave_incl_scan(sj[j]);
             }
             if (lane == 63) {
@@ -1148,11 +1191,14 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
                 for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
             }
             __syncthreads();
-            uint32_t wt[16];
+            uint32_t wt[16]; // block-uniform: kept in SGPRs
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
-                wt[j * 4 + 0] = r.x, wt[j * 4 + 1] = r.y, wt[j * 4 + 2] = r.z, wt[j * 4 + 3] = r.w;
+                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
+                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
+                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
+                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
             }
             uint32_t base = carry;
 #pragma unroll
@@ -1167,8 +1213,15 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
             __syncthreads();
             if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
             if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = nv[j];
+        };
+        // unrolled twice: the A/B tiles swap roles without register moves (a
+        // move would wait for the prefetch it copies); one exit per pair (a
+        // trailing all-masked tile costs no bandwidth: its loads hit chunk 0)
+        for (uint32_t c0 = 0; c0 < span; c0 += 2 * ST_TILE) {
+            tile_load(vb, c0 + ST_TILE);
+            tile(va, c0, 0);
+            tile_load(va, c0 + 2 * ST_TILE);
+            tile(vb, c0 + ST_TILE, 1);
         }
         if (ce == span) ee = carry;
         if (tail) acc += ee - es;
@@ -1176,49 +1229,28 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
         for (int32_t s = 64; s < ef; s += 64) {
             uint4 r[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                r[u] = make_uint4(0, 0, 0, 0);
-                if (s + 16 * u < ef) r[u] = ldg16<false>(fb + s + 16 * u);
-            }
+            for (int u = 0; u < 4; ++u) r[u] = ldg16<false>(fb + (s + 16 * u < ef ? s + 16 * u : 0));
 #pragma unroll
-            for (int u = 0; u < 4; ++u) acc += chunk_sum(r[u]);
+            for (int u = 0; u < 4; ++u)
+                if (s + 16 * u < ef) acc += chunk_sum(r[u]);
         }
     }
 
     // ---- verdict ----------------------------------------------------------
     uint32_t ck = 0;
     if (do_sum) {
-        acc += proto << 8;
-        acc += rx_bswap16(l4n);
         ck = (~fold16(acc)) & 0xFFFFu;
         if (ck == 0u && proto == 17u) ck = 0xFFFFu;
     }
-    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
     const bool ok = l4 && stored == ck;
-    if (is_tcp && !ok) flow = RXG_FLOW_NONE;
-    int32_t rc;
-    uint32_t poff = 0, plen = 0, flags = 0;
-    if (is_udp) {
-        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                   : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-        poff = 42;
-        plen = dgl > 8u ? dgl - 8u : 0u;
-        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-        if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
-    } else if (is_tcp) {
-        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-        poff = 34u + 4u * hl;
-        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-        plen = pl < 0 ? 0u : (uint32_t)pl;
+    if (is_tcp) {
+        if (!ok) flow = RXG_FLOW_NONE;
         rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-    } else {
-        rc = RXG_RC_KNI;
     }
-    if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
     if (valid) {
         uint4 vd;
         vd.x = flow;
-        vd.y = (poff & 0xFFFFu) | (plen << 16);
+        vd.y = vy;
         vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
         stg16(&out[p], vd);
@@ -1234,16 +1266,124 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     }
 }
 
-template <bool NTS, bool EARLY = true>
+template <bool NTS, int ABL = 0>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, EARLY>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Per-flow counts for 8192 < flows <= 65536 (too many for a per-block LDS
+// histogram at full occupancy, and scattered 8-B global atomics each cost one
+// memory-side request): a slab histogram over the stored verdicts.  Pass 1:
+// block b (1024 threads, one per CU: 128 KiB of LDS) adds its <= 65535
+// verdicts into 16-bit LDS bins over all flows (two per dword; a bin cannot
+// carry into its neighbour below 65536 adds) and writes the bins out as slab
+// b.  Pass 2: one thread per bin pair sums the slab column and adds it to
+// counts (each pair owned by one thread: plain read-modify-write).
+constexpr uint32_t SLAB_MAX_FLOWS = 65536;
+constexpr uint32_t SLAB_MIN_FLOWS = 8193; // below: LDS histogram in the classify kernel
+
+__global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint4 *__restrict__ vd, uint32_t n,
+                                                              uint32_t per, uint32_t nu,
+                                                              uint32_t words,
+                                                              uint32_t *__restrict__ slab) {
+    __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
+    for (uint32_t i = threadIdx.x; i < words; i += 1024) bins[i] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * per;
+    const uint64_t b1 = min((uint64_t)n, b0 + per);
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += 1024) {
+        // non-temporal: 16 B per frame read once; keeps the flow table cached
+        const uint4 v = ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i));
+        const uint32_t rc = v.z >> 24, cls = (v.z >> 16) & 0xFFu;
+        if (rc == 0u && v.x != RXG_FLOW_NONE && (cls == RXG_CLS_UDP || cls == RXG_CLS_TCP)) {
+            const uint32_t f = (cls == RXG_CLS_TCP ? nu : 0u) + v.x;
+            atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
+        }
+    }
+    __syncthreads();
+    uint32_t *dst = slab + (uint64_t)blockIdx.x * words;
+    for (uint32_t i = threadIdx.x; i < words; i += 1024) dst[i] = bins[i];
+}
+
+// block = 64 bin pairs (one per lane) x 16 waves, each wave summing every
+// 16th slab with 8 loads in flight; the 16 partial sums meet in LDS
+__global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
+                                                                uint32_t nslabs, uint32_t words,
+                                                                uint32_t nflows,
+                                                                unsigned long long *__restrict__ counts) {
+    __shared__ uint32_t part[2][16][64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t w = blockIdx.x * 64 + lane;
+    const uint32_t wc = w < words ? w : 0;
+    uint32_t lo = 0, hi = 0;
+    uint32_t b = wv;
+    for (; b + 16 * 7 < nslabs; b += 16 * 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = slab[(uint64_t)(b + 16 * u) * words + wc];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            lo += x[u] & 0xFFFFu;
+            hi += x[u] >> 16;
+        }
+    }
+    for (; b < nslabs; b += 16) {
+        const uint32_t x = slab[(uint64_t)b * words + wc];
+        lo += x & 0xFFFFu;
+        hi += x >> 16;
+    }
+    part[0][wv][lane] = lo;
+    part[1][wv][lane] = hi;
+    __syncthreads();
+    if (wv == 0 && w < words) {
+        lo = hi = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            lo += part[0][k][lane];
+            hi += part[1][k][lane];
+        }
+        if (lo) counts[2 * w] += lo;
+        if (hi && 2 * w + 1 < nflows) counts[2 * w + 1] += hi;
+    }
+}
+
+// slab geometry: a multiple of 256 blocks (whole waves of one block per CU),
+// <= 65535 verdicts each
+static void slab_geometry(uint32_t n, uint32_t *nslabs, uint32_t *per) {
+    const uint64_t waves = ((uint64_t)n + 256ull * 65535 - 1) / (256ull * 65535);
+    uint64_t nb = 256 * (waves ? waves : 1);
+    uint64_t pr = ((uint64_t)n + nb - 1) / nb;
+    if (pr == 0) pr = 1;
+    nb = ((uint64_t)n + pr - 1) / pr;
+    *nslabs = (uint32_t)(nb ? nb : 1);
+    *per = (uint32_t)pr;
+}
+
+static bool use_slab(const rx_ft_dev &ft, bool counts) {
+    const uint32_t nf = ft.nu + ft.nt;
+    return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS;
+}
+
+static hipError_t launch_count_slab(const uint4 *out, uint32_t n, const rx_ft_dev &ft,
+                                    unsigned long long *counts, uint32_t *slab, hipStream_t s) {
+    uint32_t nslabs, per;
+    slab_geometry(n, &nslabs, &per);
+    const uint32_t nf = ft.nu + ft.nt, words = (nf + 1) / 2;
+    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs), dim3(1024), 0, s, out, n, per, ft.nu,
+                       words, slab);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words + 63) / 64), dim3(1024), 0, s, slab,
+                       nslabs, words, nf, counts);
     return hipGetLastError();
 }
 
@@ -1265,7 +1405,7 @@ struct variant_entry {
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
     // defaults first (measured on MI355X, bench.py --sweep)
-    {1, 4, 1, 5, launch_lane<0, 0, true, false>, 6},
+    {1, 4, 1, 5, launch_lane_udpc<0, 0, true, false>, 6},
     {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
     {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
     {1, 4, 1, 2, launch_lane<2>},          {1, 4, 1, 3, launch_lane<3>},
@@ -1273,8 +1413,11 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 6, launch_lane<0, 0, false, false>},
     {1, 4, 1, 7, launch_lane<1, 0, true, false>}, {1, 4, 1, 8, launch_lane<2, 0, true, false>},
     {1, 4, 1, 9, launch_lane<9, 0, true, false>}, {1, 4, 1, 10, launch_lane<9, 0, false, false>},
+    {1, 4, 1, 11, launch_lane<0, 0, true, false>, 6}, // 5 without the LDS UDP table
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
+    {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},
+    {1, 4, 1, 213, launch_lane<0, 13, true, false>, 6},
     {4, 1, 1, 1, launch_v<4, 1, 1, 1>},    {4, 1, 1, 0, launch_v<4, 1, 1, 0>},
     {4, 1, 1, 3, launch_v<4, 1, 1, 1, false>}, {4, 1, 2, 2, launch_v<4, 1, 2, 0, false>},
     {4, 1, 2, 0, launch_v<4, 1, 2, 0>},    {4, 1, 2, 1, launch_v<4, 1, 2, 1>},
@@ -1287,9 +1430,9 @@ static const variant_entry k_variants[] = {
     {64, 4, 1, 0, launch_v<64, 4, 1, 0>},  {64, 2, 1, 0, launch_v<64, 2, 1, 0>},
     {64, 2, 1, 1, launch_v<64, 2, 1, 1>},
     // g = 0: stream kernel (head per lane, tails streamed per block); pipe 30 nt
-    // tail loads, 31 plain, 32 = 30 with the span from the decoded heads
+    // tail loads, 31 plain
     {0, 1, 1, 30, launch_stream<true>},    {0, 1, 1, 31, launch_stream<false>},
-    {0, 1, 1, 32, launch_stream<true, false>},
+    {0, 1, 1, 130, launch_stream<true, 1>},
 };
 
 } // namespace
@@ -1313,24 +1456,47 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
 
 void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
 
+// workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
+// frame), then the count slabs
+size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
+                            bool counts) {
+    size_t b = (g == 0 && pipe == 20) ? 16 + 8ull * n : 0;
+    if (use_slab(ft, counts)) {
+        uint32_t nslabs, per;
+        slab_geometry(n, &nslabs, &per);
+        b = ((b + 255) & ~(size_t)255) + (size_t)nslabs * ((ft.nu + ft.nt + 1) / 2) * 4;
+    }
+    return b;
+}
+
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
                               unsigned long long *counts, hipStream_t s, uint32_t *ws) {
     if (n == 0) return hipSuccess;
     const uint32_t nflows = ft.nu + ft.nt;
-    const uint32_t lds_bins = (counts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
-    if (g == 0 && pipe == 20) // size-class binned (workspace: 16 B + 8 B per frame)
-        return launch_binned(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s, ws);
-    for (const variant_entry &v : k_variants)
-        if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
-            (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
-            const uint32_t user_cap = g_bpc_cap;
-            if (!user_cap) g_bpc_cap = v.bpc;
-            hipError_t e = v.fn(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s, nullptr,
-                                nullptr);
-            g_bpc_cap = user_cap;
-            return e;
-        }
-    return hipErrorInvalidValue;
+    const bool slab = use_slab(ft, counts != nullptr);
+    unsigned long long *kcounts = slab ? nullptr : counts; // slab: counted after classify
+    const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
+    hipError_t e = hipErrorInvalidValue;
+    if (g == 0 && pipe == 20) { // size-class binned (workspace: 16 B + 8 B per frame)
+        e = launch_binned(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, ws);
+    } else {
+        for (const variant_entry &v : k_variants)
+            if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
+                (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
+                const uint32_t user_cap = g_bpc_cap;
+                if (!user_cap) g_bpc_cap = v.bpc;
+                e = v.fn(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, nullptr,
+                         nullptr);
+                g_bpc_cap = user_cap;
+                break;
+            }
+    }
+    if (e != hipSuccess || !slab) return e;
+    if (!ws) return hipErrorInvalidValue;
+    const size_t lists = (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
+    return launch_count_slab(out, n, ft, counts,
+                             reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists),
+                             s);
 }

@@ -31,7 +31,12 @@ struct rx_ft_dev {
     uint32_t udp_mask, tcp_mask;   // slots - 1 (power of two)
     uint32_t udp_probe, tcp_probe; // longest probe sequence (slots) of any present key
     uint32_t nu, nt;
+    // compact UDP table for small socket sets (null otherwise), copied into LDS
+    // by the lane kernel: slot = {dip, dport | flow << 16}, empty = y ~0u
+    const uint2 *udpc;
+    uint32_t udpc_mask, udpc_probe;
 };
+#define RX_UDPC_MAX_FLOWS 1024u // load <= 1/2: <= 2048 slots = 16 KiB of LDS
 
 RX_HD uint32_t rx_hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = 0x9E3779B9u ^ a;

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 timeout -k 10 480 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pt.log 2>&1
 rc=$?; tail -3 gpurun_out/pt.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 400 python bench.py --workload cfg4 --no-cpu --sweep "${WL:-cfg4}" --steps 10 --warmup 3 \
+timeout -k 10 400 python bench.py --workload cfg4 --no-cpu --sweep "${WL:-cfg4}" --steps 10 --warmup 3 ${SWARGS:-} \
   --sweep-variants "${VARS:-0,0,0,20;8,2,1,1;8,2,2,0;4,1,2,0;16,2,2,0;1,4,1,5;8,2,1,0}" \
   > gpurun_out/sw4.log 2>&1 || exit $?
 grep sweep gpurun_out/sw4.log
