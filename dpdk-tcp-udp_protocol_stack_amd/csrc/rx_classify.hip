@@ -167,8 +167,14 @@ __device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) 
         }
 }
 
-// parse + checksum + probe + verdict for the FPG frames of S
-template <int G, int P, int FPG, bool NTL = true>
+// parse + checksum + probe + verdict for the FPG frames of S.
+// RI = 0: passes past the first P are summed frame by frame in batches of 4
+// (one HBM round trip per batch and frame).  RI > 0: the remaining passes of
+// all FPG frames are loaded together, RI passes per frame per batch (FPG*RI
+// loads of a lane in flight; a pass past a frame's end loads the frame's first
+// chunk again, an L1/L2 hit, and adds nothing), which keeps enough bytes in
+// flight for jumbo frames.
+template <int G, int P, int FPG, bool NTL = true, int RI = 0>
 __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t gl, uint32_t gbase,
                                               int32_t s0, const rx_ft_dev &ft,
                                               uint4 *__restrict__ out,
@@ -178,7 +184,9 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
     // ---- phase C: parse + checksum per frame
     uint32_t cls[FPG], ck[FPG], stored[FPG], tl[FPG], dgl[FPG], hl[FPG], need[FPG];
     uint32_t ka[FPG], kb[FPG], kc[FPG], dport[FPG];
-    bool ok[FPG];
+    uint32_t accs[FPG], protos[FPG];
+    int32_t ends[FPG];
+    bool ok[FPG], sums[FPG];
 #pragma unroll
     for (int f = 0; f < FPG; ++f) {
         const int32_t cp = S.cap[f];
@@ -255,7 +263,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             acc = add_halves(acc, v.w);
         }
         // frames longer than P passes: the rest in batches of 4 passes
-        for (int32_t sb = P * STEP; sb < e; sb += 4 * STEP) { // group-uniform
+        for (int32_t sb = P * STEP; RI == 0 && sb < e; sb += 4 * STEP) { // group-uniform
             uint4 r[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -274,20 +282,55 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
                 acc = add_halves(acc, v.w);
             }
         }
-        uint32_t sum = gsum<G>(acc);
-        uint32_t k = 0;
-        if (do_sum) {
-            sum += proto << 8;       // psd {zero, proto}
-            sum += rx_bswap16(l4n);  // psd be16(l4_len)
-            k = (~fold16(sum)) & 0xFFFFu;
-            if (k == 0u && proto == 17u) k = 0xFFFFu;
-        }
-        ck[f] = k;
+        accs[f] = acc;
+        ends[f] = e;
+        protos[f] = proto;
+        sums[f] = do_sum;
         stored[f] = is_udp ? (h22 & 0xFFFFu) : (is_tcp ? (h30 >> 16) : 0u);
-        ok[f] = l4 && stored[f] == k;
         ka[f] = is_udp ? dip : sip;
         kb[f] = is_udp ? dport[f] : dip;
         kc[f] = is_udp ? 17u : (sport | (dport[f] << 16));
+    }
+    if constexpr (RI > 0) { // the remaining passes of all frames, RI per frame in flight
+        int32_t emax = ends[0];
+#pragma unroll
+        for (int f = 1; f < FPG; ++f) emax = ends[f] > emax ? ends[f] : emax;
+        for (int32_t sb = P * STEP; sb < emax; sb += RI * STEP) {
+            uint4 r[FPG][RI];
+#pragma unroll
+            for (int f = 0; f < FPG; ++f)
+#pragma unroll
+                for (int u = 0; u < RI; ++u) { // unconditional: partial wait counts
+                    const int32_t s = s0 + sb + u * STEP;
+                    r[f][u] = ldg16<NTL>(S.fb[f] + (s < ends[f] ? s : 0));
+                }
+#pragma unroll
+            for (int f = 0; f < FPG; ++f)
+#pragma unroll
+                for (int u = 0; u < RI; ++u) {
+                    const int32_t s = s0 + sb + u * STEP;
+                    uint4 v = r[f][u];
+                    if (s + 16 > ends[f]) v = chunk_below(v, s, ends[f]); // all-zero past the end
+                    uint32_t a = accs[f];
+                    a = add_halves(a, v.x);
+                    a = add_halves(a, v.y);
+                    a = add_halves(a, v.z);
+                    accs[f] = add_halves(a, v.w);
+                }
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < FPG; ++f) {
+        uint32_t sum = gsum<G>(accs[f]);
+        uint32_t k = 0;
+        if (sums[f]) {
+            sum += protos[f] << 8;                    // psd {zero, proto}
+            sum += rx_bswap16((uint32_t)tl[f] - 20u); // psd be16(l4_len)
+            k = (~fold16(sum)) & 0xFFFFu;
+            if (k == 0u && protos[f] == 17u) k = 0xFFFFu;
+        }
+        ck[f] = k;
+        ok[f] = (cls[f] == RXG_CLS_UDP || cls[f] == RXG_CLS_TCP) && stored[f] == k;
     }
 
     // ---- phase D: flow probes, a 4-slot window per lane group, the first
@@ -379,8 +422,8 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
 // PIPE = 1: trip t+1's descriptors are fetched one trip ahead and its frame
 // bytes are issued before trip t is processed (one extra frame set of
 // registers), so both HBM round trips overlap the previous trip's work.
-template <int G, int P, int FPG, int PIPE, bool NTL = true>
-__global__ __launch_bounds__(256) void rx_classify_kernel(
+template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
@@ -414,13 +457,13 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
         group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         for (; tile * TILE < n; tile += gridDim.x) {
             group_load<G, FPG, P, NTL>(B, s0); // no-op lanes past the end (cap 0)
-            group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             A = B;
             group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         }
     } else {
         for (; tile * TILE < n; tile += gridDim.x) {
-            group_process<G, P, FPG, NTL>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
             group_load<G, FPG, P, NTL>(A, s0);
         }
@@ -435,7 +478,7 @@ __global__ __launch_bounds__(256) void rx_classify_kernel(
     }
 }
 
-template <int G, int P, int FPG, int PIPE = 0, bool NTL = true>
+template <int G, int P, int FPG, int PIPE = 0, bool NTL = true, int RI = 0, int MINW = 1>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s, const uint32_t *idx = nullptr,
@@ -457,7 +500,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     if (cached_lds[slot] != lds) {
         int occ = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL>), 256, lds);
+            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), 256, lds);
         if (e != hipSuccess) return e;
         cached_occ[slot] = occ > 0 ? occ : 1;
         cached_lds[slot] = lds;
@@ -468,7 +511,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
@@ -1429,6 +1472,17 @@ static const variant_entry k_variants[] = {
     {32, 3, 1, 0, launch_v<32, 3, 1, 0>},  {32, 2, 1, 1, launch_v<32, 2, 1, 1>},
     {64, 4, 1, 0, launch_v<64, 4, 1, 0>},  {64, 2, 1, 0, launch_v<64, 2, 1, 0>},
     {64, 2, 1, 1, launch_v<64, 2, 1, 1>},
+    // pipe 10 + RI: interleaved remainder, RI passes of every frame per batch
+    {8, 2, 2, 15, launch_v<8, 2, 2, 0, true, 5>},   {8, 2, 2, 14, launch_v<8, 2, 2, 0, true, 4>},
+    {8, 4, 2, 18, launch_v<8, 4, 2, 0, true, 8>},   {8, 4, 1, 18, launch_v<8, 4, 1, 0, true, 8>},
+    {16, 2, 2, 14, launch_v<16, 2, 2, 0, true, 4>}, {16, 2, 2, 18, launch_v<16, 2, 2, 0, true, 8>},
+    {32, 2, 2, 18, launch_v<32, 2, 2, 0, true, 8>}, {32, 2, 1, 18, launch_v<32, 2, 1, 0, true, 8>},
+    {64, 1, 2, 18, launch_v<64, 1, 2, 0, true, 8>}, {64, 1, 1, 18, launch_v<64, 1, 1, 0, true, 8>},
+    // pipe 20 + W: register budget capped for W waves per SIMD; 2 = plain frame loads
+    {8, 2, 2, 26, launch_v<8, 2, 2, 0, true, 0, 6>}, {8, 2, 2, 28, launch_v<8, 2, 2, 0, true, 0, 8>},
+    {8, 2, 1, 28, launch_v<8, 2, 1, 0, true, 0, 8>}, {8, 1, 2, 28, launch_v<8, 1, 2, 0, true, 0, 8>},
+    {8, 2, 2, 2, launch_v<8, 2, 2, 0, false>},
+    {16, 2, 2, 26, launch_v<16, 2, 2, 0, true, 0, 6>}, {16, 2, 2, 28, launch_v<16, 2, 2, 0, true, 0, 8>},
     // g = 0: stream kernel (head per lane, tails streamed per block); pipe 30 nt
     // tail loads, 31 plain
     {0, 1, 1, 30, launch_stream<true>},    {0, 1, 1, 31, launch_stream<false>},
@@ -1449,8 +1503,8 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         *g = 0, *p = 0, *fpg = 0, *pipe = 30;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
-    } else { // jumbo (cfg5: 9000 B)
-        *g = 16, *p = 2, *fpg = 2, *pipe = 0;
+    } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 30;
     }
 }
 

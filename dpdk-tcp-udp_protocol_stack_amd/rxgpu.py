@@ -52,6 +52,12 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
                    (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1),
+                   # pipeline 10 + RI: interleaved remainder passes (RI per frame per batch)
+                   (8, 2, 2, 15), (8, 2, 2, 14), (8, 4, 2, 18), (8, 4, 1, 18), (16, 2, 2, 14),
+                   (16, 2, 2, 18), (32, 2, 2, 18), (32, 2, 1, 18), (64, 1, 2, 18), (64, 1, 1, 18),
+                   # pipeline 20 + W: capped at W waves per SIMD; (8, 2, 2, 2): plain loads
+                   (8, 2, 2, 26), (8, 2, 2, 28), (8, 2, 1, 28), (8, 1, 2, 28), (8, 2, 2, 2),
+                   (16, 2, 2, 26), (16, 2, 2, 28),
                    (0, 0, 0, 20),  # size-class binned: lane kernel + G=8 kernel
                    (0, 0, 0, 30), (0, 0, 0, 31)]  # stream kernel
 

@@ -18,13 +18,13 @@ step() { # name timeout cmd...
   return $rc
 }
 
-step pytest_gpu 420 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+step pytest_gpu 420 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ -n "${SWEEP:-}" ]; then
   step sweep 300 python bench.py --sweep "$SWEEP" --steps 10 --warmup 3 || exit $?
 fi
 step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-step bench 300 python bench.py --steps $STEPS --warmup 5 || exit $?
+step bench 300 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
 if [ "${PROF:-1}" = 1 ]; then
   export TMPDIR=/tmp
