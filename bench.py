@@ -200,40 +200,98 @@ def cpu_baseline(name, budget_s):
 
 
 # ---------------------------------------------------------------------------
-def e2e(name, local, batch, reps=20):
-    """PCIe-inclusive rate of the host-buffer path (rxg_classify_span):
-    pinned host frames + descriptors -> H2D -> K1 -> verdicts D2H, synchronous
-    per burst (no overlap between bursts).  Reported in DESIGN.md, never as value."""
+def e2e(name, local, batch, reps=20, inflight=4):
+    """PCIe-inclusive rate of the host-buffer path: pinned host frames +
+    descriptors -> H2D -> K1 -> verdicts D2H.  "sync": one burst at a time
+    (rxg_classify_span).  "pipelined": rxg_submit with `inflight` bursts
+    outstanding over the context's 3 staging slots, so copies in, the kernel
+    and copies out of consecutive bursts overlap.  Reported in DESIGN.md,
+    never as value."""
     w = rxdist.WORKLOADS[name]
     cfg = rxdist.gen_cfg(name)
     hp, ho, hl = R.gen_host(cfg, 0, batch, w["unit_log2"])
     # bytes the burst occupies (the packed layout ends before batch * slot_bytes)
     span = (int(ho[-1]) << w["unit_log2"]) + ((int(hl[-1]) + 63) & ~63) if cfg.packed \
         else batch * cfg.slot_bytes
-    pk = torch.empty(span + 64, dtype=torch.uint8).pin_memory()
-    off = torch.empty(batch, dtype=torch.int32).pin_memory()
-    ln = torch.empty(batch, dtype=torch.int16).pin_memory()
-    out = torch.empty(batch * 16, dtype=torch.uint8).pin_memory()
-    pk.numpy()[:span] = hp[:span]
-    off.numpy().view(np.uint32)[:] = ho
-    ln.numpy().view(np.uint16)[:] = hl
+    sets = []
+    for _ in range(inflight):
+        pk = torch.empty(span + 64, dtype=torch.uint8).pin_memory()
+        off = torch.empty(batch, dtype=torch.int32).pin_memory()
+        ln = torch.empty(batch, dtype=torch.int16).pin_memory()
+        out = torch.empty(batch * 16, dtype=torch.uint8).pin_memory()
+        pk.numpy()[:span] = hp[:span]
+        off.numpy().view(np.uint32)[:] = ho
+        ln.numpy().view(np.uint16)[:] = hl
+        sets.append((pk, off, ln, out))
     ctx = R.Context(local, max_pkts=batch, max_bytes=span + 64)
     udp, tcb = R.gen_flows(cfg)
     ctx.flows_sync(udp, tcb)
-    args = (pk.data_ptr(), span, off.data_ptr(), ln.data_ptr(), batch, w["unit_log2"],
-            out.data_ptr())
-    for _ in range(3):
-        ctx.classify_span(*args)
+
+    def args(k):
+        pk, off, ln, out = sets[k % inflight]
+        return (pk.data_ptr(), span, off.data_ptr(), ln.data_ptr(), batch, w["unit_log2"],
+                out.data_ptr())
+    for k in range(3):
+        ctx.classify_span(*args(k))
     t0 = time.perf_counter()
-    for _ in range(reps):
-        ctx.classify_span(*args)
+    for k in range(reps):
+        ctx.classify_span(*args(k))
+    el_sync = (time.perf_counter() - t0) / reps
+    tickets = []
+    for k in range(inflight):  # warm the pipeline
+        tickets.append(ctx.submit(*args(k)))
+    ctx.wait(tickets[-1])
+    tickets = [None] * inflight
+    t0 = time.perf_counter()
+    for k in range(reps):
+        if tickets[k % inflight] is not None:
+            ctx.wait(tickets[k % inflight])  # this buffer set's previous burst
+        tickets[k % inflight] = ctx.submit(*args(k))
+    for t in tickets:
+        if t is not None:
+            ctx.wait(t)
     el = (time.perf_counter() - t0) / reps
     frame_bytes = int(hl.astype(np.int64).sum())
+    ok = sets[0][3].numpy().view(R.VERDICT_DTYPE)["rc"]
     ctx.close()
-    return dict(workload=name, frames_per_burst=batch, ms_per_burst=round(el * 1e3, 3),
-                mpps=round(batch / el / 1e6, 1),
-                h2d_gb_per_s=round((span + 6 * batch) / el / 1e9, 2),
-                alg_gb_per_s=round((frame_bytes + 22 * batch) / el / 1e9, 2))
+    h2d = span + 6 * batch
+    return dict(workload=name, frames_per_burst=batch, bursts=reps, inflight=inflight,
+                ms_per_burst=round(el * 1e3, 3), mpps=round(batch / el / 1e6, 1),
+                h2d_gb_per_s=round(h2d / el / 1e9, 2),
+                alg_gb_per_s=round((frame_bytes + 22 * batch) / el / 1e9, 2),
+                sync_ms_per_burst=round(el_sync * 1e3, 3), sync_mpps=round(batch / el_sync / 1e6, 1),
+                rc0_frac=round(float((ok == 0).mean()), 4))
+
+
+def pcie_peaks(local, nbytes=256 << 20, reps=10):
+    """pinned host <-> HBM copy rates on this box (the PCIe roofline of the
+    host-buffer path): H2D alone, D2H alone, both at once on two streams"""
+    dev = torch.device("cuda", local)
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def rate(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps
+
+    def both():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+    t_h2d = rate(lambda: d.copy_(h, non_blocking=True))
+    t_d2h = rate(lambda: h2.copy_(d2, non_blocking=True))
+    t_both = rate(both)
+    return dict(h2d_gb_per_s=round(nbytes / t_h2d / 1e9, 2), d2h_gb_per_s=round(nbytes / t_d2h / 1e9, 2),
+                duplex_gb_per_s=round(2 * nbytes / t_both / 1e9, 2))
 
 
 def sweep(ctx, names, steps, warmup, dev, only="", with_counts=False):
@@ -348,6 +406,9 @@ def main():
             results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget / 2)
 
     if a.e2e and rank == 0:
+        pk = pcie_peaks(local)
+        log("pcie", json.dumps(pk))
+        results[names[0]]["pcie_peaks"] = pk
         for nm in names:
             r = e2e(nm, local, {"cfg2": 1 << 20, "cfg3": 1 << 16}.get(nm, 1 << 16))
             log("e2e", json.dumps(r))
@@ -377,6 +438,7 @@ def main():
         }
         if "e2e_pcie" in head:
             line["e2e_pcie"] = head["e2e_pcie"]
+            line["pcie_peaks"] = head["pcie_peaks"]
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}

@@ -119,16 +119,27 @@ struct rxg_ctx {
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
     uint32_t counts_cap = 0;
-    // staging for the host-buffer path
+    // host-buffer path: a ring of RXG_PIPE_DEPTH staging slots; burst t uses
+    // slot t % depth.  Copies in run on s_h2d, kernels on `stream`, verdict
+    // copies out on s_d2h, chained by events, so burst t+1's frames cross PCIe
+    // while burst t is classified and burst t-1's verdicts come back.
     uint32_t max_pkts = 0;
     uint64_t max_bytes = 0;
-    uint8_t *h_stage = nullptr; // pinned, mbuf gather
-    uint32_t *h_off = nullptr;
-    uint16_t *h_len = nullptr;
-    uint8_t *d_pkts = nullptr;
-    uint32_t *d_off = nullptr;
-    uint16_t *d_len = nullptr;
-    uint4 *d_out = nullptr;
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    struct slot {
+        uint8_t *h_stage = nullptr; // pinned, mbuf gather
+        uint32_t *h_off = nullptr;
+        uint16_t *h_len = nullptr;
+        uint8_t *d_pkts = nullptr;
+        uint32_t *d_off = nullptr;
+        uint16_t *d_len = nullptr;
+        uint4 *d_out = nullptr;
+        hipEvent_t ev_in = nullptr;   // inputs copied (h_stage reusable, kernel may start)
+        hipEvent_t ev_k = nullptr;    // kernel done (d_pkts/d_off/d_len reusable)
+        hipEvent_t ev_done = nullptr; // verdicts in host memory (d_out reusable)
+        uint64_t ticket = 0;          // last burst submitted to this slot (0 = none)
+    } slots[RXG_PIPE_DEPTH];
+    uint64_t next_ticket = 1;
 };
 
 static int ensure_dev(void **p, size_t *cap, size_t bytes) {
@@ -195,13 +206,23 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
         c->max_pkts = max_pkts;
         c->max_bytes = (max_bytes + 15) & ~15ull;
         if (max_pkts && c->max_bytes) {
-            if ((rc = rx_set_hip_error(hipHostMalloc((void **)&c->h_stage, c->max_bytes, 0)))) break;
-            if ((rc = rx_set_hip_error(hipHostMalloc((void **)&c->h_off, max_pkts * 4ull, 0)))) break;
-            if ((rc = rx_set_hip_error(hipHostMalloc((void **)&c->h_len, max_pkts * 2ull, 0)))) break;
-            if ((rc = rx_set_hip_error(hipMalloc(&c->d_pkts, c->max_bytes)))) break;
-            if ((rc = rx_set_hip_error(hipMalloc(&c->d_off, max_pkts * 4ull)))) break;
-            if ((rc = rx_set_hip_error(hipMalloc(&c->d_len, max_pkts * 2ull)))) break;
-            if ((rc = rx_set_hip_error(hipMalloc(&c->d_out, max_pkts * 16ull)))) break;
+            if ((rc = rx_set_hip_error(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking))))
+                break;
+            if ((rc = rx_set_hip_error(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking))))
+                break;
+            for (rxg_ctx::slot &sl : c->slots) {
+                if ((rc = rx_set_hip_error(hipHostMalloc((void **)&sl.h_stage, c->max_bytes, 0)))) break;
+                if ((rc = rx_set_hip_error(hipHostMalloc((void **)&sl.h_off, max_pkts * 4ull, 0)))) break;
+                if ((rc = rx_set_hip_error(hipHostMalloc((void **)&sl.h_len, max_pkts * 2ull, 0)))) break;
+                if ((rc = rx_set_hip_error(hipMalloc(&sl.d_pkts, c->max_bytes)))) break;
+                if ((rc = rx_set_hip_error(hipMalloc(&sl.d_off, max_pkts * 4ull)))) break;
+                if ((rc = rx_set_hip_error(hipMalloc(&sl.d_len, max_pkts * 2ull)))) break;
+                if ((rc = rx_set_hip_error(hipMalloc(&sl.d_out, max_pkts * 16ull)))) break;
+                const unsigned fl = hipEventDisableTiming;
+                if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&sl.ev_in, fl)))) break;
+                if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&sl.ev_k, fl)))) break;
+                if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&sl.ev_done, fl)))) break;
+            }
         }
     } while (0);
     if (rc == RXG_OK) rc = rxg_flows_sync(c, nullptr, 0, nullptr, 0);
@@ -220,21 +241,30 @@ void rxg_close(rxg_ctx *c) {
         return;
     }
     (void)hipSetDevice(c->device);
+    if (c->s_h2d) (void)hipStreamSynchronize(c->s_h2d);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->s_d2h) (void)hipStreamSynchronize(c->s_d2h);
     (void)hipFree(c->d_udp);
     (void)hipFree(c->d_tcp);
     (void)hipFree(c->d_listen);
     (void)hipFree(c->d_counts);
     (void)hipFree(c->d_ws);
     (void)hipFree(c->d_udpc);
-    (void)hipFree(c->d_pkts);
-    (void)hipFree(c->d_off);
-    (void)hipFree(c->d_len);
-    (void)hipFree(c->d_out);
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
-    if (c->h_off) (void)hipHostFree(c->h_off);
-    if (c->h_len) (void)hipHostFree(c->h_len);
+    for (rxg_ctx::slot &sl : c->slots) {
+        (void)hipFree(sl.d_pkts);
+        (void)hipFree(sl.d_off);
+        (void)hipFree(sl.d_len);
+        (void)hipFree(sl.d_out);
+        if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+        if (sl.h_off) (void)hipHostFree(sl.h_off);
+        if (sl.h_len) (void)hipHostFree(sl.h_len);
+        if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
+        if (sl.ev_k) (void)hipEventDestroy(sl.ev_k);
+        if (sl.ev_done) (void)hipEventDestroy(sl.ev_done);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
+    if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
     delete c;
 }
 
@@ -374,32 +404,85 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     return RXG_OK;
 }
 
-int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
-                      const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out) {
-    if (!c) return RXG_EINVAL;
-    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (n == 0) return RXG_OK;
-    if (!pkts || !off || !len || !out) return RXG_EINVAL;
-    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    if (n > c->max_pkts || !c->d_pkts) return RXG_ERANGE;
-    const uint64_t span = (span_bytes + 15) & ~15ull;
-    if (span > c->max_bytes) return RXG_ERANGE;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpyAsync(c->d_pkts, pkts, span, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_off, off, n * 4ull, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_len, len, n * 2ull, hipMemcpyHostToDevice, c->stream));
+// burst -> slot: device-side ordering only (the host blocks in rxg_wait):
+// the copy in waits until the slot's previous kernel has read its inputs, the
+// kernel until the slot's previous verdicts have left d_out.
+static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint64_t span,
+                       const uint32_t *off, const uint16_t *len, uint32_t n,
+                       uint32_t off_unit_log2, rxg_verdict *out, uint64_t ticket) {
+    const bool reused = sl.ticket != 0;
+    if (reused) HIPCHK(hipStreamWaitEvent(c->s_h2d, sl.ev_k, 0));
+    HIPCHK(hipMemcpyAsync(sl.d_pkts, pkts, span, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipMemcpyAsync(sl.d_off, off, n * 4ull, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipMemcpyAsync(sl.d_len, len, n * 2ull, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipEventRecord(sl.ev_in, c->s_h2d));
+    HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+    if (reused) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
     if (size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, c->d_counts != nullptr)) {
-        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
-        if (rc) return rc;
+        if (ws > c->d_ws_cap) { // grows only between bursts: drain the kernels using it
+            HIPCHK(hipStreamSynchronize(c->stream));
+            int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
+            if (rc) return rc;
+        }
     }
     rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(c->d_pkts, c->d_off, c->d_len, n, off_unit_log2, g, p, fpg, pipe,
-                              c->ft, c->d_out, c->d_counts, c->stream, c->d_ws));
-    HIPCHK(hipMemcpyAsync(out, c->d_out, n * 16ull, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(rx_classify_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, g, p, fpg, pipe,
+                              c->ft, sl.d_out, c->d_counts, c->stream, c->d_ws));
+    HIPCHK(hipEventRecord(sl.ev_k, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
+    HIPCHK(hipMemcpyAsync(out, sl.d_out, n * 16ull, hipMemcpyDeviceToHost, c->s_d2h));
+    HIPCHK(hipEventRecord(sl.ev_done, c->s_d2h));
+    sl.ticket = ticket;
     return RXG_OK;
+}
+
+static int check_host_burst(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                            const uint16_t *len, uint32_t n, uint32_t off_unit_log2,
+                            const rxg_verdict *out) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (!pkts || !off || !len || !out) return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    if (n > c->max_pkts || !c->slots[0].d_pkts) return RXG_ERANGE;
+    if (((span_bytes + 15) & ~15ull) > c->max_bytes) return RXG_ERANGE;
+    return RXG_OK;
+}
+
+int rxg_submit(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+               const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out,
+               uint64_t *ticket) {
+    if (ticket) *ticket = 0;
+    if (n == 0) return c ? RXG_OK : RXG_EINVAL;
+    int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2, out);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t t = c->next_ticket++;
+    rc = submit_slot(c, c->slots[t % RXG_PIPE_DEPTH], pkts, (span_bytes + 15) & ~15ull, off, len,
+                     n, off_unit_log2, out, t);
+    if (rc == RXG_OK && ticket) *ticket = t;
+    return rc;
+}
+
+int rxg_wait(rxg_ctx *c, uint64_t ticket) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (ticket == 0) return RXG_OK; // empty burst
+    if (ticket >= c->next_ticket) return RXG_EINVAL;
+    const rxg_ctx::slot &sl = c->slots[ticket % RXG_PIPE_DEPTH];
+    // a slot reused by a later burst: its events now mark that burst, which
+    // completes after this one (stream order), so waiting on it is safe
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventSynchronize(sl.ev_done));
+    return RXG_OK;
+}
+
+int rxg_classify_span(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                      const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out) {
+    uint64_t t = 0;
+    int rc = rxg_submit(c, pkts, span_bytes, off, len, n, off_unit_log2, out, &t);
+    return rc ? rc : rxg_wait(c, t);
 }
 
 int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
@@ -422,21 +505,26 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
     if (n == 0) return RXG_OK;
     if (!m || !out) return RXG_EINVAL;
-    if (n > c->max_pkts || !c->h_stage) return RXG_ERANGE;
+    if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t t = c->next_ticket++;
+    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+    if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_stage
     // gather frames (buf_addr + data_off, data_len bytes) at 64-B aligned slots
     uint64_t pos = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
         const uint32_t l = m[i]->data_len;
-        const uint64_t slot = (l + 63ull) & ~63ull;
-        if (pos + std::max<uint64_t>(slot, 64) > c->max_bytes) return RXG_ERANGE;
-        memcpy(c->h_stage + pos, (const uint8_t *)m[i]->buf_addr + m[i]->data_off, l);
-        if (slot > l) memset(c->h_stage + pos + l, 0, slot - l);
-        c->h_off[i] = (uint32_t)(pos >> 6);
-        c->h_len[i] = (uint16_t)l;
-        pos += std::max<uint64_t>(slot, 64);
+        const uint64_t step = std::max<uint64_t>((l + 63ull) & ~63ull, 64);
+        if (pos + step > c->max_bytes) return RXG_ERANGE;
+        memcpy(sl.h_stage + pos, (const uint8_t *)m[i]->buf_addr + m[i]->data_off, l);
+        if (step > l) memset(sl.h_stage + pos + l, 0, step - l);
+        sl.h_off[i] = (uint32_t)(pos >> 6);
+        sl.h_len[i] = (uint16_t)l;
+        pos += step;
     }
-    return rxg_classify(c, c->h_stage, c->h_off, c->h_len, n, 6, out);
+    int rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    return rc ? rc : rxg_wait(c, t);
 }
 
 int rxg_flow_counts(rxg_ctx *c, uint64_t *counts, uint32_t ncounts) {
@@ -445,7 +533,7 @@ int rxg_flow_counts(rxg_ctx *c, uint64_t *counts, uint32_t ncounts) {
     const uint32_t nf = c->ft.nu + c->ft.nt;
     if (ncounts < nf) return RXG_ERANGE;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream)); // every submitted burst's kernel has counted
     if (nf) HIPCHK(hipMemcpy(counts, c->d_counts, nf * 8ull, hipMemcpyDeviceToHost));
     return RXG_OK;
 }

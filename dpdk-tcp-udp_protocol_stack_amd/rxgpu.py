@@ -122,11 +122,22 @@ _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
 _gen_flows = _sig("rxg_gen_flows", _i32, C.POINTER(GenCfg), _vp, _vp)
 _gen_host = _sig("rxg_gen_host", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32)
 _gen_dev = _sig("rxg_gen_dev", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32, _vp)
+_submit = _sig("rxg_submit", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32, _vp, C.POINTER(_u64))
+_wait = _sig("rxg_wait", _i32, _vp, _u64)
+_pcap_open = _sig("rxg_pcap_open", _i32, C.POINTER(_vp), C.c_char_p)
+_pcap_close = _sig("rxg_pcap_close", None, _vp)
+_pcap_rewind = _sig("rxg_pcap_rewind", _i32, _vp)
+_pcap_read = _sig("rxg_pcap_read_burst", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32,
+                  C.POINTER(_u32), C.POINTER(_u64))
+_pcap_write = _sig("rxg_pcap_write", _i32, C.c_char_p, _vp, _vp, _vp, _u32, _u32)
+PIPE_DEPTH = 3
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
-            "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev"]
+            "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
+            "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
+            "rxg_pcap_write"]
 
 
 class RxgError(RuntimeError):
@@ -235,6 +246,17 @@ class Context:
         _check(_classify_span(self._h, pkts_ptr, span, off_ptr, len_ptr, n, off_unit_log2,
                               out_ptr), "rxg_classify_span")
 
+    def submit(self, pkts_ptr: int, span: int, off_ptr: int, len_ptr: int, n: int,
+               off_unit_log2: int, out_ptr: int) -> int:
+        """raw-pointer pipelined burst (pinned host buffers); returns the ticket"""
+        t = _u64()
+        _check(_submit(self._h, pkts_ptr, span, off_ptr, len_ptr, n, off_unit_log2, out_ptr,
+                       C.byref(t)), "rxg_submit")
+        return t.value
+
+    def wait(self, ticket: int):
+        _check(_wait(self._h, ticket), "rxg_wait")
+
     def classify_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
                      d_out, d_counts=None, stream=None):
         """Device tensors in/out (torch tensors or raw ints), asynchronous on `stream`."""
@@ -258,6 +280,53 @@ class Context:
 
     def counts_reset(self):
         _check(_counts_reset(self._h), "rxg_counts_reset")
+
+
+class Pcap:
+    """rxg_pcap: a capture file read burst by burst into the packed layout."""
+
+    def __init__(self, path: str):
+        h = _vp()
+        _check(_pcap_open(C.byref(h), path.encode()), "rxg_pcap_open")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _pcap_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rewind(self):
+        _check(_pcap_rewind(self._h), "rxg_pcap_rewind")
+
+    def read_burst_into(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
+                        off_unit_log2: int = 6):
+        """fill caller arrays (e.g. pinned tensors' numpy views); returns (n, span)"""
+        n, span = _u32(), _u64()
+        _check(_pcap_read(self._h, _ptr(pkts), pkts.nbytes, _ptr(off), _ptr(lens), len(off),
+                          off_unit_log2, C.byref(n), C.byref(span)), "rxg_pcap_read_burst")
+        return n.value, span.value
+
+    def read_burst(self, max_frames: int, cap_bytes: int, off_unit_log2: int = 6):
+        pkts = np.zeros(cap_bytes, np.uint8)
+        off = np.zeros(max_frames, np.uint32)
+        lens = np.zeros(max_frames, np.uint16)
+        n, span = self.read_burst_into(pkts, off, lens, off_unit_log2)
+        return pkts[:span + 16], off[:n], lens[:n]
+
+
+def pcap_write(path: str, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
+               off_unit_log2: int = 6):
+    pkts = np.ascontiguousarray(pkts, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    lens = np.ascontiguousarray(lens, np.uint16)
+    _check(_pcap_write(path.encode(), _ptr(pkts), _ptr(off), _ptr(lens), len(off), off_unit_log2),
+           "rxg_pcap_write")
 
 
 def rss_hash(sip: int, dip: int, sport: int, dport: int) -> int:

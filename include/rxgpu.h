@@ -173,6 +173,20 @@ int rxg_classify_span(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, co
  * netfamily.c:147.  Frames are gathered into the context's staging buffer. */
 int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
 
+/* Pipelined host-buffer bursts (PCIe-inclusive, overlapped).  The context owns
+ * RXG_PIPE_DEPTH staging slots (each sized by rxg_open's max_pkts/max_bytes);
+ * burst t copies in while burst t-1 is classified and burst t-2's verdicts
+ * copy out.  rxg_submit returns at once with a ticket; the caller keeps pkts,
+ * off, len and out untouched until rxg_wait(ticket) returns (pass pinned host
+ * memory, e.g. hipHostMalloc'd or hipHostRegister'ed, or the copies are not
+ * asynchronous).  Tickets complete in submission order.  rxg_classify_span is
+ * rxg_submit + rxg_wait. */
+#define RXG_PIPE_DEPTH 3
+int rxg_submit(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+               const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out,
+               uint64_t *ticket);
+int rxg_wait(rxg_ctx *ctx, uint64_t ticket);
+
 /* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
  * loaded up front, frames per lane group, pipeline mode; 0xFFFFFFFF = the
  * default pipeline); lanes_per_frame = 0 = automatic from len_hint.  Unknown
@@ -198,6 +212,26 @@ uint32_t rxg_ft_lookup_tcp(const rxg_ctx *ctx, uint32_t sip, uint32_t dip, uint1
 /* RSS: Toeplitz hash (standard 40-byte key) over sip,dip,sport,dport in
  * network byte order, as a multi-queue NIC computes it; shard = hash % n. */
 uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
+
+/* ---- pcap ingest (the NIC stand-in: rte_eth_rx_burst into the in-ring,
+ * netfamily.c:438-440) -------------------------------------------------- */
+/* Classic libpcap files, LINKTYPE_ETHERNET, either byte order, us or ns
+ * stamps.  A file is mapped once and read burst by burst in capture order. */
+typedef struct rxg_pcap rxg_pcap;
+int rxg_pcap_open(rxg_pcap **p, const char *path);
+void rxg_pcap_close(rxg_pcap *p);
+int rxg_pcap_rewind(rxg_pcap *p);
+/* Pack up to max_frames next frames into pkts (cap_bytes) in the burst layout:
+ * frame k at off[k] << off_unit_log2, captured length len[k], zero fill to the
+ * next 16-B boundary.  *n = frames packed (0 at end of file), *span = bytes
+ * used.  A record longer than 65535 bytes is RXG_ERANGE; a truncated file is
+ * RXG_EINVAL. */
+int rxg_pcap_read_burst(rxg_pcap *p, uint8_t *pkts, uint64_t cap_bytes, uint32_t *off,
+                        uint16_t *len, uint32_t max_frames, uint32_t off_unit_log2, uint32_t *n,
+                        uint64_t *span);
+/* Write n frames of a burst as a pcap file (capture order = burst order). */
+int rxg_pcap_write(const char *path, const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                   uint32_t n, uint32_t off_unit_log2);
 
 /* ---- synthetic traffic (pktgen) --------------------------------------- */
 /* Deterministic counter-based generator: frame i is a pure function of
