@@ -15,11 +15,17 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define D_DEFAULT_FD_NUM 3   /* common.h:33 */
 #define D_MAX_FD_COUNT 1024  /* common.h:34 */
 #define D_RING_SIZE 1024     /* common.h:29 */
 #define D_TCP_INITIAL_WINDOW 14600
+#define D_TCP_MAX_SEQ 0xffffffffu /* common.h:40 */
+#define TCP_FIN 0x01
+#define TCP_SYN 0x02
+#define TCP_PSH 0x08
+#define TCP_ACK 0x10
 
 enum {
     TCP_STATUS_CLOSED = 0,
@@ -142,7 +148,9 @@ static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
 static rxg_ctx *g_ctx;
 static int g_dirty = 1;
-static uint64_t g_stat[4];
+static uint64_t g_stat[5];
+static unsigned int g_isn_seed; /* tcp_stream_create seeds rand_r with time(NULL) (tcp.c:30-31) */
+static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 
 /* snapshot: creation-order arrays given to rxg_flows_sync, and the blocks
  * their flow ids name */
@@ -282,6 +290,7 @@ void nstack_fini(void) {
     s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL;
     s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = 0;
     memset(g_stat, 0, sizeof(g_stat));
+    g_isn_seed = 0;
     if (g_ctx) rxg_close(g_ctx);
     g_ctx = NULL;
     g_dirty = 1;
@@ -619,12 +628,199 @@ static inline uint16_t rd16(const uint8_t *p) {
     return v;
 }
 
+static inline uint32_t rdbe32(const uint8_t *p) { return ntohl(rd32(p)); }
+
+/* ---- TCP state machine (tcp.c:3-331, dispatch :373-415), driven by verdicts.
+ * Where tcp.c holds unresolved merge-conflict hunks the HEAD side is taken
+ * (rcv_nxt += payloadlen at :244-248 and :266-279, no ntohl round trip). */
+
+/* tcp_stream_search (common.c:31-55) over the live list: the exact 4-tuple
+ * (status ignored), else the first LISTEN block on dport (dst IP ignored) */
+static struct tcp_stream *tcb_search(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport) {
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
+        if (s->sip == sip && s->dip == dip && s->sport == sport && s->dport == dport) return s;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
+        if (s->dport == dport && s->status == TCP_STATUS_LISTEN) return s;
+    return NULL;
+}
+
+static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport,
+                                  int status) { /* tcp_stream_create, tcp.c:3-41 */
+    struct tcp_stream *s = calloc(1, sizeof(*s));
+    if (!s) return NULL;
+    s->sip = sip;
+    s->dip = dip;
+    s->sport = sport;
+    s->dport = dport;
+    s->protocol = IPPROTO_TCP;
+    s->fd = -1;
+    s->status = status;
+    s->rcvbuf = ring_create(D_RING_SIZE);
+    s->sndbuf = ring_create(D_RING_SIZE);
+    if (!s->rcvbuf || !s->sndbuf) {
+        ring_free(s->rcvbuf);
+        ring_free(s->sndbuf);
+        free(s);
+        return NULL;
+    }
+    if (!g_isn_seed) g_isn_seed = (unsigned int)time(NULL);
+    s->snd_nxt = (uint32_t)((unsigned long)rand_r(&g_isn_seed) % D_TCP_MAX_SEQ);
+    pthread_cond_init(&s->cond, NULL);
+    pthread_cond_init(&s->accept_cond, NULL);
+    pthread_mutex_init(&s->mutex, NULL);
+    return s;
+}
+
+static void wake_acceptors(uint16_t dport) { /* tcp.c:107-116 */
+    for (struct tcp_stream *l = g_tcb_set; l; l = l->next)
+        if (l->dport == dport && l->status == TCP_STATUS_LISTEN)
+            pthread_cond_broadcast(&l->accept_cond);
+}
+
+static void queue_ctl(struct tcp_stream *s, uint16_t sport_raw, uint16_t dport_raw, uint8_t flags) {
+    struct tcp_fragment *f = calloc(1, sizeof(*f)); /* ng_tcp_send_ackpkt, tcp.c:187-216 */
+    if (!f) return;
+    f->sport = sport_raw;
+    f->dport = dport_raw;
+    f->seqnum = s->snd_nxt;
+    f->acknum = s->rcv_nxt;
+    f->tcp_flags = flags;
+    f->windows = D_TCP_INITIAL_WINDOW;
+    f->hdrlen_off = 0x50;
+    pthread_mutex_lock(&s->mutex);
+    if (ring_enqueue(s->sndbuf, f)) free(f);
+    pthread_mutex_unlock(&s->mutex);
+}
+
+/* ng_tcp_enqueue_recvbuffer, tcp.c:133-185: payloadlen = tcplen - 4*hl;
+ * > 0: a copy of the payload (bytes past the capture read as 0), 0 or < 0: a
+ * 0-length fragment (nrecv's EOF) */
+static void tcp_enqueue_rcv(struct tcp_stream *s, const uint8_t *f, uint32_t cap, int tcplen) {
+    struct tcp_fragment *fr = calloc(1, sizeof(*fr));
+    if (!fr) return;
+    const uint32_t hl = (cap > 46 ? f[46] : 0) >> 4;
+    fr->dport = ntohs(cap >= 38 ? rd16(f + 36) : 0);
+    fr->sport = ntohs(cap >= 36 ? rd16(f + 34) : 0);
+    const int plen = tcplen - (int)hl * 4;
+    if (plen > 0) {
+        fr->data = calloc(1, (size_t)plen + 1);
+        if (!fr->data) {
+            free(fr);
+            return;
+        }
+        const uint32_t from = 34 + hl * 4;
+        const uint32_t avail = cap > from ? cap - from : 0;
+        memcpy(fr->data, f + from, (uint32_t)plen < avail ? (uint32_t)plen : avail);
+        fr->length = (uint32_t)plen;
+    }
+    pthread_mutex_lock(&s->mutex);
+    int e = ring_enqueue(s->rcvbuf, fr);
+    if (!e) pthread_cond_signal(&s->cond);
+    pthread_mutex_unlock(&s->mutex);
+    if (e) {
+        free(fr->data);
+        free(fr);
+        g_stat[1]++;
+    } else {
+        g_stat[4]++;
+    }
+}
+
+/* tcp_process after the lookup (tcp.c:373-415) for the frame's tcb (g_lock held) */
+static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
+    const uint8_t fl = cap > 47 ? f[47] : 0;
+    const uint16_t sport = cap >= 36 ? rd16(f + 34) : 0, dport = cap >= 38 ? rd16(f + 36) : 0;
+    const uint32_t seq = cap >= 42 ? rdbe32(f + 38) : 0, ack = cap >= 46 ? rdbe32(f + 42) : 0;
+    switch (s->status) {
+    case TCP_STATUS_LISTEN: /* tcp_handle_listen, tcp.c:43-87 */
+        if (fl & TCP_SYN) {
+            struct tcp_stream *syn = tcb_new(cap >= 30 ? rd32(f + 26) : 0, cap >= 34 ? rd32(f + 30) : 0,
+                                             sport, dport, TCP_STATUS_LISTEN);
+            if (!syn) return;
+            LL_ADD(syn, g_tcb_set);
+            g_burst_mutated = 1;
+            g_dirty = 1;
+            syn->rcv_nxt = seq + 1;
+            queue_ctl(syn, dport, sport, TCP_SYN | TCP_ACK);
+            syn->status = TCP_STATUS_SYN_RCVD;
+        }
+        break;
+    case TCP_STATUS_SYN_RCVD: /* tcp_handle_syn_rcvd, tcp.c:89-131 */
+        if (fl & TCP_ACK) {
+            s->status = TCP_STATUS_ESTABLISHED; /* acknum == snd_nxt + 1 only printed */
+            g_dirty = 1;
+            wake_acceptors(s->dport);
+        }
+        break;
+    case TCP_STATUS_ESTABLISHED: { /* tcp_handle_established, tcp.c:218-297 */
+        const int tcplen = (int)(cap >= 18 ? ((uint32_t)f[16] << 8 | f[17]) : 0) - 20; /* :391 */
+        if (fl & TCP_PSH) {
+            tcp_enqueue_rcv(s, f, cap, tcplen);
+            const int plen = tcplen - (int)((cap > 46 ? f[46] : 0) >> 4) * 4;
+            s->rcv_nxt = s->rcv_nxt + (uint32_t)plen;
+            s->snd_nxt = ack;
+            queue_ctl(s, dport, sport, TCP_ACK);
+        }
+        if (fl & TCP_FIN) {
+            s->status = TCP_STATUS_CLOSE_WAIT;
+            g_dirty = 1;
+            tcp_enqueue_rcv(s, f, cap, (cap > 46 ? f[46] : 0) >> 4); /* EOF marker */
+            s->rcv_nxt = s->rcv_nxt + 1;
+            s->snd_nxt = ack;
+            queue_ctl(s, dport, sport, TCP_ACK);
+        }
+        break;
+    }
+    case TCP_STATUS_LAST_ACK: /* tcp_handle_last_ack, tcp.c:312-331 */
+        if (fl & TCP_ACK) {
+            s->status = TCP_STATUS_CLOSED;
+            LL_REMOVE(s, g_tcb_set);
+            void *p;
+            while (ring_dequeue(s->rcvbuf, &p) == 0) {
+                free(((struct tcp_fragment *)p)->data);
+                free(p);
+            }
+            while (ring_dequeue(s->sndbuf, &p) == 0) {
+                free(((struct tcp_fragment *)p)->data);
+                free(p);
+            }
+            ring_free(s->rcvbuf);
+            ring_free(s->sndbuf);
+            free(s);
+            g_burst_mutated = 1;
+            g_dirty = 1;
+        }
+        break;
+    default: /* CLOSED, SYN_SENT, FIN_WAIT_*, CLOSING, TIME_WAIT, CLOSE_WAIT: no-ops */
+        break;
+    }
+}
+
+/* one TCP verdict (g_lock held).  The verdict's lookup is the one the
+ * reference would make against the snapshot the burst was classified with;
+ * once this burst's own deliveries have changed the tcb list (a SYN created
+ * a tcb, an ACK in LAST_ACK freed one), later segments are looked up again on
+ * the live list, as the reference's frame-by-frame loop would.  Returns the
+ * reference's rc for the frame. */
+static int deliver_tcp(const rxg_mbuf *m, const rxg_verdict *v) {
+    if (v->rc == RXG_RC_TCP_BAD_CKSUM) return v->rc; /* depends on the bytes only */
+    const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
+    const uint32_t cap = m->data_len;
+    struct tcp_stream *s;
+    if (g_burst_mutated)
+        s = tcb_search(cap >= 30 ? rd32(f + 26) : 0, cap >= 34 ? rd32(f + 30) : 0,
+                       cap >= 36 ? rd16(f + 34) : 0, cap >= 38 ? rd16(f + 36) : 0);
+    else
+        s = (v->rc == RXG_RC_OK && v->flow_id < s_nt) ? s_tcb_cb[v->flow_id] : NULL;
+    if (!s) return RXG_RC_TCP_NO_TCB;
+    g_stat[2]++;
+    tcp_dispatch(s, f, cap);
+    return RXG_RC_OK;
+}
+
 /* udp.c:25-52 for one verdict (g_lock held) */
 static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v) {
-    if (v->cls == RXG_CLS_TCP) {
-        if (v->rc == RXG_RC_OK) g_stat[2]++;
-        return 0;
-    }
+    if (v->cls == RXG_CLS_TCP) return 0;
     if (v->cls != RXG_CLS_UDP) {
         g_stat[3]++;
         return 0;
@@ -663,14 +859,28 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v) {
     return 1;
 }
 
-int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v) {
+/* verdicts -> sockets, frame by frame in burst order (g_lock held) */
+static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out) {
+    int delivered = 0;
+    g_burst_mutated = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        int rc = v[i].rc;
+        if (v[i].cls == RXG_CLS_TCP)
+            rc = deliver_tcp(m[i], &v[i]);
+        else
+            delivered += deliver_one(m[i], &v[i]);
+        if (rc_out) rc_out[i] = rc;
+    }
+    return delivered;
+}
+
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out) {
     if (!m || !v) return n ? RXG_EINVAL : 0;
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && g_dirty) rc = snapshot();
     int delivered = 0;
-    if (rc == RXG_OK)
-        for (uint32_t i = 0; i < n; i++) delivered += deliver_one(m[i], &v[i]);
+    if (rc == RXG_OK) delivered = deliver_burst(m, n, v, rc_out);
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
 }
@@ -685,44 +895,23 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     if (rc == RXG_OK) rc = rxg_process_mbufs(g_ctx, m, n, s_v);
     int delivered = 0;
     if (rc == RXG_OK) {
-        for (uint32_t i = 0; i < n; i++) {
-            delivered += deliver_one(m[i], &s_v[i]);
-            if (rc_out) rc_out[i] = s_v[i].rc;
-        }
         if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
+        delivered = deliver_burst(m, n, s_v, rc_out);
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
 }
 
 int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status) {
-    struct tcp_stream *s = calloc(1, sizeof(*s)); /* tcp_stream_create, tcp.c:3-41 */
-    if (!s) return -1;
-    s->sip = sip;
-    s->dip = dip;
-    s->sport = sport;
-    s->dport = dport;
-    s->protocol = IPPROTO_TCP;
-    s->fd = -1;
-    s->status = status;
-    s->rcvbuf = ring_create(D_RING_SIZE);
-    s->sndbuf = ring_create(D_RING_SIZE);
-    if (!s->rcvbuf || !s->sndbuf) {
-        ring_free(s->rcvbuf);
-        ring_free(s->sndbuf);
-        free(s);
+    pthread_mutex_lock(&g_lock);
+    struct tcp_stream *s = tcb_new(sip, dip, sport, dport, status);
+    if (!s) {
+        pthread_mutex_unlock(&g_lock);
         return -1;
     }
-    pthread_cond_init(&s->cond, NULL);
-    pthread_cond_init(&s->accept_cond, NULL);
-    pthread_mutex_init(&s->mutex, NULL);
-    pthread_mutex_lock(&g_lock);
     LL_ADD(s, g_tcb_set); /* tcp.c:52 */
     g_dirty = 1;
-    /* wake naccept waiters on a listener of this port (tcp.c:108-116) */
-    for (struct tcp_stream *l = g_tcb_set; l; l = l->next)
-        if (l->dport == dport && l->status == TCP_STATUS_LISTEN)
-            pthread_cond_broadcast(&l->accept_cond);
+    wake_acceptors(dport);
     pthread_mutex_unlock(&g_lock);
     return 0;
 }
@@ -743,7 +932,7 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
 }
 
 uint64_t nstack_stat(int which) {
-    if (which < 0 || which > 3) return 0;
+    if (which < 0 || which > 4) return 0;
     pthread_mutex_lock(&g_lock);
     uint64_t v = g_stat[which];
     pthread_mutex_unlock(&g_lock);

@@ -397,7 +397,7 @@ class NStack:
                    ("nsendto", ssz, [_i32, _vp, C.c_size_t, _i32, _vp, _u32]),
                    ("nclose", _i32, [_i32]),
                    ("nstack_rx_burst", _i32, [_vp, _u32, _vp, _vp]),
-                   ("nstack_deliver", _i32, [_vp, _u32, _vp]),
+                   ("nstack_deliver", _i32, [_vp, _u32, _vp, _vp]),
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp]),
                    ("nstack_stat", _u64, [_i32])]
@@ -475,9 +475,11 @@ class NStack:
         arr = (C.POINTER(Mbuf) * len(ms))(*[C.pointer(m) for m in ms])
         return arr, (bufs, ms)
 
-    def deliver(self, frames: list[bytes], verdicts: np.ndarray) -> int:
+    def deliver(self, frames: list[bytes], verdicts: np.ndarray, rcs: np.ndarray | None = None) -> int:
+        """apply verdicts; rcs (int32[n], optional) receives the per-frame return codes"""
         arr, keep = self.mbufs(frames)
-        r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts))
+        verdicts = np.ascontiguousarray(verdicts, VERDICT_DTYPE)
+        r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts), _ptr(rcs))
         if r < 0:
             _check(r, "nstack_deliver")
         return r

@@ -22,8 +22,16 @@
  *   - the 8 bytes nrecvfrom returns past the payload (offload.length =
  *     dgram_len, udp.c:37, but only dgram_len-8 bytes are stored, udp.c:38) read
  *     as zeros instead of adjacent heap memory.
- * TCP segments are classified (verdicts/return codes) but not yet delivered:
- * the TCP state machine (tcp.c:43-331) is out of this round's scope.
+ * TCP segments that pass classify drive the reference's state machine
+ * (tcp.c:43-331, dispatch :373-415) on the host, frame by frame in burst
+ * order: LISTEN+SYN creates a tcb and queues SYN|ACK, SYN_RCVD+ACK
+ * establishes and wakes naccept, ESTABLISHED+PSH queues the payload for
+ * nrecv and an ACK, +FIN queues the EOF marker and moves to CLOSE_WAIT,
+ * LAST_ACK+ACK frees the tcb.  A burst is classified against one snapshot of
+ * the tcb list; once the burst's own segments change that list (SYN, final
+ * ACK), later segments of the burst are looked up again on the live list, so
+ * the outcome is the reference's sequential one (a SYN and its ACK may share
+ * a burst).  Unresolved merge-conflict hunks of tcp.c take the HEAD side.
  */
 #ifndef NSTACK_H
 #define NSTACK_H
@@ -64,8 +72,9 @@ int nclose(int fd);
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 
 /* Delivery half only: apply verdicts computed by rxg_* for the current
- * control-block snapshot to the frames (UDP -> socket receive rings). */
-int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v);
+ * control-block snapshot to the frames (UDP -> socket receive rings, TCP ->
+ * state machine).  rc_out (nullable) as for nstack_rx_burst. */
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out);
 
 /* Install a tcb as tcp_stream_create + LL_ADD do on a SYN (tcp.c:3-52) and
  * wake a blocked naccept (tcp.c:108-116).  All values raw network order. */
@@ -76,9 +85,9 @@ int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, i
 int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
                  uint32_t *nt);
 
-/* counters: 0 = UDP datagrams delivered, 1 = dropped (receive ring full),
- * 2 = TCP segments accepted by classify but not delivered (state machine out
- * of scope), 3 = frames handed to KNI */
+/* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),
+ * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,
+ * 4 = TCP fragments (payload or EOF) queued for nrecv */
 uint64_t nstack_stat(int which);
 
 #ifdef __cplusplus

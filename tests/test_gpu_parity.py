@@ -285,6 +285,30 @@ def test_nstack_udp_echo_through_gpu(torch_dev):
         ns.fini()
 
 
+def test_nstack_tcp_session_through_gpu(torch_dev):
+    """handshake, data and FIN in ONE GPU-classified burst: the state machine
+    re-resolves segments after the SYN creates the tcb (nstack.h)"""
+    ns = R.NStack(0)
+    L, C_IP = "192.168.100.77", "10.0.0.9"
+    try:
+        lfd = ns.socket(R.SOCK_STREAM)
+        ns.bind(lfd, L, 9999)
+        ns.listen(lfd)
+        seg = lambda fl, p=b"", seq=1000: F.tcp_frame(C_IP, 40000, L, 9999, p, flags=fl, seq=seq)
+        frames = [seg(0x02), seg(0x10, seq=1001), seg(0x18, b"payload", seq=1001),
+                  seg(0x11, seq=1008), F.tcp_frame(C_IP, 40000, L, 9999, b"x", corrupt=True)]
+        delivered, rcs, v = ns.rx_burst(frames)
+        assert list(rcs) == [0, 0, 0, 0, -1]
+        # the GPU saw the pre-burst list: every good segment matched the listener
+        assert list(v["flow_id"][:4]) == [0, 0, 0, 0]
+        cfd, a = ns.accept(lfd)
+        assert a.sin_port == R.port_raw(40000)
+        assert ns.recv(cfd, 64) == (7, b"payload")
+        assert ns.recv(cfd, 64) == (0, b"")
+    finally:
+        ns.fini()
+
+
 @pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
 def test_full_size_properties(ctx, torch_dev, name):
     """BASELINE sizes (16M x 64 B, 4M x 1500 B): verdicts of a random sample of

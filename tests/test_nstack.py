@@ -92,8 +92,11 @@ def test_tcp_listen_accept(ns):
     v = _verdicts(ns, frames)
     assert list(v["rc"]) == [0, 0, -1, -2]
     assert list(v["flow_id"][:2]) == [1, 0]
-    ns.deliver(frames, v)
-    assert ns.stat(2) == 2          # classified, TCP state machine out of scope
+    rcs = np.zeros(len(frames), np.int32)
+    ns.deliver(frames, v, rcs)
+    assert list(rcs) == [0, 0, -1, -2]
+    assert ns.stat(2) == 2          # dispatched to the state machine
+    assert ns.recv(cfd, 64) == (4, b"data")   # ESTABLISHED + PSH (tcp.c:228-252)
     assert ns.recv(cfd, 64)[0] == -1
     assert ns.send(cfd, b"hi") == 2
     assert ns.close(cfd) == 0       # FIN queued, tcb stays until LAST_ACK
@@ -108,3 +111,93 @@ def test_rx_burst_needs_gpu(ns):
     ns.socket(R.SOCK_DGRAM)
     with pytest.raises(R.RxgError):
         ns.rx_burst([F.udp_frame("1.1.1.1", 1, L, 2, b"x")])
+
+
+def _deliver(ns, frames):
+    v = _verdicts(ns, frames)
+    rcs = np.zeros(len(frames), np.int32)
+    ns.deliver(frames, v, rcs)
+    return list(rcs)
+
+
+def _status(ns):
+    _, t = ns.flows()
+    return {(int(x["sip"]), int(x["sport"])): int(x["status"]) for x in t}
+
+
+SYN, ACK, PSH, FIN = 0x02, 0x10, 0x08, 0x01
+C_IP, C_PORT = "10.0.0.9", 40000
+
+
+def _seg(flags, payload=b"", seq=1000, ack=2000):
+    return F.tcp_frame(C_IP, C_PORT, L, 9999, payload, flags=flags, seq=seq, ack=ack)
+
+
+def test_tcp_handshake_in_one_burst(ns):
+    """SYN and its ACK in the same burst: the ACK must see the tcb the SYN
+    created (tcp.c:43-131 run frame by frame), though the burst was classified
+    against the list without it"""
+    lfd = ns.socket(R.SOCK_STREAM)
+    ns.bind(lfd, L, 9999)
+    ns.listen(lfd)
+    key = (R.ip_raw(C_IP), R.port_raw(C_PORT))
+    assert _deliver(ns, [_seg(SYN), _seg(ACK, seq=1001)]) == [0, 0]
+    assert _status(ns)[key] == 4  # SYN_RCVD -> ESTABLISHED
+    cfd, a = ns.accept(lfd)
+    assert cfd > lfd and a.sin_port == R.port_raw(C_PORT)
+
+
+def test_tcp_session_data_fin_close(ns):
+    lfd = ns.socket(R.SOCK_STREAM)
+    ns.bind(lfd, L, 9999)
+    ns.listen(lfd)
+    key = (R.ip_raw(C_IP), R.port_raw(C_PORT))
+    assert _deliver(ns, [_seg(SYN)]) == [0]
+    assert _status(ns)[key] == 2  # SYN_RCVD, SYN|ACK queued
+    assert _deliver(ns, [_seg(ACK, seq=1001)]) == [0]
+    cfd, _ = ns.accept(lfd)
+    # two data segments and a FIN in one burst; a corrupted one is dropped (-1)
+    burst = [_seg(PSH | ACK, b"hello ", seq=1001),
+             F.tcp_frame(C_IP, C_PORT, L, 9999, b"bad", flags=PSH | ACK, corrupt=True),
+             _seg(PSH | ACK, b"world", seq=1007), _seg(FIN | ACK, seq=1012)]
+    assert _deliver(ns, burst) == [0, -1, 0, 0]
+    assert _status(ns)[key] == 9              # CLOSE_WAIT
+    assert ns.stat(4) == 3                    # two payloads + the EOF marker
+    # split read (common.c:483-496): copies 3 bytes, returns the REMAINING
+    # length, and re-enqueues the rest at the ring's tail
+    r, data = ns.recv(cfd, 3)
+    assert r == 3 and data == b"hel"
+    assert ns.recv(cfd, 64) == (5, b"world")
+    assert ns.recv(cfd, 64) == (0, b"")       # EOF marker of the FIN
+    assert ns.recv(cfd, 64) == (3, b"lo ")
+
+
+def test_tcp_last_ack_frees_tcb_mid_burst(ns):
+    lfd = ns.socket(R.SOCK_STREAM)
+    ns.bind(lfd, L, 9999)
+    ns.listen(lfd)
+    ns.tcb_add(C_IP, L, C_PORT, 9999)
+    cfd, _ = ns.accept(lfd)
+    assert ns.close(cfd) == 0                 # FIN queued, LAST_ACK
+    key = (R.ip_raw(C_IP), R.port_raw(C_PORT))
+    assert _status(ns)[key] == 10
+    # the final ACK frees the tcb; the next segment of the same burst falls
+    # through to the listener (no SYN: ignored), a segment to a port with no
+    # listener is -2
+    burst = [_seg(ACK), _seg(PSH | ACK, b"late"),
+             F.tcp_frame(C_IP, C_PORT, L, 80, b"x", flags=PSH | ACK)]
+    assert _deliver(ns, burst) == [0, 0, -2]
+    assert key not in _status(ns)
+    assert len(ns.flows()[1]) == 1            # the listener only
+
+
+def test_tcp_nrecv_eof_after_fin(ns):
+    lfd = ns.socket(R.SOCK_STREAM)
+    ns.bind(lfd, L, 9999)
+    ns.listen(lfd)
+    ns.tcb_add(C_IP, L, C_PORT, 9999)
+    cfd, _ = ns.accept(lfd)
+    assert _deliver(ns, [_seg(PSH | ACK, b"abc"), _seg(FIN | ACK, seq=1003)]) == [0, 0]
+    assert ns.recv(cfd, 64) == (3, b"abc")
+    assert ns.recv(cfd, 64) == (0, b"")       # 0-length fragment = EOF (common.c:497-501)
+    assert ns.recv(cfd, 64)[0] == -1
