@@ -21,6 +21,8 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
                               unsigned long long *counts, hipStream_t s, uint32_t *ws);
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts);
+hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                           uint32_t unit_log2, uint32_t len_hint, hipStream_t s);
 
 static thread_local std::string g_last_hip;
 
@@ -439,11 +441,10 @@ static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint6
 }
 
 static int check_host_burst(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
-                            const uint16_t *len, uint32_t n, uint32_t off_unit_log2,
-                            const rxg_verdict *out) {
+                            const uint16_t *len, uint32_t n, uint32_t off_unit_log2) {
     if (!c) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (!pkts || !off || !len || !out) return RXG_EINVAL;
+    if (!pkts || !off || !len) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     if (n > c->max_pkts || !c->slots[0].d_pkts) return RXG_ERANGE;
     if (((span_bytes + 15) & ~15ull) > c->max_bytes) return RXG_ERANGE;
@@ -455,7 +456,8 @@ int rxg_submit(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint3
                uint64_t *ticket) {
     if (ticket) *ticket = 0;
     if (n == 0) return c ? RXG_OK : RXG_EINVAL;
-    int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2, out);
+    if (!out) return RXG_EINVAL;
+    int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
     const uint64_t t = c->next_ticket++;
@@ -525,6 +527,46 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
     }
     int rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
     return rc ? rc : rxg_wait(c, t);
+}
+
+int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const uint16_t *d_len,
+                     uint32_t n, uint32_t off_unit_log2, uint32_t len_hint, void *stream) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n == 0) return RXG_OK;
+    if (!d_pkts || !d_off || !d_len) return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(tx_cksum_launch(d_pkts, d_off, d_len, n, off_unit_log2, len_hint, (hipStream_t)stream));
+    return RXG_OK;
+}
+
+// host frames through one staging slot: copy in, K2, frames copied back
+int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                 const uint16_t *len, uint32_t n, uint32_t off_unit_log2) {
+    if (n == 0) return c ? RXG_OK : RXG_EINVAL;
+    int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t span = (span_bytes + 15) & ~15ull;
+    const uint64_t t = c->next_ticket++;
+    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+    if (sl.ticket) HIPCHK(hipStreamWaitEvent(c->s_h2d, sl.ev_k, 0));
+    HIPCHK(hipMemcpyAsync(sl.d_pkts, pkts, span, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipMemcpyAsync(sl.d_off, off, n * 4ull, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipMemcpyAsync(sl.d_len, len, n * 2ull, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(hipEventRecord(sl.ev_in, c->s_h2d));
+    HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+    if (sl.ticket) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
+    HIPCHK(tx_cksum_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, (uint32_t)(span / n),
+                           c->stream));
+    HIPCHK(hipEventRecord(sl.ev_k, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
+    HIPCHK(hipMemcpyAsync(pkts, sl.d_pkts, span, hipMemcpyDeviceToHost, c->s_d2h));
+    HIPCHK(hipEventRecord(sl.ev_done, c->s_d2h));
+    sl.ticket = t;
+    HIPCHK(hipEventSynchronize(sl.ev_done));
+    return RXG_OK;
 }
 
 int rxg_flow_counts(rxg_ctx *c, uint64_t *counts, uint32_t ncounts) {

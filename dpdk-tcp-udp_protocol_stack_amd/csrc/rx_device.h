@@ -1,0 +1,92 @@
+// rx_device.h — gfx950 device helpers shared by the classify (rx_classify.hip)
+// and TX checksum (tx_cksum.hip) kernels: lane-group broadcast / reduction
+// over DPP and ds_swizzle, the dot2 word-sum, byte masks at a frame's end, and
+// 16-B streaming loads / stores.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+// ---- intra-group broadcast / reduction (group = G aligned lanes) ----------
+template <int G, int K>
+__device__ __forceinline__ uint32_t gbcast(uint32_t x) {
+    static_assert(K < G, "lane out of group");
+    if constexpr (G == 4) {
+        return __builtin_amdgcn_update_dpp(0u, x, K * 0x55, 0xF, 0xF, false); // quad_perm [K,K,K,K]
+    } else if constexpr (G <= 32) {
+        // ds_swizzle bitmask mode: lane' = (lane & and) | or, within 32 lanes
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (0x1F & ~(G - 1)) | (K << 5));
+    } else {
+        return __builtin_amdgcn_readlane(x, K);
+    }
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t gsum(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x += __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xF, 0xF, false); // row_half_mirror
+    if constexpr (G >= 16) x += __builtin_amdgcn_update_dpp(0u, x, 0x140, 0xF, 0xF, false); // row_mirror
+    if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 10)); // xor 16
+    if constexpr (G == 64) x = __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 32);
+    return x;
+}
+
+typedef unsigned short rx_us2 __attribute__((ext_vector_type(2)));
+
+// acc + x.lo + x.hi in one v_dot2_u32_u16
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t x) {
+    const rx_us2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(rx_us2, x), one, acc, false);
+}
+
+// keep only the bytes of dword x (at frame offset pos) that lie below `end`
+__device__ __forceinline__ uint32_t keep_below(uint32_t x, int32_t pos, int32_t end) {
+    int32_t k = end - pos;
+    k = k < 0 ? 0 : (k > 4 ? 4 : k);
+    return k == 4 ? x : (x & ((1u << (8 * k)) - 1u));
+}
+
+__device__ __forceinline__ uint4 chunk_below(uint4 c, int32_t s, int32_t end) {
+    c.x = keep_below(c.x, s + 0, end);
+    c.y = keep_below(c.y, s + 4, end);
+    c.z = keep_below(c.z, s + 8, end);
+    c.w = keep_below(c.w, s + 12, end);
+    return c;
+}
+
+typedef unsigned int rx_u32x4 __attribute__((ext_vector_type(4)));
+
+// streaming 16-B load / store.  nt (non-temporal) pays for coalesced 1-KiB
+// wave accesses and costs for 16-B-per-lane strided ones (tools/membw.hip), so
+// the policy is a template choice of each kernel.
+template <bool NT = true>
+__device__ __forceinline__ uint4 ldg16(const uint8_t *p) {
+    if constexpr (NT) {
+        const rx_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rx_u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+// one 16-B flow-table slot in a single dwordx4 load (a uint4 member-wise load
+// lets the compiler split off .w, test it, then load .xyz: two round trips)
+__device__ __forceinline__ uint4 ld_slot(const uint4 *p) {
+    const rx_u32x4 v = *reinterpret_cast<const rx_u32x4 *>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
+    const rx_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(p));
+}
+
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+    s = (s >> 16) + (s & 0xFFFFu);
+    s = (s >> 16) + (s & 0xFFFFu);
+    return s;
+}
+
+} // namespace

@@ -130,6 +130,8 @@ _pcap_rewind = _sig("rxg_pcap_rewind", _i32, _vp)
 _pcap_read = _sig("rxg_pcap_read_burst", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32,
                   C.POINTER(_u32), C.POINTER(_u64))
 _pcap_write = _sig("rxg_pcap_write", _i32, C.c_char_p, _vp, _vp, _vp, _u32, _u32)
+_tx_cksum_dev = _sig("rxg_tx_cksum_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp)
+_tx_cksum = _sig("rxg_tx_cksum", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32)
 PIPE_DEPTH = 3
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
@@ -137,7 +139,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
-            "rxg_pcap_write"]
+            "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum"]
 
 
 class RxgError(RuntimeError):
@@ -264,6 +266,25 @@ class Context:
             return x if (x is None or isinstance(x, int)) else x.data_ptr()
         _check(_classify_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, len_hint,
                              p(d_out), p(d_counts), stream), "rxg_classify_dev")
+
+    def tx_cksum(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
+                 off_unit_log2: int) -> np.ndarray:
+        """TX checksum fill of a host burst (PCIe round trip); returns the filled copy"""
+        out = np.array(pkts, np.uint8, copy=True)
+        off = np.ascontiguousarray(off, np.uint32)
+        lens = np.ascontiguousarray(lens, np.uint16)
+        span = max(((int(o) << off_unit_log2) + int(n) for o, n in zip(off, lens)), default=0)
+        _check(_tx_cksum(self._h, _ptr(out), span, _ptr(off), _ptr(lens), len(off), off_unit_log2),
+               "rxg_tx_cksum")
+        return out
+
+    def tx_cksum_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
+                     stream=None):
+        """in-place TX checksum fill of a device burst (torch tensors or raw ints)"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        _check(_tx_cksum_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, len_hint,
+                             stream), "rxg_tx_cksum_dev")
 
     def process_mbufs(self, mbufs) -> np.ndarray:
         arr = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])

@@ -187,6 +187,21 @@ int rxg_submit(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, const uin
                uint64_t *ticket);
 int rxg_wait(rxg_ctx *ctx, uint64_t ticket);
 
+/* TX checksum generation (the send side's per-frame work, udp.c:84-95 and
+ * tcp.c:444-463): for every IPv4 frame of the burst, the IPv4 header checksum
+ * (rte_ipv4_cksum, rte_ip.h:255-265) is written at frame offset 24, and for
+ * IPv4 UDP/TCP frames the L4 checksum (rte_ipv4_udptcp_cksum, :325-349; UDP
+ * 0 -> 0xFFFF) at offset 40 / 50, each computed with its own field taken as 0
+ * and the reference's rx conventions (L4 at ip+20, length tl-20, bytes past
+ * the captured length read as 0).  Frames are modified in place; fields not
+ * wholly inside the captured length and non-IPv4 frames are left as they are.
+ * Device form: asynchronous on `stream`.  Host form: pkts (span_bytes, pinned
+ * for speed) is copied to the device, checksummed and copied back; synchronous. */
+int rxg_tx_cksum_dev(rxg_ctx *ctx, uint8_t *d_pkts, const uint32_t *d_off, const uint16_t *d_len,
+                     uint32_t n, uint32_t off_unit_log2, uint32_t len_hint, void *stream);
+int rxg_tx_cksum(rxg_ctx *ctx, uint8_t *pkts, uint64_t span_bytes, const uint32_t *off,
+                 const uint16_t *len, uint32_t n, uint32_t off_unit_log2);
+
 /* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
  * loaded up front, frames per lane group, pipeline mode; 0xFFFFFFFF = the
  * default pipeline); lanes_per_frame = 0 = automatic from len_hint.  Unknown

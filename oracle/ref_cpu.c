@@ -355,6 +355,34 @@ void oracle_classify(const oracle_tables *tb, const uint8_t *pkts, const uint32_
 }
 
 /* ------------------------------------------------------------------ */
+/* TX checksum fill, in place: what ng_encode_udp_apppkt (udp.c:84-95) and
+ * ng_encode_tcp_apppkt (tcp.c:444-463) store — rte_ipv4_cksum of the IPv4
+ * header and rte_ipv4_udptcp_cksum of the L4 segment, each with its own field
+ * zeroed first — for every IPv4 (UDP/TCP) frame of a burst; bytes past the
+ * captured length read as 0 and fields not wholly captured are not written. */
+void oracle_tx_cksum(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                     uint32_t off_unit_log2) {
+    uint8_t *scratch = (uint8_t *)malloc(SCRATCH_BYTES);
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t *f = pkts + ((uint64_t)off[i] << off_unit_log2);
+        const uint32_t cap = len[i];
+        if (rdbe16s(f, cap, 12) != 0x0800) continue;
+        uint8_t ip[20];
+        for (uint32_t k = 0; k < 20; k++) ip[k] = rd8(f, cap, 14 + k);
+        ip[10] = ip[11] = 0; /* pstIp->hdr_checksum = 0 (udp.c:84, tcp.c:444) */
+        const uint16_t hc = oracle_ipv4_cksum(ip);
+        if (cap >= 26) memcpy(f + 24, &hc, 2);
+        const uint8_t proto = ip[9];
+        if (proto != 17 && proto != 6) continue;
+        const uint32_t tl = rdbe16s(f, cap, 16);
+        const uint32_t hole = proto == 17 ? 40 : 50; /* dgram_cksum / cksum = 0 (udp.c:94, tcp.c:462) */
+        const uint16_t c = frame_cksum(f, cap, hole, 34 + (tl >= 20 ? tl - 20 : 0), scratch);
+        if (cap >= hole + 2) memcpy(f + hole, &c, 2);
+    }
+    free(scratch);
+}
+
+/* ------------------------------------------------------------------ */
 /* Toeplitz RSS with the standard 40-byte key (Microsoft RSS spec)       */
 
 static const uint8_t k_rss_key[40] = {

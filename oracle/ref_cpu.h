@@ -41,6 +41,10 @@ void oracle_classify(const oracle_tables *tb, const uint8_t *pkts, const uint32_
                      const uint16_t *len, uint32_t n, uint32_t off_unit_log2, rxg_verdict *out,
                      uint64_t *counts);
 
+/* TX checksum fill in place (udp.c:84-95, tcp.c:444-463), see ref_cpu.c */
+void oracle_tx_cksum(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                     uint32_t off_unit_log2);
+
 /* Toeplitz RSS (same definition as rxg_rss_hash, written independently) */
 uint32_t oracle_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
 

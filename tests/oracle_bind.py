@@ -38,6 +38,8 @@ def _load(name: str):
     lib.oracle_classify.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp]
     lib.oracle_rss_hash.restype = u32
     lib.oracle_rss_hash.argtypes = [u32, u32, u16, u16]
+    lib.oracle_tx_cksum.restype = None
+    lib.oracle_tx_cksum.argtypes = [vp, vp, vp, u32, u32]
     return lib
 
 
@@ -105,6 +107,15 @@ class Tables:
         if counts:
             return out, cnt[: len(self.udp) + len(self.tcb)]
         return out
+
+
+def tx_cksum(pkts: np.ndarray, off: np.ndarray, lens: np.ndarray, off_unit_log2: int) -> np.ndarray:
+    """TX checksum fill (udp.c:84-95, tcp.c:444-463) on a copy of the burst"""
+    out = np.array(pkts, np.uint8, copy=True)
+    off = np.ascontiguousarray(off, np.uint32)
+    lens = np.ascontiguousarray(lens, np.uint16)
+    lib.oracle_tx_cksum(_p(out), _p(off), _p(lens), len(off), off_unit_log2)
+    return out
 
 
 def rss_hash(sip, dip, sport, dport):
