@@ -34,6 +34,7 @@ import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
 COUNTS = True
+TX = True
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 
 
@@ -140,6 +141,21 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                            unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                            traffic=pmc_traffic(name))
+    if TX:  # K2 (TX checksum fill) over the same burst, in place: same bytes read + 4 B written
+        tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        for _ in range(warmup):
+            ctx.tx_cksum_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], stream=sh)
+        for a, b in tev:
+            a.record(stream)
+            ctx.tx_cksum_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], stream=sh)
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        tms = float(np.mean([a.elapsed_time(b) for a, b in tev]))
+        tx_bytes = frame_bytes + 6 * n + 4 * n
+        res["tx_cksum"] = dict(kernel_ms_avg=round(tms, 4), mpps=round(n / tms / 1e3, 1),
+                               gb_per_s=round(tx_bytes / tms / 1e6, 1),
+                               frac=round(tx_bytes / tms / 1e6 / HBM_PEAK_GBS, 4))
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
@@ -363,6 +379,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--no-tx", action="store_true", help="skip timing the TX checksum kernel")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; "
                     "gloo only to rehearse N > 1 on one GPU)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
@@ -388,8 +405,9 @@ def main():
     torch.cuda.set_device(dev)
 
     ctx = R.Context(local)
-    global COUNTS
+    global COUNTS, TX
     COUNTS = not a.no_counts
+    TX = not a.no_tx
     if a.variant:
         ctx.tune(*[int(x) for x in a.variant.split(",")])
     if a.sweep:

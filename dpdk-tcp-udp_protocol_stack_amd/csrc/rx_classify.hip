@@ -486,6 +486,30 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
     }
 }
 
+// The first 64 B of the wave's 64 frames when they sit in consecutive 64-B
+// slots starting at b: four coalesced 1-KiB loads (lane l holds chunk
+// q*64 + l = quarter l%4 of frame 16q + l/4), written to this wave's 4-KiB LDS
+// stage with the quarter index rotated by (frame>>2)&3 so that the read-back
+// (lane f reads its frame's four quarters, ds_read_b128) is bank-conflict
+// free, then read back one frame per lane.  Replaces four per-lane strided
+// 16-B loads (64 distinct 64-B segments per instruction) by stream-shaped
+// ones; bytes past a frame's caplen are masked later, as for lane_load.
+__device__ __forceinline__ void lane_load_staged(lane_frame &L, const uint8_t *b, uint4 *st,
+                                                 uint32_t lane) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = ldg16<true>(b + 16u * (q * 64u + lane));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t c = q * 64u + lane, f = c >> 2;
+        st[f * 4u + (((c & 3u) + (f >> 2)) & 3u)] = v[q];
+    }
+    __builtin_amdgcn_wave_barrier(); // LDS ops of one wave run in order; keep the compiler's too
+#pragma unroll
+    for (int k = 0; k < 4; ++k) L.c[k] = st[lane * 4u + ((k + (lane >> 2)) & 3u)];
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Parse + checksum + probe + verdict of one lane-owned frame.  `next` (may be
 // null) is the following trip's frame: its loads are issued here, after the
 // current frame's arithmetic and before the current frame's bucket probe, so
@@ -685,7 +709,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0, "LDS table: PIPE 0 only");
+    static_assert(!LDT || PIPE == 0 || PIPE == 12, "LDS table: PIPE 0 / 12 only");
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
@@ -736,6 +760,28 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2, idx);
             lane_load<NTL>(L);
+            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
+        }
+    } else if constexpr (PIPE == 12) {
+        // as 0, but a wave whose 64 frames fill consecutive 64-B slots loads
+        // them coalesced through its LDS stage (lane_load_staged)
+        uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                       (tid >> 6) * 256u;
+        const uint32_t lane = tid & 63u;
+        for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
+            lane_frame L;
+            lane_desc(L, p, n, pkts, off, len, unit_log2, idx);
+            const uint64_t fpos = (uint64_t)(L.fb - pkts);
+            const uint64_t f0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fpos >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)fpos);
+            // (the 4 KiB must lie inside the buffer: slots 0..62 end where the
+            // next frame starts, slot 63 only if its frame reaches past byte 48)
+            if (__ballot(L.valid && fpos == f0 + 64ull * lane && (lane != 63u || L.cap > 48)) ==
+                ~0ull) // wave-uniform
+                lane_load_staged(L, pkts + f0, stage, lane);
+            else
+                lane_load<NTL>(L);
             lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
         }
     } else if constexpr (PIPE == 3) {
@@ -798,8 +844,8 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
-    const size_t lds =
-        (size_t)((lds_bins + 3u) & ~3u) * 4u + (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u);
+    const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
+                       (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u) + (PIPE == 12 ? 16384u : 0u);
     static int cu = 0;
     static int cached_occ[2] = {0, 0};
     static size_t cached_lds[2] = {~(size_t)0, ~(size_t)0};
@@ -1369,6 +1415,7 @@ struct variant_entry {
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
     // defaults first (measured on MI355X, bench.py --sweep)
+    {1, 4, 1, 12, launch_lane_udpc<12, 0, true, false>, 6},
     {1, 4, 1, 5, launch_lane_udpc<0, 0, true, false>, 6},
     {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
     {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
@@ -1378,6 +1425,8 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 7, launch_lane<1, 0, true, false>}, {1, 4, 1, 8, launch_lane<2, 0, true, false>},
     {1, 4, 1, 9, launch_lane<9, 0, true, false>}, {1, 4, 1, 10, launch_lane<9, 0, false, false>},
     {1, 4, 1, 11, launch_lane<0, 0, true, false>, 6}, // 5 without the LDS UDP table
+    // 12 (first entry): 5 with coalesced LDS-staged head loads; 13: 12 without the LDS UDP table
+    {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},
@@ -1418,8 +1467,8 @@ static const variant_entry k_variants[] = {
 // choice only moves speed.
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
     if (len_hint == 0) len_hint = 1518;
-    if (len_hint <= 64) { // cfg2: 64 B
-        *g = 1, *p = 4, *fpg = 1, *pipe = 5;
+    if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b)
+        *g = 1, *p = 4, *fpg = 1, *pipe = 12;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel
         *g = 0, *p = 0, *fpg = 0, *pipe = 30;
     } else if (len_hint <= 1536) { // cfg3: 1500 B

@@ -155,6 +155,47 @@ __global__ __launch_bounds__(256) void k_build(const u32x4 *__restrict__ in, con
     }
 }
 
+// (e) lane-per-frame through a per-wave LDS transpose: the wave's 64 frames
+// (4 KiB contiguous) arrive as 4 coalesced 1-KiB loads, are written to LDS
+// with a quarter swizzle (conflict-free ds_read_b128), and each lane reads its
+// own frame's four quarters back
+template <bool NT, bool WR>
+__global__ __launch_bounds__(256) void k_lane_lds(const u32x4 *__restrict__ in, size_t nframes,
+                                                  u32x4 *__restrict__ out,
+                                                  unsigned *__restrict__ sink) {
+    __shared__ u32x4 st[4][256];
+    const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    u32x4 *my = st[wv];
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t f0 = (size_t)blockIdx.x * 256 + wv * 64; f0 + 64 <= nframes; f0 += stride) {
+        const u32x4 *p = in + f0 * 4;
+        u32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ld<NT>(p + q * 64 + lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned c = q * 64 + lane, f = c >> 2;
+            my[f * 4 + (((c & 3u) + (f >> 2)) & 3u)] = v[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const u32x4 a = my[lane * 4 + ((0 + (lane >> 2)) & 3u)];
+        const u32x4 b = my[lane * 4 + ((1 + (lane >> 2)) & 3u)];
+        const u32x4 c = my[lane * 4 + ((2 + (lane >> 2)) & 3u)];
+        const u32x4 d = my[lane * 4 + ((3 + (lane >> 2)) & 3u)];
+        __builtin_amdgcn_wave_barrier();
+        const unsigned h = a.x ^ b.y ^ c.z ^ d.w ^ a.w ^ b.x ^ c.y ^ d.z;
+        if (WR) {
+            u32x4 w = {h, a.y, b.z, c.w};
+            if (NT) __builtin_nontemporal_store(w, out + f0 + lane);
+            else out[f0 + lane] = w;
+        } else {
+            acc += h;
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <typename F>
 float timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -213,6 +254,18 @@ int main() {
             ms = timeit([&] { k_build<4><<<g, 256>>>(in, off, len, nframes, tbl, out); }, reps);
             printf("bpc=%d build4 probe, desc prefetch %.3f ms %7.0f GB/s(alg)\n", bpc, ms, alg / ms / 1e6);
         }
+    }
+    for (int blocks_per_cu : {4, 6, 8}) {
+        const int g = cu * blocks_per_cu;
+        float ms;
+        ms = timeit([&] { k_lane<false, true, 0><<<g, 256>>>(in, nframes, out, sink); }, reps);
+        printf("bpc=%d lane         rd+wr stride  %.3f ms %7.0f GB/s (+wr)\n", blocks_per_cu, ms, (bytes + nframes * 16) / ms / 1e6);
+        ms = timeit([&] { k_lane_lds<false, true><<<g, 256>>>(in, nframes, out, sink); }, reps);
+        printf("bpc=%d lane-lds     rd+wr         %.3f ms %7.0f GB/s (+wr)\n", blocks_per_cu, ms, (bytes + nframes * 16) / ms / 1e6);
+        ms = timeit([&] { k_lane_lds<true, true><<<g, 256>>>(in, nframes, out, sink); }, reps);
+        printf("bpc=%d lane-lds nt  rd+wr         %.3f ms %7.0f GB/s (+wr)\n", blocks_per_cu, ms, (bytes + nframes * 16) / ms / 1e6);
+        ms = timeit([&] { k_lane_lds<true, false><<<g, 256>>>(in, nframes, out, sink); }, reps);
+        printf("bpc=%d lane-lds nt  rd            %.3f ms %7.0f GB/s\n", blocks_per_cu, ms, bytes / ms / 1e6);
     }
     for (int blocks_per_cu : {8}) {
         const int g = cu * blocks_per_cu;
