@@ -68,6 +68,11 @@ static int ring_enqueue(struct nring *r, void *p) {
     r->count++;
     return 0;
 }
+static int ring_peek(struct nring *r, void **p) {
+    if (!r->count) return -ENOENT;
+    *p = r->slot[r->head];
+    return 0;
+}
 static int ring_dequeue(struct nring *r, void **p) {
     if (!r->count) return -ENOENT;
     *p = r->slot[r->head];
@@ -150,6 +155,18 @@ static rxg_ctx *g_ctx;
 static int g_dirty = 1;
 static uint64_t g_stat[5];
 static unsigned int g_isn_seed; /* tcp_stream_create seeds rand_r with time(NULL) (tcp.c:30-31) */
+
+/* ARP table and local identity (common.c:145-204; gLocalIp / g_stCpuMac,
+ * netfamily.c:11,13,415) */
+struct arp_entry {
+    uint32_t ip;
+    uint8_t mac[6];
+    struct arp_entry *prev, *next;
+};
+static struct arp_entry *g_arp; /* head-inserted (LL_ADD, common.c:195) */
+static uint32_t g_local_ip;
+static uint8_t g_local_mac[6];
+static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 
 /* snapshot: creation-order arrays given to rxg_flows_sync, and the blocks
@@ -291,6 +308,13 @@ void nstack_fini(void) {
     s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = 0;
     memset(g_stat, 0, sizeof(g_stat));
     g_isn_seed = 0;
+    while (g_arp) {
+        struct arp_entry *e = g_arp;
+        LL_REMOVE(e, g_arp);
+        free(e);
+    }
+    g_local_ip = 0;
+    memset(g_local_mac, 0, sizeof(g_local_mac));
     if (g_ctx) rxg_close(g_ctx);
     g_ctx = NULL;
     g_dirty = 1;
@@ -361,10 +385,12 @@ int nbind(int sockfd, const struct sockaddr *addr, socklen_t addrlen) { /* :342-
         if (h->protocol == IPPROTO_UDP) {
             h->localport = a->sin_port;
             memcpy(&h->localip, &a->sin_addr.s_addr, 4);
+            memcpy(h->localmac, g_local_mac, 6);
         } else {
             struct tcp_stream *s = info;
             s->dport = a->sin_port;
             memcpy(&s->dip, &a->sin_addr.s_addr, 4);
+            memcpy(s->localmac, g_local_mac, 6);
             s->status = TCP_STATUS_CLOSED;
         }
         g_dirty = 1;
@@ -663,6 +689,7 @@ static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, ui
         free(s);
         return NULL;
     }
+    memcpy(s->localmac, g_local_mac, 6); /* tcp.c:32 */
     if (!g_isn_seed) g_isn_seed = (unsigned int)time(NULL);
     s->snd_nxt = (uint32_t)((unsigned long)rand_r(&g_isn_seed) % D_TCP_MAX_SEQ);
     pthread_cond_init(&s->cond, NULL);
@@ -859,12 +886,40 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v) {
     return 1;
 }
 
+static const uint8_t *arp_lookup(uint32_t ip) { /* ng_get_dst_macaddr, common.c:161-175 */
+    for (struct arp_entry *e = g_arp; e; e = e->next)
+        if (e->ip == ip) return e->mac;
+    return NULL;
+}
+
+static int arp_insert(uint32_t ip, const uint8_t *mac) { /* ng_arp_entry_insert, common.c:177-204 */
+    if (arp_lookup(ip)) return 0;
+    struct arp_entry *e = calloc(1, sizeof(*e));
+    if (!e) return 0;
+    e->ip = ip;
+    memcpy(e->mac, mac, 6);
+    LL_ADD(e, g_arp);
+    return 1;
+}
+
+/* the ARP branch of pkt_process (netfamily.c:156-170): an ARP frame whose
+ * target protocol address is the local IP teaches (sender, Ethernet source).
+ * The reference inserts pstIpHdr->src_addr there, a pointer left over from an
+ * earlier IPv4 frame (uninitialised before the first); the ARP sender
+ * protocol address is what that code means and is used here. */
+static void arp_learn(const rxg_mbuf *m) {
+    const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
+    if (m->data_len < 42 || rd32(f + 38) != g_local_ip) return;
+    arp_insert(rd32(f + 28), f + 6);
+}
+
 /* verdicts -> sockets, frame by frame in burst order (g_lock held) */
 static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out) {
     int delivered = 0;
     g_burst_mutated = 0;
     for (uint32_t i = 0; i < n; i++) {
         int rc = v[i].rc;
+        if (v[i].cls == RXG_CLS_ARP) arp_learn(m[i]);
         if (v[i].cls == RXG_CLS_TCP)
             rc = deliver_tcp(m[i], &v[i]);
         else
@@ -929,6 +984,217 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
     }
     pthread_mutex_unlock(&g_lock);
     return rc;
+}
+
+/* ---- TX: one udp_out + tcp_out pass of the protocol loop (netfamily.c:205-206) */
+static inline void wr16be(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+static inline void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+
+/* ng_encode_arp_pkt, common.c:206-241 (request, opcode 1); an all-ones
+ * target MAC puts the zero MAC into the Ethernet destination (:216-223) */
+static uint32_t enc_arp(uint8_t *m, const uint8_t *dst_mac, uint32_t sip, uint32_t dip) {
+    static const uint8_t zero[6];
+    memcpy(m, memcmp(dst_mac, k_default_arp_mac, 6) ? dst_mac : zero, 6);
+    memcpy(m + 6, g_local_mac, 6);
+    wr16be(m + 12, 0x0806);
+    wr16be(m + 14, 1);
+    wr16be(m + 16, 0x0800);
+    m[18] = 6;
+    m[19] = 4;
+    wr16be(m + 20, 1);
+    memcpy(m + 22, g_local_mac, 6);
+    wr32(m + 28, sip);
+    memcpy(m + 32, dst_mac, 6);
+    wr32(m + 38, dip);
+    return 42;
+}
+
+/* IPv4 header of ng_encode_udp_apppkt / ng_encode_tcp_apppkt (udp.c:74-85,
+ * tcp.c:434-445); the header checksum is left 0 for rxg_tx_cksum */
+static void enc_ipv4(uint8_t *ip, uint32_t total_len, uint8_t proto, uint32_t sip, uint32_t dip) {
+    ip[0] = 0x45;
+    ip[1] = 0;
+    wr16be(ip + 2, total_len - 14);
+    wr16be(ip + 4, 0);
+    wr16be(ip + 6, 0);
+    ip[8] = 64;
+    ip[9] = proto;
+    ip[10] = ip[11] = 0;
+    wr32(ip + 12, sip);
+    wr32(ip + 16, dip);
+}
+
+/* ng_encode_udp_apppkt, udp.c:59-98: total = length + 42 */
+static uint32_t enc_udp(uint8_t *m, const uint8_t *src_mac, const uint8_t *dst_mac,
+                        const struct offload *o) {
+    const uint32_t total = (uint32_t)o->length + 42u;
+    memcpy(m, dst_mac, 6);
+    memcpy(m + 6, src_mac, 6);
+    wr16be(m + 12, 0x0800);
+    enc_ipv4(m + 14, total, IPPROTO_UDP, o->sip, o->dip);
+    memcpy(m + 34, &o->sport, 2);
+    memcpy(m + 36, &o->dport, 2);
+    wr16be(m + 38, total - 34); /* dgram_len = 8 + payload (udp.c:91-92) */
+    m[40] = m[41] = 0;
+    if (o->length) memcpy(m + 42, o->data, o->length);
+    return total;
+}
+
+/* ng_encode_tcp_apppkt, tcp.c:420-466: total = 54 + 4*optlen + length; the
+ * window is stored without htons (tcp.c:454), options are not written (0) */
+static uint32_t enc_tcp(uint8_t *m, const uint8_t *src_mac, const uint8_t *dst_mac, uint32_t sip,
+                        uint32_t dip, const struct tcp_fragment *f) {
+    const uint32_t opt = (uint32_t)f->optlen * 4u, total = 54u + opt + f->length;
+    memcpy(m, dst_mac, 6);
+    memcpy(m + 6, src_mac, 6);
+    wr16be(m + 12, 0x0800);
+    enc_ipv4(m + 14, total, IPPROTO_TCP, sip, dip);
+    uint8_t *t = m + 34;
+    memcpy(t, &f->sport, 2);
+    memcpy(t + 2, &f->dport, 2);
+    wr32(t + 4, htonl(f->seqnum));
+    wr32(t + 8, htonl(f->acknum));
+    t[12] = f->hdrlen_off;
+    t[13] = f->tcp_flags;
+    memcpy(t + 14, &f->windows, 2);
+    t[16] = t[17] = 0;
+    memcpy(t + 18, &f->tcp_urp, 2);
+    memset(t + 20, 0, opt);
+    if (f->data && f->length) memcpy(t + 20 + opt, f->data, f->length);
+    return total;
+}
+
+static inline uint64_t align64(uint64_t x) { return (x + 63u) & ~63ull; }
+
+int nstack_set_local(uint32_t ip, const uint8_t mac[6]) {
+    pthread_mutex_lock(&g_lock);
+    g_local_ip = ip;
+    if (mac) memcpy(g_local_mac, mac, 6);
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+int nstack_arp_insert(uint32_t ip, const uint8_t mac[6]) {
+    if (!mac) return RXG_EINVAL;
+    pthread_mutex_lock(&g_lock);
+    int r = arp_insert(ip, mac);
+    pthread_mutex_unlock(&g_lock);
+    return r;
+}
+
+/* frame k of the burst: zero fill to the 64-B slot end, descriptor */
+static void tx_place(uint8_t *fp, uint32_t fl, uint64_t *pos, uint32_t *off, uint16_t *len,
+                     uint32_t *n) {
+    memset(fp + fl, 0, align64(fl) - fl);
+    off[*n] = (uint32_t)(*pos >> 6);
+    len[*n] = (uint16_t)fl;
+    *pos += align64(fl);
+    ++*n;
+}
+
+int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *len,
+                    uint32_t max_frames, int cksum, uint64_t *span) {
+    if (span) *span = 0;
+    if (!pkts || !off || !len) return max_frames ? RXG_EINVAL : 0;
+    pthread_mutex_lock(&g_lock);
+    uint32_t n = 0;
+    uint64_t pos = 0;
+    int full = 0;
+    /* udp_out, udp.c:123-164: at most one datagram per socket, list order */
+    for (struct localhost *h = g_pstHost; h && n < max_frames && !full; h = h->next) {
+        struct offload *o = NULL;
+        pthread_mutex_lock(&h->mutex);
+        if (ring_peek(h->sndbuf, (void **)&o) != 0) {
+            pthread_mutex_unlock(&h->mutex);
+            continue;
+        }
+        const uint8_t *dmac = arp_lookup(o->dip);
+        const uint32_t fl = dmac ? 42u + o->length : 42u;
+        if (fl > 65535u) { /* no frame can carry it: dropped */
+            ring_dequeue(h->sndbuf, (void **)&o);
+            pthread_mutex_unlock(&h->mutex);
+            free(o->data);
+            free(o);
+            g_stat[1]++;
+            continue;
+        }
+        if (pos + align64(fl) > cap_bytes) {
+            pthread_mutex_unlock(&h->mutex);
+            full = 1;
+            break;
+        }
+        ring_dequeue(h->sndbuf, (void **)&o);
+        uint8_t *fp = pkts + pos;
+        if (!dmac) { /* an ARP request first, the datagram queued again (udp.c:139-146) */
+            enc_arp(fp, k_default_arp_mac, o->sip, o->dip);
+            if (ring_enqueue(h->sndbuf, o)) {
+                free(o->data);
+                free(o);
+                g_stat[1]++;
+            }
+            pthread_mutex_unlock(&h->mutex);
+        } else {
+            pthread_mutex_unlock(&h->mutex);
+            enc_udp(fp, h->localmac, dmac, o);
+            free(o->data);
+            free(o);
+        }
+        tx_place(fp, fl, &pos, off, len, &n);
+    }
+    /* tcp_out, tcp.c:492-555: at most one fragment per tcb, list order */
+    for (struct tcp_stream *s = g_tcb_set; s && n < max_frames && !full; s = s->next) {
+        struct tcp_fragment *f = NULL;
+        pthread_mutex_lock(&s->mutex);
+        if (!s->sndbuf || ring_peek(s->sndbuf, (void **)&f) != 0) {
+            pthread_mutex_unlock(&s->mutex);
+            continue;
+        }
+        const uint8_t *dmac = arp_lookup(s->sip); /* the remote side (tcp.c:521) */
+        const uint64_t fl64 = dmac ? 54u + (uint64_t)f->optlen * 4u + f->length : 42u;
+        if (fl64 > 65535u) {
+            ring_dequeue(s->sndbuf, (void **)&f);
+            pthread_mutex_unlock(&s->mutex);
+            free(f->data);
+            free(f);
+            g_stat[1]++;
+            continue;
+        }
+        const uint32_t fl = (uint32_t)fl64;
+        if (pos + align64(fl) > cap_bytes) {
+            pthread_mutex_unlock(&s->mutex);
+            full = 1;
+            break;
+        }
+        ring_dequeue(s->sndbuf, (void **)&f);
+        uint8_t *fp = pkts + pos;
+        if (!dmac) { /* tcp.c:522-535 */
+            enc_arp(fp, k_default_arp_mac, s->dip, s->sip);
+            if (ring_enqueue(s->sndbuf, f)) {
+                free(f->data);
+                free(f);
+                g_stat[1]++;
+            }
+            pthread_mutex_unlock(&s->mutex);
+        } else {
+            pthread_mutex_unlock(&s->mutex);
+            enc_tcp(fp, s->localmac, dmac, s->dip, s->sip, f); /* local -> remote (tcp.c:542) */
+            free(f->data);
+            free(f);
+        }
+        tx_place(fp, fl, &pos, off, len, &n);
+    }
+    rxg_ctx *ctx = g_ctx;
+    pthread_mutex_unlock(&g_lock);
+    if (span) *span = pos;
+    if (cksum && n) {
+        if (!ctx) return RXG_EINVAL;
+        int rc = rxg_tx_cksum(ctx, pkts, pos, off, len, n, 6); /* K2 on the GPU */
+        if (rc) return rc;
+    }
+    return (int)n;
 }
 
 uint64_t nstack_stat(int which) {

@@ -421,7 +421,10 @@ class NStack:
                    ("nstack_deliver", _i32, [_vp, _u32, _vp, _vp]),
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp]),
-                   ("nstack_stat", _u64, [_i32])]
+                   ("nstack_stat", _u64, [_i32]),
+                   ("nstack_set_local", _i32, [_u32, _vp]),
+                   ("nstack_arp_insert", _i32, [_u32, _vp]),
+                   ("nstack_tx_burst", _i32, [_vp, _u64, _vp, _vp, _u32, _i32, _vp])]
             for name, res, args in sig:
                 f = getattr(lib, name)
                 f.restype, f.argtypes = res, args
@@ -516,3 +519,22 @@ class NStack:
 
     def stat(self, which):
         return self.lib.nstack_stat(which)
+
+    def set_local(self, ip: str, mac: bytes):
+        """gLocalIp + port MAC (netfamily.c:11, 415)"""
+        return self.lib.nstack_set_local(ip_raw(ip), (C.c_uint8 * 6)(*mac))
+
+    def arp_insert(self, ip: str, mac: bytes) -> int:
+        return self.lib.nstack_arp_insert(ip_raw(ip), (C.c_uint8 * 6)(*mac))
+
+    def tx_burst(self, max_frames: int = 256, cap_bytes: int = 1 << 20, cksum: bool = False):
+        """one udp_out + tcp_out pass: the frames (bytes) it produced"""
+        pk = np.zeros(cap_bytes, np.uint8)
+        off = np.zeros(max(max_frames, 1), np.uint32)
+        ln = np.zeros(max(max_frames, 1), np.uint16)
+        span = C.c_uint64()
+        r = self.lib.nstack_tx_burst(_ptr(pk), cap_bytes, _ptr(off), _ptr(ln), max_frames,
+                                     int(cksum), C.byref(span))
+        if r < 0:
+            _check(r, "nstack_tx_burst")
+        return [pk[int(o) << 6:(int(o) << 6) + int(n)].tobytes() for o, n in zip(off[:r], ln[:r])]

@@ -85,9 +85,30 @@ int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, i
 int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
                  uint32_t *nt);
 
+/* ---- TX (the udp_out / tcp_out pass of the protocol loop, netfamily.c:205-206)
+ * Local identity: gLocalIp (netfamily.c:11) and the port MAC g_stCpuMac
+ * (netfamily.c:415).  Frames leave from this MAC (copied into sockets at
+ * nbind and into tcbs at creation, as common.c:356,365 / tcp.c:32 do); an
+ * ARP frame addressed to this IP teaches the ARP table.  Raw network-order ip. */
+int nstack_set_local(uint32_t ip, const uint8_t mac[6]);
+/* ng_arp_entry_insert (common.c:177-204): 1 = inserted, 0 = already known */
+int nstack_arp_insert(uint32_t ip, const uint8_t mac[6]);
+/* One udp_out + tcp_out pass (udp.c:123-164, tcp.c:492-555): at most one
+ * queued datagram per UDP socket and one fragment per tcb, in list order,
+ * encoded as frames (ng_encode_udp_apppkt udp.c:59-98, ng_encode_tcp_apppkt
+ * tcp.c:420-466) into pkts/off/len (the rx burst layout, off in 64-B units).
+ * A destination with no ARP entry gets an ARP request (ng_send_arp,
+ * common.c:206-260) and its item is queued again, as the reference does.
+ * cksum != 0: both checksums are filled on the GPU (rxg_tx_cksum) before the
+ * call returns; 0: both fields are left 0.  Items that do not fit stay queued.
+ * Returns the number of frames (or a negative RXG_E* code); *span = bytes used. */
+int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *len,
+                    uint32_t max_frames, int cksum, uint64_t *span);
+
 /* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),
  * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,
- * 4 = TCP fragments (payload or EOF) queued for nrecv */
+ * 4 = TCP fragments (payload or EOF) queued for nrecv.  Counter 1 also counts
+ * TX items dropped (a send ring full, or a datagram too long for a frame). */
 uint64_t nstack_stat(int which);
 
 #ifdef __cplusplus

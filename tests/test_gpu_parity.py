@@ -309,6 +309,31 @@ def test_nstack_tcp_session_through_gpu(torch_dev):
         ns.fini()
 
 
+def test_nstack_tx_burst_checksums_on_gpu(torch_dev):
+    """udp_out/tcp_out frames with both checksums filled by K2 (rxg_tx_cksum)
+    equal the oracle's fill of the same frames"""
+    ns = R.NStack(0)
+    L = "192.168.100.77"
+    try:
+        ns.set_local(L, F.LOCAL_MAC)
+        ns.arp_insert("10.0.0.1", F.PEER_MAC)
+        ns.arp_insert("10.0.0.9", F.PEER_MAC)
+        fd = ns.socket(R.SOCK_DGRAM)
+        ns.bind(fd, L, 8889)
+        ns.sendto(fd, b"reply" * 100, "10.0.0.1", 5555)
+        lfd = ns.socket(R.SOCK_STREAM)
+        ns.bind(lfd, L, 9999)
+        ns.listen(lfd)
+        ns.rx_burst([F.tcp_frame("10.0.0.9", 40000, L, 9999, b"", flags=0x02)])
+        fr = ns.tx_burst(cksum=True)
+        assert len(fr) == 2
+        buf, off, lens = F.pack_frames(fr, 6)
+        assert np.array_equal(O.tx_cksum(buf, off, lens, 6), buf)
+        assert all(f[24:26] != b"\0\0" for f in fr)
+    finally:
+        ns.fini()
+
+
 @pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
 def test_full_size_properties(ctx, torch_dev, name):
     """BASELINE sizes (16M x 64 B, 4M x 1500 B): verdicts of a random sample of

@@ -2,6 +2,8 @@
 socket-call semantics (common.c:262-666) and UDP delivery with offload
 semantics (udp.c:25-52).  Verdicts for delivery come from the oracle here
 (no GPU); test_gpu_parity.py drives the same path through the GPU."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -201,3 +203,74 @@ def test_tcp_nrecv_eof_after_fin(ns):
     assert ns.recv(cfd, 64) == (3, b"abc")
     assert ns.recv(cfd, 64) == (0, b"")       # 0-length fragment = EOF (common.c:497-501)
     assert ns.recv(cfd, 64)[0] == -1
+
+
+# ---- TX: udp_out / tcp_out (udp.c:59-164, tcp.c:420-555), ARP (common.c:145-260)
+LMAC, PMAC = F.LOCAL_MAC, F.PEER_MAC
+
+
+def _ipv4(tl, proto, src, dst):  # ng_encode_*: id 0, no DF, ttl 64, checksum left 0
+    return struct.pack(">BBHHHBBH4s4s", 0x45, 0, tl, 0, 0, 64, proto, 0, F.ip4(src), F.ip4(dst))
+
+
+def _arp_request(sip, tip):  # ng_encode_arp_pkt with the all-ones target MAC
+    return (bytes(6) + LMAC + b"\x08\x06" + struct.pack(">HHBBH", 1, 0x0800, 6, 4, 1) + LMAC +
+            F.ip4(sip) + b"\xff" * 6 + F.ip4(tip))
+
+
+def test_tx_udp_arp_then_datagram(ns):
+    ns.set_local(L, LMAC)
+    fd = ns.socket(R.SOCK_DGRAM)
+    ns.bind(fd, L, 8889)
+    assert ns.sendto(fd, b"reply", "10.0.0.1", 5555) == 5
+    assert ns.tx_burst() == [_arp_request(L, "10.0.0.1")]     # no ARP entry yet
+    arp_in = F.arp_frame("10.0.0.1", L)                        # the peer's ARP frame teaches it
+    _deliver(ns, [arp_in])
+    want = (PMAC + LMAC + b"\x08\x00" + _ipv4(33, 17, L, "10.0.0.1") +
+            struct.pack(">HHHH", 8889, 5555, 13, 0) + b"reply")
+    fr = ns.tx_burst()
+    assert fr == [want]
+    assert ns.tx_burst() == []
+    # the oracle's TX fill makes it a frame whose checksums verify on rx
+    buf, off, lens = F.pack_frames(fr, 6)
+    filled = O.tx_cksum(buf, off, lens, 6)
+    v = O.Tables(np.zeros(0, R.UDP_SOCK_DTYPE), np.zeros(0, R.TCB_DTYPE)).classify(
+        filled, off, lens, 6)
+    assert v["cksum_ok"][0] == 1 and v["rc"][0] == -3
+
+
+def test_tx_one_datagram_per_socket_per_pass(ns):
+    ns.set_local(L, LMAC)
+    ns.arp_insert("10.0.0.1", PMAC)
+    a, b = ns.socket(R.SOCK_DGRAM), ns.socket(R.SOCK_DGRAM)
+    ns.bind(a, L, 1000)
+    ns.bind(b, L, 2000)
+    for fd, p in ((a, b"a1"), (a, b"a2"), (b, b"b1")):
+        ns.sendto(fd, p, "10.0.0.1", 7777)
+    first = ns.tx_burst()
+    assert [f[42:] for f in first] == [b"b1", b"a1"]           # newest socket first (LL_ADD)
+    assert [f[42:] for f in ns.tx_burst()] == [b"a2"]
+
+
+def test_tx_tcp_synack_and_data(ns):
+    ns.set_local(L, LMAC)
+    ns.arp_insert("10.0.0.9", PMAC)
+    lfd = ns.socket(R.SOCK_STREAM)
+    ns.bind(lfd, L, 9999)
+    ns.listen(lfd)
+    _deliver(ns, [_seg(SYN, seq=5000)])
+    fr = ns.tx_burst()
+    assert len(fr) == 1
+    f = fr[0]
+    assert f[:14] == PMAC + LMAC + b"\x08\x00"
+    assert f[14:34] == _ipv4(40, 6, L, "10.0.0.9")
+    sport, dport, seq, ack, doff, flags = struct.unpack(">HHIIBB", f[34:48])
+    assert (sport, dport, ack, doff, flags) == (9999, 40000, 5001, 0x50, SYN | ACK)
+    assert f[48:50] == (14600).to_bytes(2, "little")           # rx_win without htons (tcp.c:454)
+    assert f[50:54] == bytes(4)                                 # checksum 0, urp 0
+    _deliver(ns, [_seg(ACK, seq=5001, ack=seq + 1)])
+    cfd, _ = ns.accept(lfd)
+    assert ns.send(cfd, b"hi there") == 8
+    f = ns.tx_burst()[0]
+    assert f[47] == PSH | ACK and f[54:] == b"hi there" and len(f) == 62
+    assert struct.unpack(">I", f[42:46])[0] == 5001             # acknum = rcv_nxt
