@@ -454,6 +454,8 @@ def main():
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
         }
+        if "tx_cksum" in head:
+            line["tx_cksum"] = head["tx_cksum"]
         if "e2e_pcie" in head:
             line["e2e_pcie"] = head["e2e_pcie"]
             line["pcie_peaks"] = head["pcie_peaks"]

@@ -32,6 +32,6 @@ if [ "${PROF:-1}" = 1 ]; then
       -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
 fi
 if [ "${PMC:-0}" = 1 ]; then
-  step pmc 600 python tools/pmc_traffic.py $TAG cfg2,cfg3 || exit $?
+  step pmc 600 python tools/pmc_traffic.py $TAG ${PMC_WL:-cfg2,cfg3} || exit $?
 fi
 echo ALLDONE
