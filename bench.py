@@ -215,6 +215,50 @@ def cpu_baseline(name, budget_s):
                 seconds=round(el, 2))
 
 
+def cpu_baseline_mt(name, budget_s, threads):
+    """the same oracle on `threads` host cores, the
+    sample split into one contiguous shard per thread (every verdict depends
+    only on its own frame, so any split is an RSS-style shard).  ctypes drops
+    the GIL inside the C call, so the threads run in parallel."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as O  # cpu_baseline leg only
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name)
+    sample = {"cfg2": 1 << 20, "cfg3": 1 << 16, "cfg4": 1 << 16, "cfg5": 1 << 12}[name]
+    pk, off, ln = R.gen_host(cfg, 0, sample, w["unit_log2"])
+    udp, tcb = R.gen_flows(cfg)
+    tb = O.Tables(udp, tcb)
+    k = min(sample, 4096)
+    t0 = time.perf_counter()
+    tb.classify(pk, off[:k], ln[:k], w["unit_log2"])
+    per = (time.perf_counter() - t0) / k  # one core
+    per_thread = max(k, int(budget_s / max(per, 1e-9)))
+    bounds = np.linspace(0, sample, threads + 1).astype(np.int64)
+    done = [0] * threads
+
+    def work(i):
+        lo, hi = int(bounds[i]), int(bounds[i + 1])
+        o, l = off[lo:hi], ln[lo:hi]
+        n = 0
+        while n < per_thread:
+            tb.classify(pk, o, l, w["unit_log2"])
+            n += hi - lo
+        done[i] = n
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    return dict(value=round(sum(done) / el / 1e6, 4), unit="Mpps", cores=threads, kind="port",
+                sample=f"{sum(done)} frames of {name} ({sample} distinct, {threads} contiguous "
+                       f"shards cycled); oracle/ref_cpu.c -O2, list-scan lookups, "
+                       f"{threads} threads", seconds=round(el, 2))
+
+
 # ---------------------------------------------------------------------------
 def e2e(name, local, batch, reps=20, inflight=4):
     """PCIe-inclusive rate of the host-buffer path: pinned host frames +
@@ -376,6 +420,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2,cfg3")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the all-cores CPU baseline (the GPU box's CPU share "
+                         "is 16 per GPU; 0/1 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
@@ -417,9 +464,11 @@ def main():
     results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}
     head = results[names[0]]
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(names[0], a.cpu_budget)
+        cpu_mt = cpu_baseline_mt(names[0], a.cpu_budget / 2, a.cpu_threads) \
+            if a.cpu_threads > 1 else None
         for nm in names[1:]:
             results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget / 2)
 
@@ -451,6 +500,7 @@ def main():
             "gb_per_s": round(head["gbps"], 2),
             "roofline": head["roofline"],
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_mt,
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
         }
