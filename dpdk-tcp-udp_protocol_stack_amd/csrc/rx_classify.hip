@@ -487,27 +487,13 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 }
 
 // The first 64 B of the wave's 64 frames when they sit in consecutive 64-B
-// slots starting at b: four coalesced 1-KiB loads (lane l holds chunk
-// q*64 + l = quarter l%4 of frame 16q + l/4), written to this wave's 4-KiB LDS
-// stage with the quarter index rotated by (frame>>2)&3 so that the read-back
-// (lane f reads its frame's four quarters, ds_read_b128) is bank-conflict
-// free, then read back one frame per lane.  Replaces four per-lane strided
-// 16-B loads (64 distinct 64-B segments per instruction) by stream-shaped
-// ones; bytes past a frame's caplen are masked later, as for lane_load.
+// slots starting at b: stage64_load (rx_device.h), four coalesced 1-KiB loads
+// through this wave's 4-KiB LDS stage, replacing four per-lane strided 16-B
+// loads (64 distinct 64-B segments per instruction); bytes past a frame's
+// caplen are masked later, as for lane_load.
 __device__ __forceinline__ void lane_load_staged(lane_frame &L, const uint8_t *b, uint4 *st,
                                                  uint32_t lane) {
-    uint4 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = ldg16<true>(b + 16u * (q * 64u + lane));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t c = q * 64u + lane, f = c >> 2;
-        st[f * 4u + (((c & 3u) + (f >> 2)) & 3u)] = v[q];
-    }
-    __builtin_amdgcn_wave_barrier(); // LDS ops of one wave run in order; keep the compiler's too
-#pragma unroll
-    for (int k = 0; k < 4; ++k) L.c[k] = st[lane * 4u + ((k + (lane >> 2)) & 3u)];
-    __builtin_amdgcn_wave_barrier();
+    stage64_load(b, st, lane, L.c);
 }
 
 // Parse + checksum + probe + verdict of one lane-owned frame.  `next` (may be

@@ -83,6 +83,28 @@ __device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
     __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(p));
 }
 
+// The first 64 B of a wave's 64 frames that sit in consecutive 64-B slots
+// starting at b, one frame per lane, read as four coalesced 1-KiB loads (lane
+// l holds chunk q*64 + l = quarter l%4 of frame 16q + l/4), written to the
+// wave's 4-KiB LDS stage st with the quarter index rotated by (frame>>2)&3 so
+// that the read-back (lane f reads its frame's four quarters, ds_read_b128) is
+// bank-conflict free.  The caller checks that the 4 KiB lie in the buffer.
+__device__ __forceinline__ void stage64_load(const uint8_t *b, uint4 *st, uint32_t lane,
+                                             uint4 (&c)[4]) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = ldg16<true>(b + 16u * (q * 64u + lane));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t k = q * 64u + lane, f = k >> 2;
+        st[f * 4u + (((k & 3u) + (f >> 2)) & 3u)] = v[q];
+    }
+    __builtin_amdgcn_wave_barrier(); // LDS ops of one wave run in order; keep the compiler's too
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = st[lane * 4u + ((k + (lane >> 2)) & 3u)];
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
     s = (s >> 16) + (s & 0xFFFFu);
     s = (s >> 16) + (s & 0xFFFFu);

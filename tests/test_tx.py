@@ -4,6 +4,8 @@ ng_encode_tcp_apppkt (tcp.c:444-463) do.  The oracle's fill is pinned against
 the pktgen's independently built checksums; the gfx950 kernel (K2) against
 the oracle, bit-exact on whole buffers, and at BASELINE sizes through the
 round trip "zero the fields -> K2 -> identical to the generated burst"."""
+import os
+
 import numpy as np
 import pytest
 
@@ -101,13 +103,21 @@ def test_gpu_tx_cksum_matches_oracle():
     with R.Context(0, max_pkts=len(off), max_bytes=len(buf) + 64) as ctx:
         got = ctx.tx_cksum(buf, off, lens, 4)                    # host path
         assert np.array_equal(got, want)
-        for hint in (64, 1500, 9000):                            # each lanes-per-frame width
-            d = torch.from_numpy(buf.copy()).to(dev)
-            ctx.tx_cksum_dev(d, torch.from_numpy(off.view(np.int32)).to(dev),
-                             torch.from_numpy(lens.view(np.int16)).to(dev), len(off), 4, hint,
-                             torch.cuda.current_stream(dev).cuda_stream)
-            torch.cuda.synchronize(dev)
-            assert np.array_equal(d.cpu().numpy(), want), hint
+        # each default width (by len_hint), then every tuning variant of
+        # tx_cksum.hip's k_tx table (forced through RXG_TX_VARIANT)
+        runs = [(hint, None) for hint in (64, 128, 1500, 9000)] + [(1500, v) for v in range(13)]
+        try:
+            for hint, v in runs:
+                if v is not None:
+                    os.environ["RXG_TX_VARIANT"] = str(v)
+                d = torch.from_numpy(buf.copy()).to(dev)
+                ctx.tx_cksum_dev(d, torch.from_numpy(off.view(np.int32)).to(dev),
+                                 torch.from_numpy(lens.view(np.int16)).to(dev), len(off), 4, hint,
+                                 torch.cuda.current_stream(dev).cuda_stream)
+                torch.cuda.synchronize(dev)
+                assert np.array_equal(d.cpu().numpy(), want), (hint, v)
+        finally:
+            os.environ.pop("RXG_TX_VARIANT", None)
 
 
 @pytest.mark.gpu
