@@ -1,0 +1,43 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer:
+the oracle's C restatement, the pcap ingest (rx_pcap.cpp) and the socket layer
+(host/nstack.c) are compiled with -fsanitize=address,undefined into
+tests/san/san_harness.c and run on edge-case frames, malformed pcap files and
+a UDP + TCP socket session.  CPU only; any sanitizer report fails the run."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "dpdk-tcp-udp_protocol_stack_amd")
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None or shutil.which("g++") is None,
+                    reason="needs gcc/g++")
+def test_host_code_under_asan_ubsan(tmp_path):
+    if not os.path.exists(os.path.join(PKG, "librxgpu.so")):
+        pytest.fail("librxgpu.so not built (run __graft_entry__.build())")
+    san = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+           "-g", "-O1"]
+    objs = []
+    for src, cc, std in [("oracle/ref_cpu.c", "gcc", "-std=gnu11"),
+                         ("dpdk-tcp-udp_protocol_stack_amd/host/nstack.c", "gcc", "-std=gnu11"),
+                         ("tests/san/san_harness.c", "gcc", "-std=gnu11"),
+                         ("dpdk-tcp-udp_protocol_stack_amd/csrc/rx_pcap.cpp", "g++", "-std=c++17")]:
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.run([cc, std, *san, "-Iinclude", "-c", os.path.join(ROOT, src), "-o", o],
+                       check=True, cwd=ROOT)
+        objs.append(o)
+    exe = str(tmp_path / "san_harness")
+    # nstack's control-plane calls (rxg_open with RXG_HOST_ONLY, flow sync, host
+    # lookups) come from the product library; the pcap entry points above
+    # interpose on its copies
+    subprocess.run(["g++", *san, *objs, "-o", exe, f"-L{PKG}", "-lrxgpu", f"-Wl,-rpath,{PKG}",
+                    "-lpthread"], check=True, cwd=ROOT)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               LSAN_OPTIONS="suppressions=" + os.path.join(ROOT, "tests", "san", "lsan.supp"))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "SAN OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
