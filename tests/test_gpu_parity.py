@@ -334,9 +334,10 @@ def test_nstack_tx_burst_checksums_on_gpu(torch_dev):
         ns.fini()
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4", "cfg5"])
 def test_full_size_properties(ctx, torch_dev, name):
-    """BASELINE sizes (16M x 64 B, 4M x 1500 B): verdicts of a random sample of
+    """BASELINE sizes (16M x 64 B, 4M x 1500 B, 16M IMIX, 1.25M x 9000 B with
+    1M tcbs): verdicts of a random sample of
     indices regenerate bit-exactly on the CPU (counter-based pktgen + oracle),
     per-flow counts add up to the delivered frames, and two lane-group widths
     give identical verdict arrays."""
@@ -363,7 +364,8 @@ def test_full_size_properties(ctx, torch_dev, name):
     rc = v[:, 11].view(torch.int8)
     assert int(cnt.sum().item()) == int((rc == 0).sum().item())
     rng = np.random.default_rng(11)
-    idx = np.sort(rng.choice(n, 1500, replace=False))
+    # (the oracle's list scans cost ~3 ms per lookup at cfg5's 1M tcbs)
+    idx = np.sort(rng.choice(n, 200 if name == "cfg5" else 1500, replace=False))
     vh = outs[0].cpu().numpy().view(R.VERDICT_DTYPE)
     tb = O.Tables(udp, tcb)
     for i in idx:
