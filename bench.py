@@ -155,23 +155,30 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
         tx_bytes = frame_bytes + 6 * n + 4 * n
         res["tx_cksum"] = dict(kernel_ms_avg=round(tms, 4), mpps=round(n / tms / 1e3, 1),
                                gb_per_s=round(tx_bytes / tms / 1e6, 1),
-                               frac=round(tx_bytes / tms / 1e6 / HBM_PEAK_GBS, 4))
+                               frac=round(tx_bytes / tms / 1e6 / HBM_PEAK_GBS, 4),
+                               traffic=pmc_traffic(name, "tx_cksum"))
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
 
 
-def pmc_traffic(name):
+def pmc_traffic(name, kernel=None):
     """HBM bytes per launch from the newest committed PMC summary for this
-    workload (profiles/pmc_*.json, written by tools/pmc_traffic.py), or None."""
+    workload (profiles/pmc_*.json, written by tools/pmc_traffic.py), or None.
+    kernel=None: K1 (rx_classify); "tx_cksum": K2."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if name in d.get("workloads", {}):
-            return d["workloads"][name].get("hbm_bytes_per_launch")
+        w = d.get("workloads", {}).get(name)
+        if w is not None:
+            if kernel is not None:
+                w = w.get(kernel)
+                if w is None:
+                    continue
+            return w.get("hbm_bytes_per_launch")
     return None
 
 

@@ -4,7 +4,7 @@
 Two separate counter passes (TCC has 4 slots: FETCH_SIZE needs 3, WRITE_SIZE
 2 — MI355X_MICROARCH.md §rocprofv3 PMC slots), each with nothing but the
 counter collection, over `bench.py --workload <w> --no-cpu`.  Per dispatch of
-rx_classify_kernel: hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
+rx_classify_kernel (and of K2 tx_cksum_kernel, the bench's TX leg): hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
 (gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced
 streaming read, MI355X_MICROARCH.md §HBM; WRITE_SIZE is exact for 16-B
 stores).  Writes profiles/pmc_<tag>.json, which bench.py reads for
@@ -31,12 +31,14 @@ def collect(workload, counter, outdir):
         sys.stderr.write(r.stdout[-3000:] + r.stderr[-3000:])
         raise SystemExit(r.returncode)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    vals = []
+    vals = {"rx_classify": [], "tx_cksum": []}
     for f in files:
         for row in csv.DictReader(open(f)):
-            if "rx_classify" in row.get("Kernel_Name", "") and \
-                    row.get("Counter_Name") == counter:
-                vals.append(float(row["Counter_Value"]))
+            if row.get("Counter_Name") != counter:
+                continue
+            for k in vals:
+                if k in row.get("Kernel_Name", ""):
+                    vals[k].append(float(row["Counter_Value"]))
     return vals, files
 
 
@@ -50,14 +52,18 @@ def main():
     for w in wls:
         fetch, ff = collect(w, "FETCH_SIZE", outdir)
         write, wf = collect(w, "WRITE_SIZE", outdir)
-        if not fetch or not write:
+        if not fetch["rx_classify"] or not write["rx_classify"]:
             raise SystemExit(f"no rx_classify_kernel rows for {w}: {ff} {wf}")
-        fetch.sort()
-        write.sort()
-        fk, wk = fetch[len(fetch) // 2], write[len(write) // 2]
-        res["workloads"][w] = {"fetch_size_kb": fk, "write_size_kb": wk,
-                               "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024),
-                               "dispatches": len(fetch)}
+
+        def summary(k):
+            fe, wr = sorted(fetch[k]), sorted(write[k])
+            fk, wk = fe[len(fe) // 2], wr[len(wr) // 2]
+            return {"fetch_size_kb": fk, "write_size_kb": wk,
+                    "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024),
+                    "dispatches": len(fe)}
+        res["workloads"][w] = summary("rx_classify")
+        if fetch["tx_cksum"] and write["tx_cksum"]:  # K2 over the same burst (bench's TX leg)
+            res["workloads"][w]["tx_cksum"] = summary("tx_cksum")
         print(w, res["workloads"][w], flush=True)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(outdir, f"pmc_{tag}.json"), "w") as fh:
