@@ -22,7 +22,9 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts);
 hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
-                           uint32_t unit_log2, uint32_t len_hint, hipStream_t s);
+                           uint32_t unit_log2, uint32_t len_hint, uint32_t variant,
+                           uint32_t bpc_cap, hipStream_t s);
+uint32_t tx_num_variants();
 
 static thread_local std::string g_last_hip;
 
@@ -116,6 +118,7 @@ struct rxg_ctx {
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
+    uint32_t tune_tx = RXG_TX_AUTO, tune_tx_bpc = 0; // rxg_tune_tx
     uint32_t *d_ws = nullptr; // launch workspace (binned lists, count slabs), grown on demand
     size_t d_ws_cap = 0;
     // context-owned per-flow counts (host-buffer path)
@@ -364,6 +367,14 @@ int rxg_tune_grid(rxg_ctx *c, uint32_t blocks_per_cu) {
     return RXG_OK;
 }
 
+int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
+    if (!c || blocks_per_cu > 32 || (variant != RXG_TX_AUTO && variant >= tx_num_variants()))
+        return RXG_EINVAL;
+    c->tune_tx = variant;
+    c->tune_tx_bpc = blocks_per_cu;
+    return RXG_OK;
+}
+
 uint32_t rxg_num_flows(const rxg_ctx *c) { return c ? c->ft.nu + c->ft.nt : 0; }
 
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *c, uint32_t dip, uint16_t dport) {
@@ -537,7 +548,8 @@ int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const u
     if (!d_pkts || !d_off || !d_len) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(tx_cksum_launch(d_pkts, d_off, d_len, n, off_unit_log2, len_hint, (hipStream_t)stream));
+    HIPCHK(tx_cksum_launch(d_pkts, d_off, d_len, n, off_unit_log2, len_hint, c->tune_tx,
+                           c->tune_tx_bpc, (hipStream_t)stream));
     return RXG_OK;
 }
 
@@ -559,7 +571,7 @@ int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t 
     HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_in, 0));
     if (sl.ticket) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
     HIPCHK(tx_cksum_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, (uint32_t)(span / n),
-                           c->stream));
+                           c->tune_tx, c->tune_tx_bpc, c->stream));
     HIPCHK(hipEventRecord(sl.ev_k, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
     HIPCHK(hipMemcpyAsync(pkts, sl.d_pkts, span, hipMemcpyDeviceToHost, c->s_d2h));

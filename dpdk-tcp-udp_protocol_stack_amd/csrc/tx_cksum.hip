@@ -21,8 +21,6 @@
 // TX_FULL_GRID, the round-1 shape, kept as a tuning alternative).
 #include <hip/hip_runtime.h>
 
-#include <stdlib.h>
-
 #include "rx_common.h"
 #include "rx_device.h"
 
@@ -183,8 +181,8 @@ struct tx_variant {
     tx_launch_fn fn;
     uint32_t bpc; // resident blocks per CU cap (0 = occupancy)
 };
-// 0..3: the defaults for <= 64, <= 128, <= 1536 and longer frames; the rest
-// are tuning alternatives (environment RXG_TX_VARIANT=i, RXG_TX_BPC=b).
+// 0..3: the defaults for <= 64, <= 128, <= 1536 and longer frames, 10 the one
+// for mixed sizes; the rest are tuning alternatives (rxg_tune_tx).
 // Measured (tools/tx_sweep.py, profiles/r01d/tx_sweep.txt): the write mode and
 // the schedule move these by only 2-4%.  Changing 4 bytes in a frame's first
 // 64 B dirties its first 128-B line, and the line goes back to HBM whole, so
@@ -202,17 +200,18 @@ static const tx_variant k_tx[] = {
 
 } // namespace
 
-// lanes per frame and passes in flight from the typical frame length
+uint32_t tx_num_variants() { return (uint32_t)(sizeof(k_tx) / sizeof(k_tx[0])); }
+
+// lanes per frame and passes in flight from the typical frame length, unless
+// `variant` (< tx_num_variants()) forces one; bpc_cap 0 = the variant's own
 hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
-                           uint32_t unit_log2, uint32_t len_hint, hipStream_t s) {
+                           uint32_t unit_log2, uint32_t len_hint, uint32_t variant,
+                           uint32_t bpc_cap, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (len_hint == 0) len_hint = 1518;
     // (mixed sizes, e.g. IMIX at 354 B average: G=4, one frame per group and
     // block per tile, 1.88 ms vs 2.30 for G=8 on cfg4, profiles/r01d + r01e)
     uint32_t v = len_hint <= 64 ? 0 : (len_hint <= 128 ? 1 : (len_hint <= 600 ? 10 : (len_hint <= 1536 ? 2 : 3)));
-    uint32_t bpc = k_tx[v].bpc;
-    const char *ev = getenv("RXG_TX_VARIANT"), *eb = getenv("RXG_TX_BPC"); // tuning only
-    if (ev && (uint32_t)atoi(ev) < sizeof(k_tx) / sizeof(k_tx[0])) v = (uint32_t)atoi(ev);
-    if (eb) bpc = (uint32_t)atoi(eb);
-    return k_tx[v].fn(pkts, off, len, n, unit_log2, bpc, s);
+    if (variant < tx_num_variants()) v = variant;
+    return k_tx[v].fn(pkts, off, len, n, unit_log2, bpc_cap ? bpc_cap : k_tx[v].bpc, s);
 }

@@ -116,6 +116,8 @@ _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
 _num_flows = _sig("rxg_num_flows", _u32, _vp)
 _tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
 _tune_grid = _sig("rxg_tune_grid", _i32, _vp, _u32)
+_tune_tx = _sig("rxg_tune_tx", _i32, _vp, _u32, _u32)
+TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
 _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
@@ -136,7 +138,7 @@ PIPE_DEPTH = 3
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum"]
@@ -220,6 +222,11 @@ class Context:
     def tune_grid(self, blocks_per_cu: int = 0):
         """cap resident blocks per CU (0 = occupancy)"""
         _check(_tune_grid(self._h, blocks_per_cu), "rxg_tune_grid")
+
+    def tune_tx(self, variant: int = TX_AUTO, blocks_per_cu: int = 0):
+        """force a TX checksum kernel variant (tx_cksum.hip k_tx index; TX_AUTO =
+        by len_hint) and cap its resident blocks per CU (0 = its default)"""
+        _check(_tune_tx(self._h, variant, blocks_per_cu), "rxg_tune_tx")
 
     @property
     def num_flows(self) -> int:

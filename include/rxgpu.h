@@ -213,6 +213,12 @@ int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t f
  * (0 = as many as the occupancy allows). */
 int rxg_tune_grid(rxg_ctx *ctx, uint32_t blocks_per_cu);
 
+/* Tuning hook for the TX checksum kernel: force entry `variant` of its
+ * variant table (csrc/tx_cksum.hip k_tx; RXG_TX_AUTO = chosen from len_hint)
+ * and cap its resident blocks per CU (0 = the variant's default). */
+#define RXG_TX_AUTO 0xFFFFFFFFu
+int rxg_tune_tx(rxg_ctx *ctx, uint32_t variant, uint32_t blocks_per_cu);
+
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);

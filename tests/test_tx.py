@@ -4,8 +4,6 @@ ng_encode_tcp_apppkt (tcp.c:444-463) do.  The oracle's fill is pinned against
 the pktgen's independently built checksums; the gfx950 kernel (K2) against
 the oracle, bit-exact on whole buffers, and at BASELINE sizes through the
 round trip "zero the fields -> K2 -> identical to the generated burst"."""
-import os
-
 import numpy as np
 import pytest
 
@@ -104,12 +102,15 @@ def test_gpu_tx_cksum_matches_oracle():
         got = ctx.tx_cksum(buf, off, lens, 4)                    # host path
         assert np.array_equal(got, want)
         # each default width (by len_hint), then every tuning variant of
-        # tx_cksum.hip's k_tx table (forced through RXG_TX_VARIANT)
-        runs = [(hint, None) for hint in (64, 128, 1500, 9000)] + [(1500, v) for v in range(13)]
+        # tx_cksum.hip's k_tx table (forced through rxg_tune_tx)
+        runs = [(hint, None) for hint in (64, 128, 354, 1500, 9000)] + \
+            [(1500, v) for v in range(13)]
+        with pytest.raises(R.RxgError):
+            ctx.tune_tx(13)  # past the table
         try:
             for hint, v in runs:
                 if v is not None:
-                    os.environ["RXG_TX_VARIANT"] = str(v)
+                    ctx.tune_tx(v)
                 d = torch.from_numpy(buf.copy()).to(dev)
                 ctx.tx_cksum_dev(d, torch.from_numpy(off.view(np.int32)).to(dev),
                                  torch.from_numpy(lens.view(np.int16)).to(dev), len(off), 4, hint,
@@ -117,7 +118,7 @@ def test_gpu_tx_cksum_matches_oracle():
                 torch.cuda.synchronize(dev)
                 assert np.array_equal(d.cpu().numpy(), want), (hint, v)
         finally:
-            os.environ.pop("RXG_TX_VARIANT", None)
+            ctx.tune_tx(R.TX_AUTO)
 
 
 @pytest.mark.gpu

@@ -1,4 +1,4 @@
-"""K2 (TX checksum) variant sweep: times every tx_cksum variant (RXG_TX_VARIANT)
+"""K2 (TX checksum) variant sweep: times every tx_cksum variant (rxg_tune_tx)
 on the bench workloads, interleaved over rounds in one process.  Tuning only.
     python tools/tx_sweep.py cfg2,cfg3,cfg5 [variants] [bpc list]"""
 import os
@@ -32,8 +32,7 @@ for nm in names:
     times = {(v, b): [] for v in variants for b in bpcs}
     for rnd in range(5):
         for v, b in times:
-            os.environ["RXG_TX_VARIANT"] = str(v)
-            os.environ["RXG_TX_BPC"] = str(b)
+            ctx.tune_tx(v, b)
             for _ in range(3):
                 ctx.tx_cksum_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], stream=sh)
             a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,5 +49,5 @@ for nm in names:
               flush=True)
     del pk, off, ln
     torch.cuda.empty_cache()
-os.environ.pop("RXG_TX_VARIANT")
+ctx.tune_tx(R.TX_AUTO)
 ctx.close()
