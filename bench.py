@@ -440,6 +440,8 @@ def main():
                     "gloo only to rehearse N > 1 on one GPU)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
+    ap.add_argument("--flow-load", type=int, default=0,
+                    help="flow tables at load <= 2**-N (rxg_tune_flow_load; 0 = default)")
     ap.add_argument("--sweep-counts", action="store_true", help="sweep with per-flow counts on")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
@@ -461,6 +463,8 @@ def main():
     torch.cuda.set_device(dev)
 
     ctx = R.Context(local)
+    if a.flow_load:
+        ctx.tune_flow_load(a.flow_load)
     global COUNTS, TX
     COUNTS = not a.no_counts
     TX = not a.no_tx

@@ -46,12 +46,15 @@ struct ft_host {
     std::vector<uint4> slots;
     uint32_t mask = 0, probe = 1;
 
-    // entries: x,y,z = key, w = value, in creation order (newest wins)
-    void build(const std::vector<uint4> &entries) {
+    // entries: x,y,z = key, w = value, in creation order (newest wins); load
+    // factor <= 2^-load_log2 (>= 1: always an empty slot)
+    void build(const std::vector<uint4> &entries, uint32_t load_log2) {
         const uint64_t n = entries.size();
         uint64_t ns = 16;
-        while (ns < 4 * n) ns <<= 1; // load factor <= 1/4: always an empty slot
-        slots.assign(ns, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
+        while (ns < (n << load_log2)) ns <<= 1;
+        // one slot past the end mirrors slot 0, so a two-slot probe window at
+        // any index reads in bounds (the stream kernel's first probe)
+        slots.assign(ns + 1, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
         mask = (uint32_t)(ns - 1);
         probe = 1;
         for (const uint4 &e : entries) {
@@ -69,6 +72,7 @@ struct ft_host {
                 break;
             }
         }
+        slots[ns] = slots[0];
     }
 
     uint32_t lookup(uint32_t a, uint32_t b, uint32_t c) const {
@@ -119,6 +123,7 @@ struct rxg_ctx {
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
     uint32_t tune_tx = RXG_TX_AUTO, tune_tx_bpc = 0; // rxg_tune_tx
+    uint32_t ft_load_log2 = RX_FT_LOAD_LOG2;           // rxg_tune_flow_load
     uint32_t *d_ws = nullptr; // launch workspace (binned lists, count slabs), grown on demand
     size_t d_ws_cap = 0;
     // context-owned per-flow counts (host-buffer path)
@@ -287,8 +292,8 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
     for (uint32_t i = 0; i < nt; ++i)
         te.push_back(make_uint4(t[i].sip, t[i].dip,
                                 (uint32_t)t[i].sport | ((uint32_t)t[i].dport << 16), i));
-    c->h_udp.build(ue);
-    c->h_tcp.build(te);
+    c->h_udp.build(ue, c->ft_load_log2);
+    c->h_tcp.build(te, c->ft_load_log2);
     build_udpc(c->h_udp, nu, &c->h_udpc, &c->udpc_probe);
     c->h_listen.assign(65536, RXG_FLOW_NONE);
     for (uint32_t i = 0; i < nt; ++i)
@@ -345,8 +350,9 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
-    if (lanes_per_frame == 0 && (pipeline == 20 || pipeline == 30 || pipeline == 31 || pipeline == 130)) {
-        c->tune_g = 0; // size-class binned path (20) / stream kernel (30, 31)
+    if (lanes_per_frame == 0 &&
+        (pipeline == 20 || (pipeline >= 30 && pipeline <= 39) || pipeline == 130)) {
+        c->tune_g = 0; // size-class binned path (20) / stream kernel (30..39, 130)
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;
         return RXG_OK;
@@ -372,6 +378,12 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
         return RXG_EINVAL;
     c->tune_tx = variant;
     c->tune_tx_bpc = blocks_per_cu;
+    return RXG_OK;
+}
+
+int rxg_tune_flow_load(rxg_ctx *c, uint32_t load_log2) {
+    if (!c || load_log2 > 4) return RXG_EINVAL;
+    c->ft_load_log2 = load_log2 ? load_log2 : RX_FT_LOAD_LOG2;
     return RXG_OK;
 }
 

@@ -1011,8 +1011,17 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // outstanding load (vmcnt(0)), which would serialise the tile prefetch.
 // ABL (diagnostic builds only, never selected automatically): 1 = no flow
 // table probe (flow id from the port: wrong verdicts by construction)
-template <bool NTS, int ABL = 0>
-__global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
+// HO (issue order of the first tile against the flow probe): 0 = probe, then
+// the first tile's loads; 1 = the first tile's loads, then the probe (its
+// dependent slot reads overlap the tile in flight); 2 = the probe and the
+// verdict fields after the whole tail stream (the slot read's latency hides
+// behind the stream; the key words stay live across it); 3 = 2 at a register
+// budget for 5 resident blocks per CU instead of 6 (2 spills one VGPR at 6).
+// PW (first probe window): 1 = one slot; 2 = the home slot and the next one in
+// the same trip (the table keeps a mirror of slot 0 past its end), so a key
+// displaced by one slot costs no dependent second read
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1>
+__global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
@@ -1085,12 +1094,14 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     const uint32_t ka = is_udp ? dip : sip;
     const uint32_t kb = is_udp ? dport : dip;
     const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-    const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
-    const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
     const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-    uint32_t pi = rx_hash3(ka, kb, kc) & mask;
     const bool probe0 = probe && maxp > 0 && !(ABL & 1);
-    const uint4 sl0 = ld_slot(probe0 ? tbl + pi : reinterpret_cast<const uint4 *>(fb));
+    const uint4 *sp0 = probe0 ? (is_udp ? ft.udp : ft.tcp) +
+                                    (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                              : reinterpret_cast<const uint4 *>(fb);
+    const uint4 sl0 = ld_slot(sp0);
+    uint4 sl1 = sl0;
+    if constexpr (PW == 2) sl1 = ld_slot(sp0 + (probe0 ? 1 : 0));
 
     uint4 h1 = c[1], h2 = c[2], h3 = c[3];
     h1.x = 0;
@@ -1128,47 +1139,66 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     };
     if (part) acc = lane_chunk_sum(acc, pc, ef, e);
 
-    // flow probe (UDP always, TCP speculatively: a bad checksum drops the hit)
-    uint32_t flow = RXG_FLOW_NONE;
-    if (probe0) {
-        uint4 sl = sl0;
-        for (uint32_t pr = 0;;) {
-            if (sl.w == RX_SLOT_EMPTY) break;
-            if (sl.x == ka && sl.y == kb && sl.z == kc) {
-                flow = sl.w;
-                break;
-            }
-            if (++pr >= maxp) break;
-            pi = (pi + 1) & mask;
-            sl = ld_slot(tbl + pi);
-        }
-    }
-    if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
-    if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
-
-    // every verdict field but the checksum outcome, before the tail phase (so
-    // the header words are dead across the stream loop)
-    uint32_t poff = 0, plen = 0, flags = 0;
-    int32_t rc = RXG_RC_KNI;
+    // every verdict field that does not depend on the flow: payload offset and
+    // length, flags (the truncation flag for both UDP outcomes: a delivered
+    // datagram extends the bytes the reference reads to 42 + payload)
+    uint32_t flags = 0, poff = 0, plen = 0;
     if (is_udp) {
-        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                   : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
         poff = 42;
         plen = dgl > 8u ? dgl - 8u : 0u;
         if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-        if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
     } else if (is_tcp) {
         const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
         poff = 34u + 4u * hl;
         if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
         plen = pl < 0 ? 0u : (uint32_t)pl;
     }
-    if ((int32_t)nd > cp) flags |= RXG_F_TRUNC;
+    const bool trunc = (int32_t)nd > cp;
+    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
     const uint32_t vy = (poff & 0xFFFFu) | (plen << 16);
 
-    // ---- tail phase -------------------------------------------------------
+    // flow probe (UDP always, TCP speculatively: a bad checksum drops the hit)
+    // and the return code
+    uint32_t flow = RXG_FLOW_NONE;
+    int32_t rc = RXG_RC_KNI;
+    auto probe_flow = [&]() {
+        if (probe0) {
+            // slot index and table recomputed from the keys (HO = 2 keeps only
+            // the keys and the first slot live across the stream)
+            const uint4 *tb = is_udp ? ft.udp : ft.tcp;
+            const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
+            const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
+            uint32_t pj = rx_hash3(ka, kb, kc) & mk;
+            uint4 sl = sl0;
+            for (uint32_t pr = 0;;) {
+                if (sl.w == RX_SLOT_EMPTY) break;
+                if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                    flow = sl.w;
+                    break;
+                }
+                if (++pr >= mp) break;
+                pj = (pj + 1) & mk;
+                if constexpr (PW == 2) {
+                    if (pr == 1) {
+                        sl = sl1;
+                        continue;
+                    }
+                }
+                sl = ld_slot(tb + pj);
+            }
+        }
+        if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+        if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = ft.listen[kc >> 16];
+        if (is_udp)
+            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                       : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+    };
     uint4 va[4], vb[4];
+    if constexpr (HO == 0) probe_flow();
+    // ---- tail phase -------------------------------------------------------
     tile_load(va, 0);
+    if constexpr (HO == 1) probe_flow();
     if (streamed) {
         const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
         const uint32_t ce = tail ? (uint32_t)(ce_abs - lo) : 0xFFFFFFFFu;
@@ -1232,6 +1262,7 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
         }
     }
 
+    if constexpr (HO >= 2) probe_flow();
     // ---- verdict ----------------------------------------------------------
     uint32_t ck = 0;
     if (do_sum) {
@@ -1262,14 +1293,14 @@ __global__ __launch_bounds__(256, 6) void rx_classify_stream_kernel(
     }
 }
 
-template <bool NTS, int ABL = 0>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -1443,6 +1474,13 @@ static const variant_entry k_variants[] = {
     // tail loads, 31 plain
     {0, 1, 1, 30, launch_stream<true>},    {0, 1, 1, 31, launch_stream<false>},
     {0, 1, 1, 130, launch_stream<true, 1>},
+    // 32/33/34: pipe 30 with the stream kernel's HO = 1/2/3 (first tile issued
+    // before the probe / the probe after the stream / same at 5 blocks per CU)
+    {0, 1, 1, 32, launch_stream<true, 0, 1>}, {0, 1, 1, 33, launch_stream<true, 0, 2>},
+    {0, 1, 1, 34, launch_stream<true, 0, 3>},
+    // 35/36/37: HO = 0/1/3 with the two-slot first probe (PW = 2)
+    {0, 1, 1, 35, launch_stream<true, 0, 0, 2>}, {0, 1, 1, 36, launch_stream<true, 0, 1, 2>},
+    {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
 };
 
 } // namespace
@@ -1455,8 +1493,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b)
         *g = 1, *p = 4, *fpg = 1, *pipe = 12;
-    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel
-        *g = 0, *p = 0, *fpg = 0, *pipe = 30;
+    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel, flow probe after the
+        // tail stream at 5 blocks/CU (HO = 3): 1-3% ahead of pipe 30 in every interleaved
+        // sweep (r01g: 1.184 vs 1.194, 1.177 vs 1.211, 1.305 vs 1.319 ms)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 34;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep)

@@ -37,6 +37,7 @@ struct rx_ft_dev {
     uint32_t udpc_mask, udpc_probe;
 };
 #define RX_UDPC_MAX_FLOWS 1024u // load <= 1/2: <= 2048 slots = 16 KiB of LDS
+#define RX_FT_LOAD_LOG2 2u      // exact-key tables: load <= 1/4 by default (rxg_tune_flow_load)
 
 RX_HD uint32_t rx_hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = 0x9E3779B9u ^ a;

@@ -59,7 +59,9 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (8, 2, 2, 26), (8, 2, 2, 28), (8, 2, 1, 28), (8, 1, 2, 28), (8, 2, 2, 2),
                    (16, 2, 2, 26), (16, 2, 2, 28),
                    (0, 0, 0, 20),  # size-class binned: lane kernel + G=8 kernel
-                   (0, 0, 0, 30), (0, 0, 0, 31)]  # stream kernel
+                   (0, 0, 0, 30), (0, 0, 0, 31),  # stream kernel
+                   (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
+                   (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37)]  # two-slot first probe
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -117,6 +119,7 @@ _num_flows = _sig("rxg_num_flows", _u32, _vp)
 _tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
 _tune_grid = _sig("rxg_tune_grid", _i32, _vp, _u32)
 _tune_tx = _sig("rxg_tune_tx", _i32, _vp, _u32, _u32)
+_tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
@@ -138,7 +141,7 @@ PIPE_DEPTH = 3
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum"]
@@ -227,6 +230,11 @@ class Context:
         """force a TX checksum kernel variant (tx_cksum.hip k_tx index; TX_AUTO =
         by len_hint) and cap its resident blocks per CU (0 = its default)"""
         _check(_tune_tx(self._h, variant, blocks_per_cu), "rxg_tune_tx")
+
+    def tune_flow_load(self, load_log2: int = 0):
+        """exact-key flow tables at load <= 2**-load_log2 from the next
+        flows_sync (0 = default); verdicts do not depend on it"""
+        _check(_tune_flow_load(self._h, load_log2), "rxg_tune_flow_load")
 
     @property
     def num_flows(self) -> int:

@@ -219,6 +219,12 @@ int rxg_tune_grid(rxg_ctx *ctx, uint32_t blocks_per_cu);
 #define RXG_TX_AUTO 0xFFFFFFFFu
 int rxg_tune_tx(rxg_ctx *ctx, uint32_t variant, uint32_t blocks_per_cu);
 
+/* Tuning hook for the exact-key flow tables: load factor <= 2^-load_log2
+ * (1 = 1/2, 2 = 1/4, up to 4; 0 = the default), applied by the next
+ * rxg_flows_sync.  Verdicts do not depend on it; the table's cache footprint
+ * and probe length do. */
+int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
+
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);

@@ -74,12 +74,16 @@ def _random_flows(rng, nu, nt, dup_frac=0.1):
     return udp, tcb
 
 
+@pytest.mark.parametrize("load_log2", [0, 1, 4])
 @pytest.mark.parametrize("nu,nt", [(0, 0), (1, 1), (1024, 4097), (5000, 300), (20000, 65536)])
-def test_flow_table_matches_list_scan(nu, nt):
+def test_flow_table_matches_list_scan(nu, nt, load_log2):
+    """the hash tables (at every load factor rxg_tune_flow_load allows to be
+    set) answer like the reference's first-match list scans"""
     rng = np.random.default_rng(nu * 7 + nt)
     udp, tcb = _random_flows(rng, nu, nt)
     ora = O.Tables(udp, tcb)
     with R.Context(R.HOST_ONLY) as c:
+        c.tune_flow_load(load_log2)
         c.flows_sync(udp, tcb)
         assert c.num_flows == nu + nt
         qs = 3000
@@ -97,6 +101,12 @@ def test_flow_table_matches_list_scan(nu, nt):
             assert c.lookup_udp(dip, dp) == ora.lookup_udp(dip, dp)
             a = (int(rng.integers(0, 600)), dip, int(rng.integers(0, 70)), int(rng.integers(0, 140)))
             assert c.lookup_tcp(*a) == ora.lookup_tcp(*a)
+
+
+def test_flow_load_rejects_out_of_range():
+    with R.Context(R.HOST_ONLY) as c:
+        with pytest.raises(R.RxgError):
+            c.tune_flow_load(5)
 
 
 CFGS = {
