@@ -159,6 +159,28 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
 
 
+@pytest.mark.parametrize("load_log2", [1, 4])
+@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (8, 2, 2, 0),
+                                     (1, 4, 1, 0), (4, 1, 2, 0)])
+def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2):
+    """verdicts and counts do not depend on the flow-table load factor
+    (rxg_tune_flow_load): longer probe chains at <= 1/2, sparse tables at <= 1/16"""
+    cfg = rxdist.gen_cfg("cfg4", n_udp=3000, n_tcp=3000)
+    pk, off, ln = R.gen_host(cfg, 11, 6000, 6)
+    udp, tcb = R.gen_flows(cfg)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    ctx.tune_flow_load(load_log2)
+    ctx.tune(*variant)
+    try:
+        ctx.flows_sync(udp, tcb)
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0, counts=True)
+    finally:
+        ctx.tune(0)
+        ctx.tune_flow_load(0)
+    assert got.tobytes() == want.tobytes(), (variant, load_log2, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt)
+
+
 @pytest.mark.parametrize("layout", ["packed", "block_shuffled", "scattered", "gapped"])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 20),
