@@ -1019,8 +1019,12 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // budget for 5 resident blocks per CU instead of 6 (2 spills one VGPR at 6).
 // PW (first probe window): 1 = one slot; 2 = the home slot and the next one in
 // the same trip (the table keeps a mirror of slot 0 past its end), so a key
-// displaced by one slot costs no dependent second read
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1>
+// displaced by one slot costs no dependent second read.  B1: one barrier per
+// tail tile instead of two (a tile's boundary prefixes are read after the next
+// tile's barrier, which already orders them after their writes; s_pre and
+// s_wt are double-buffered, so the next writes to a buffer come a barrier
+// after its last reads)
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1217,6 +1221,11 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
             }
             __syncthreads();
+            if constexpr (B1) { // the previous tile's boundaries (buffer buf ^ 1)
+                const uint32_t p0 = c0 - ST_TILE; // wraps for c0 = 0: no frame matches
+                if (c0 != 0 && cs - p0 < ST_TILE) es = s_pre[buf ^ 1u][cs - p0];
+                if (c0 != 0 && ce - p0 < ST_TILE) ee = s_pre[buf ^ 1u][ce - p0];
+            }
             uint32_t wt[16]; // block-uniform: kept in SGPRs
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1236,18 +1245,27 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
             }
             carry = base;
-            __syncthreads();
-            if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
-            if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+            if constexpr (!B1) {
+                __syncthreads();
+                if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
+                if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+            }
         };
         // unrolled twice: the A/B tiles swap roles without register moves (a
         // move would wait for the prefetch it copies); one exit per pair (a
         // trailing all-masked tile costs no bandwidth: its loads hit chunk 0)
-        for (uint32_t c0 = 0; c0 < span; c0 += 2 * ST_TILE) {
+        uint32_t c0 = 0;
+        for (; c0 < span; c0 += 2 * ST_TILE) {
             tile_load(vb, c0 + ST_TILE);
             tile(va, c0, 0);
             tile_load(va, c0 + 2 * ST_TILE);
             tile(vb, c0 + ST_TILE, 1);
+        }
+        if constexpr (B1) { // the last tile's boundaries (buffer 1)
+            __syncthreads();
+            const uint32_t p0 = c0 - ST_TILE;
+            if (cs - p0 < ST_TILE) es = s_pre[1][cs - p0];
+            if (ce - p0 < ST_TILE) ee = s_pre[1][ce - p0];
         }
         if (ce == span) ee = carry;
         if (tail) acc += ee - es;
@@ -1293,14 +1311,14 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     }
 }
 
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -1481,6 +1499,8 @@ static const variant_entry k_variants[] = {
     // 35/36/37: HO = 0/1/3 with the two-slot first probe (PW = 2)
     {0, 1, 1, 35, launch_stream<true, 0, 0, 2>}, {0, 1, 1, 36, launch_stream<true, 0, 1, 2>},
     {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
+    // 38/39: pipes 34/30 with one barrier per tail tile (B1)
+    {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>}, {0, 1, 1, 39, launch_stream<true, 0, 0, 1, true>},
 };
 
 } // namespace
@@ -1495,8 +1515,9 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         *g = 1, *p = 4, *fpg = 1, *pipe = 12;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel, flow probe after the
         // tail stream at 5 blocks/CU (HO = 3): 1-3% ahead of pipe 30 in every interleaved
-        // sweep (r01g: 1.184 vs 1.194, 1.177 vs 1.211, 1.305 vs 1.319 ms)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 34;
+        // sweep (r01g: 1.184 vs 1.194, 1.177 vs 1.211, 1.305 vs 1.319 ms); one barrier per
+        // tail tile (B1) takes another 0.7% (r01g: 1.177 vs 1.185 vs 1.194 ms for pipe 30)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 38;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep)
