@@ -409,3 +409,20 @@ def test_single_hip_runtime_loaded(ctx):
             libs.add(os.path.realpath(line.split()[-1]))
     assert len(libs) == 1, libs
     assert any("librxgpu.so" in line for line in open("/proc/self/maps"))
+
+
+def test_unknown_variant_fails_loudly(ctx, torch_dev):
+    """a tuned combination that is not compiled in fails the burst (RXG_EHIP),
+    never falls back to another kernel silently"""
+    cfg = rxdist.gen_cfg("cfg4", n_udp=64, n_tcp=64)
+    pk, off, ln = R.gen_host(cfg, 0, 256, 6)
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    ctx.tune(8, 3, 2, 0)
+    try:
+        with pytest.raises(R.RxgError):
+            _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0)
+    finally:
+        ctx.tune(0)
+    got = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0)
+    assert got.tobytes() == O.Tables(udp, tcb).classify(pk, off, ln, 6).tobytes()
