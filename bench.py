@@ -35,6 +35,7 @@ import rxgpu as R  # noqa: E402
 
 COUNTS = True
 TX = True
+RAMP_MS = 200.0
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 
 
@@ -93,6 +94,15 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
         drain(0)
         drain(1)
 
+    # clock ramp (untimed, before the W warmup steps): the burst kernel runs
+    # back to back for RAMP_MS of wall time without counts, so the timed steps
+    # see the GPU at its loaded clocks (W = 5 alone left cfg2 7% slow: 0.279
+    # vs 0.259 ms after 200 warmup steps, profiles/r01h/bench_warmup.txt)
+    t_ramp = time.perf_counter() + RAMP_MS / 1e3
+    while RAMP_MS > 0 and time.perf_counter() < t_ramp:
+        for _ in range(8):
+            ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None, stream=sh)
+        torch.cuda.synchronize(dev)
     for _ in range(warmup):
         step()
     drain_all()
@@ -440,6 +450,8 @@ def main():
                     "gloo only to rehearse N > 1 on one GPU)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
+    ap.add_argument("--ramp-ms", type=float, default=200.0,
+                    help="untimed clock ramp per workload before the warmup steps (ms of wall time)")
     ap.add_argument("--flow-load", type=int, default=0,
                     help="flow tables at load <= 2**-N (rxg_tune_flow_load; 0 = default)")
     ap.add_argument("--sweep-counts", action="store_true", help="sweep with per-flow counts on")
@@ -465,7 +477,8 @@ def main():
     ctx = R.Context(local)
     if a.flow_load:
         ctx.tune_flow_load(a.flow_load)
-    global COUNTS, TX
+    global COUNTS, TX, RAMP_MS
+    RAMP_MS = a.ramp_ms
     COUNTS = not a.no_counts
     TX = not a.no_tx
     if a.variant:
@@ -502,6 +515,7 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "ramp_ms": a.ramp_ms,
             "ms_per_step": round(head["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",

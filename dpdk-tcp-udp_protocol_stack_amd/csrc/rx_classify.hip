@@ -1450,7 +1450,10 @@ struct variant_entry {
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
     // defaults first (measured on MI355X, bench.py --sweep)
-    {1, 4, 1, 12, launch_lane_udpc<12, 0, true, false>, 6},
+    // pipe 12 at 4 blocks/CU: with per-flow counts its LDS (stage + UDP table +
+    // histogram) allows 4 anyway; without counts 5 fit and ran 36% slower
+    // (r01g: 0.255 vs 0.346 ms on cfg2, profiles/r01g/sweep_lane_bpc_counts.txt)
+    {1, 4, 1, 12, launch_lane_udpc<12, 0, true, false>, 4},
     {1, 4, 1, 5, launch_lane_udpc<0, 0, true, false>, 6},
     {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
     {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
