@@ -1340,23 +1340,33 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint4 *__rest
                                                               uint32_t per, uint32_t nu,
                                                               uint32_t words,
                                                               uint32_t *__restrict__ slab) {
+    // blockIdx.y = flow range: flows [y * 65536, y * 65536 + 2 * words)
     __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
     for (uint32_t i = threadIdx.x; i < words; i += 1024) bins[i] = 0;
     __syncthreads();
+    const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += 1024) {
-        // non-temporal: 16 B per frame read once; keeps the flow table cached
-        const uint4 v = ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i));
+    auto count = [&](const uint4 v) {
         const uint32_t rc = v.z >> 24, cls = (v.z >> 16) & 0xFFu;
         if (rc == 0u && v.x != RXG_FLOW_NONE && (cls == RXG_CLS_UDP || cls == RXG_CLS_TCP)) {
-            const uint32_t f = (cls == RXG_CLS_TCP ? nu : 0u) + v.x;
-            atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
+            const uint32_t f = (cls == RXG_CLS_TCP ? nu : 0u) + v.x - f0;
+            if (f < 2u * words) atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
         }
+    };
+    // four verdicts in flight per thread; non-temporal: read once per range
+    uint64_t i = b0 + threadIdx.x;
+    for (; i + 3 * 1024 < b1; i += 4 * 1024) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i + u * 1024));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) count(v[u]);
     }
+    for (; i < b1; i += 1024) count(ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i)));
     __syncthreads();
-    uint32_t *dst = slab + (uint64_t)blockIdx.x * words;
-    for (uint32_t i = threadIdx.x; i < words; i += 1024) dst[i] = bins[i];
+    uint32_t *dst = slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words;
+    for (uint32_t k = threadIdx.x; k < words; k += 1024) dst[k] = bins[k];
 }
 
 // block = 64 bin pairs (one per lane) x 16 waves, each wave summing every
@@ -1367,6 +1377,10 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
                                                                 unsigned long long *__restrict__ counts) {
     __shared__ uint32_t part[2][16][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // blockIdx.y = flow range (its slabs, its 65536 counts)
+    slab += (uint64_t)blockIdx.y * nslabs * words;
+    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
+    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
     const uint32_t w = blockIdx.x * 64 + lane;
     const uint32_t wc = w < words ? w : 0;
     uint32_t lo = 0, hi = 0;
@@ -1401,9 +1415,31 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
     }
 }
 
-// slab geometry: a multiple of 256 blocks (whole waves of one block per CU),
+// Flows above 65536: the count is split into ranges of 65536 flows
+// (blockIdx.y), each range's blocks scanning every verdict; up to
+// SLAB_MAX_RANGES ranges, beyond that global atomics in the classify kernel.
+constexpr uint32_t SLAB_MAX_RANGES = 32;
+
+static uint32_t slab_ranges(const rx_ft_dev &ft) {
+    return (ft.nu + ft.nt + SLAB_MAX_FLOWS - 1) / SLAB_MAX_FLOWS;
+}
+
+// 16-bit bin pairs per slab: all flows for one range, a whole range otherwise
+static uint32_t slab_words(const rx_ft_dev &ft) {
+    return slab_ranges(ft) > 1 ? SLAB_MAX_FLOWS / 2 : (ft.nu + ft.nt + 1) / 2;
+}
+
+// slab geometry: one range, a multiple of 256 blocks (whole waves of one block
+// per CU); several ranges, as few slabs per range as the 16-bit bins allow;
 // <= 65535 verdicts each
-static void slab_geometry(uint32_t n, uint32_t *nslabs, uint32_t *per) {
+static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
+    if (nranges > 1) {
+        const uint64_t nb = ((uint64_t)n + 65534) / 65535;
+        *nslabs = (uint32_t)(nb ? nb : 1);
+        *per = (uint32_t)(((uint64_t)n + *nslabs - 1) / *nslabs);
+        if (*per == 0) *per = 1;
+        return;
+    }
     const uint64_t waves = ((uint64_t)n + 256ull * 65535 - 1) / (256ull * 65535);
     uint64_t nb = 256 * (waves ? waves : 1);
     uint64_t pr = ((uint64_t)n + nb - 1) / nb;
@@ -1415,19 +1451,19 @@ static void slab_geometry(uint32_t n, uint32_t *nslabs, uint32_t *per) {
 
 static bool use_slab(const rx_ft_dev &ft, bool counts) {
     const uint32_t nf = ft.nu + ft.nt;
-    return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS;
+    return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS * SLAB_MAX_RANGES;
 }
 
 static hipError_t launch_count_slab(const uint4 *out, uint32_t n, const rx_ft_dev &ft,
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
+    const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
-    slab_geometry(n, &nslabs, &per);
-    const uint32_t nf = ft.nu + ft.nt, words = (nf + 1) / 2;
-    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs), dim3(1024), 0, s, out, n, per, ft.nu,
+    slab_geometry(n, nr, &nslabs, &per);
+    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs, nr), dim3(1024), 0, s, out, n, per, ft.nu,
                        words, slab);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words + 63) / 64), dim3(1024), 0, s, slab,
+    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words + 63) / 64, nr), dim3(1024), 0, s, slab,
                        nslabs, words, nf, counts);
     return hipGetLastError();
 }
@@ -1537,8 +1573,8 @@ size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_d
     size_t b = (g == 0 && pipe == 20) ? 16 + 8ull * n : 0;
     if (use_slab(ft, counts)) {
         uint32_t nslabs, per;
-        slab_geometry(n, &nslabs, &per);
-        b = ((b + 255) & ~(size_t)255) + (size_t)nslabs * ((ft.nu + ft.nt + 1) / 2) * 4;
+        slab_geometry(n, slab_ranges(ft), &nslabs, &per);
+        b = ((b + 255) & ~(size_t)255) + (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
     }
     return b;
 }
