@@ -1559,8 +1559,9 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         *g = 0, *p = 0, *fpg = 0, *pipe = 38;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
-    } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 30;
+    } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), the
+        // IMIX shape: pipe 38 vs 30 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms (r01g, r01j)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 38;
     }
 }
 
