@@ -6,8 +6,17 @@ A "step" = one pass of the hot path (rxg_classify_dev: the fused gfx950
 kernel) over one burst of synthetic frames already resident in HBM, plus at
 N > 1 the per-flow count all-reduce (the path's only exchange).
 Default workload = BASELINE configs[1] (64 B UDP, 1024 flows, 16M frames per
-GPU); configs[2] (1500 B TCP, 4096 flows, 4M frames per GPU, the HBM-roofline
-run) is measured in the same run and reported under "cfg3".
+GPU); configs[2..4] are measured in the same run and reported under
+"cfg3".."cfg5", BASELINE configs[0] (100K x 64 B UDP from a pcap, 1 flow)
+under "cfg1".
+
+N > 1 (one rank per GPU, weak scaling): every rank generates the GLOBAL burst
+of N x n frames, RSS-splits it on its GPU (rxg_rss_split_dev) and gathers its
+own shard (rxg_gather_dev) before the timed steps; a step classifies the shard
+and all-reduces the per-flow counts over RCCL (rxg_counts_allreduce); value =
+N x n frames / the max-over-ranks step time.  Every workload line carries a
+"parity" field: a seeded sample of the run's verdicts checked bit for bit
+against the oracle (the exit code is 3 if any differs).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2,cfg3]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -19,7 +28,6 @@ import glob
 import json
 import os
 import platform
-import subprocess
 import sys
 import time
 
@@ -44,55 +52,66 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------
-def run_workload(name, ctx, rank, world, steps, warmup, dev):
+def collective_fn(group, nccl_group, nflows):
+    """the path's one exchange, on stream `cs`: rxgpu.Group (RCCL through the
+    C ABI) or, if that could not be opened, torch.distributed's RCCL"""
+    def run(t, cs):
+        if group is not None:
+            group.allreduce(t, nflows, stream=cs.cuda_stream)
+        else:
+            with torch.cuda.stream(cs):
+                torch.distributed.all_reduce(t, group=nccl_group)
+    return run
+
+
+def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_sample=4096,
+                 oracle_threads=1):
     w = rxdist.WORKLOADS[name]
-    cfg = rxdist.gen_cfg(name, rank, world)
-    n = w["n"]
+    cfg = rxdist.gen_cfg(name)
+    ul = w["unit_log2"]
     udp, tcb = R.gen_flows(cfg)
     ctx.flows_sync(udp, tcb)
     nflows = len(udp) + len(tcb)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
-    off = torch.empty(n, dtype=torch.int32, device=dev)
-    ln = torch.empty(n, dtype=torch.int16, device=dev)
-    out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    t_setup = time.perf_counter()
+    pk, off, ln, n, gidx = rxdist.build_shard(ctx, name, rank, world, dev, stream)
+    t_setup = time.perf_counter() - t_setup
+    out = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=dev)
     counts = torch.zeros(max(nflows, 1), dtype=torch.int64, device=dev)
-    # N > 1: per-step counts double-buffered; step k's all-reduce runs on the
-    # collective stream while step k+1's kernel runs (drained at step k+2)
-    step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)]
-    pending = [None, None]
-    R.gen_dev(cfg, 0, n, pk, off, ln, w["unit_log2"], stream=sh)
-    torch.cuda.synchronize(dev)
-    frame_bytes = int(ln.to(torch.int64).bitwise_and(0xFFFF).sum().item())
+    frame_bytes = int(ln[:n].to(torch.int64).bitwise_and(0xFFFF).sum().item())
     alg_bytes = frame_bytes + 22 * n  # frame + off(4) + len(2) read + verdict(16) written
+    # N > 1: step k's counts go to step_counts[k & 1]; the all-reduce runs on
+    # the collective stream cs while step k+1's kernel runs, then adds into counts
+    cs = torch.cuda.Stream(dev) if world > 1 else None
+    step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)] if world > 1 else None
+    k_ev = [torch.cuda.Event(), torch.cuda.Event()]
+    done_ev = [torch.cuda.Event(), torch.cuda.Event()]
+    pend = [False, False]
     kstep = [0]
-
-    def drain(b):
-        if pending[b] is not None:
-            pending[b].wait()
-            counts.add_(step_counts[b])
-            pending[b] = None
 
     def step(ev=None):
         b = kstep[0] & 1
         kstep[0] += 1
         if world > 1:
-            drain(b)
+            if pend[b]:
+                stream.wait_event(done_ev[b])  # its previous all-reduce + add are done
             step_counts[b].zero_()
         tgt = counts if world == 1 else step_counts[b]
         if ev is not None:
             ev[0].record(stream)
-        ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out,
-                         tgt if COUNTS else None, stream=sh)
+        ctx.classify_dev(pk, off, ln, n, ul, w["len_hint"], out, tgt if COUNTS else None,
+                         stream=sh)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            pending[b] = rxdist.allreduce_counts(step_counts[b], world, async_op=True)
-
-    def drain_all():
-        drain(0)
-        drain(1)
+            k_ev[b].record(stream)
+            cs.wait_event(k_ev[b])
+            coll(step_counts[b], cs)
+            with torch.cuda.stream(cs):
+                counts.add_(step_counts[b])
+            done_ev[b].record(cs)
+            pend[b] = True
 
     # clock ramp (untimed, before the W warmup steps): the burst kernel runs
     # back to back for RAMP_MS of wall time without counts, so the timed steps
@@ -101,11 +120,10 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     t_ramp = time.perf_counter() + RAMP_MS / 1e3
     while RAMP_MS > 0 and time.perf_counter() < t_ramp:
         for _ in range(8):
-            ctx.classify_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], out, None, stream=sh)
+            ctx.classify_dev(pk, off, ln, n, ul, w["len_hint"], out, None, stream=sh)
         torch.cuda.synchronize(dev)
     for _ in range(warmup):
         step()
-    drain_all()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     if world > 1:
@@ -114,51 +132,69 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     t0 = time.perf_counter()
     for k in range(steps):
         step(evs[k])
-    drain_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
     kms = [a.elapsed_time(b) for a, b in evs]
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:  # max over ranks (gloo: control plane on the host)
+        t = torch.tensor([el], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
-    # self-consistency of the burst (parity proper lives in tests/): every
-    # delivered verdict was counted exactly once per step on this rank
-    v = out.view(n, 16)
-    rc = v[:, 11].view(torch.int8)
-    n_ok = int((rc == 0).sum().item())
+    # counts: every delivered verdict counted once per step, on every rank
+    # after the all-reduce (the global histogram)
+    v = out[:n * 16].view(n, 16)
+    n_ok = int((v[:, 11].view(torch.int8) == 0).sum().item())
     total_steps = warmup + steps
     counted = int(counts.sum().item())
     n_ok_all = n_ok
-    if world > 1:  # every rank holds the all-reduced histogram of all ranks' frames
-        t = torch.tensor([n_ok], dtype=torch.int64, device=dev)
+    if world > 1:
+        t = torch.tensor([n_ok], dtype=torch.int64)
         torch.distributed.all_reduce(t)
         n_ok_all = int(t.item())
     expect = n_ok_all * total_steps if COUNTS else None
     kavg = float(np.mean(kms))
+    n_all, alg_all = n, alg_bytes
+    if world > 1:  # the whole job: frames and algorithmic bytes of every rank
+        t = torch.tensor([n, alg_bytes], dtype=torch.int64)
+        torch.distributed.all_reduce(t)
+        n_all, alg_all = int(t[0].item()), int(t[1].item())
     res = dict(
-        workload=name, desc=w["desc"], n_per_gpu=n, nflows=nflows,
-        mpps=n * world * steps / el / 1e6,
-        gbps=alg_bytes * world * steps / el / 1e9,
-        ms_per_step=el / steps * 1e3,
+        workload=name, desc=w["desc"], frames_per_step=n_all, frames_this_rank=n,
+        nflows=nflows, mpps=n_all * steps / el / 1e6,
+        gbps=alg_all * steps / el / 1e9, ms_per_step=el / steps * 1e3,
         kernel_ms_avg=kavg, kernel_ms_min=float(np.min(kms)),
         alg_bytes_per_launch=alg_bytes, frame_bytes=frame_bytes,
-        rc0_frac=n_ok / n, counts_ok=(expect is None or counted == expect),
+        rc0_frac=n_ok / max(n, 1), counts_ok=(expect is None or counted == expect),
+        setup_s=round(t_setup, 2),
     )
-    achieved = alg_bytes / (kavg * 1e-3) / 1e9
+    achieved = alg_bytes / (kavg * 1e-3) / 1e9  # this rank's kernel (HIP events)
     res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                            unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                           traffic=pmc_traffic(name))
-    if TX:  # K2 (TX checksum fill) over the same burst, in place: same bytes read + 4 B written
+                           traffic=pmc_traffic(name) if world == 1 else None)
+    # parity of this run: a seeded sample of the verdicts regenerated on the CPU
+    t_par = time.perf_counter()
+    checked, bad, first_bad = parity_check(name, cfg, udp, tcb, out, n, gidx, ul,
+                                           parity_sample, seed=1000 + rank,
+                                           threads=oracle_threads)
+    if world > 1:
+        t = torch.tensor([checked, bad], dtype=torch.int64)
+        torch.distributed.all_reduce(t)
+        checked, bad = int(t[0].item()), int(t[1].item())
+    res["parity"] = dict(checked=checked, mismatches=bad,
+                         sample="seeded uniform sample of this run's verdicts (every rank), "
+                                "frames regenerated on the CPU and classified by "
+                                "oracle/ref_cpu.c", seconds=round(time.perf_counter() - t_par, 2))
+    if first_bad:
+        log(f"PARITY FAILURE {name}: {first_bad}")
+    if TX and world == 1:  # K2 (TX checksum fill) over the same burst, in place
         tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(steps)]
         for _ in range(warmup):
-            ctx.tx_cksum_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], stream=sh)
+            ctx.tx_cksum_dev(pk, off, ln, n, ul, w["len_hint"], stream=sh)
         for a, b in tev:
             a.record(stream)
-            ctx.tx_cksum_dev(pk, off, ln, n, w["unit_log2"], w["len_hint"], stream=sh)
+            ctx.tx_cksum_dev(pk, off, ln, n, ul, w["len_hint"], stream=sh)
             b.record(stream)
         torch.cuda.synchronize(dev)
         tms = float(np.mean([a.elapsed_time(b) for a, b in tev]))
@@ -172,15 +208,29 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev):
     return res
 
 
+def lib_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    with open(R.LIB_PATH, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
 def pmc_traffic(name, kernel=None):
     """HBM bytes per launch from the newest committed PMC summary for this
-    workload (profiles/pmc_*.json, written by tools/pmc_traffic.py), or None.
+    workload (profiles/pmc_*.json, written by tools/pmc_traffic.py) — only if
+    that summary was measured on THIS librxgpu.so (same SHA-256), else None:
+    a kernel edit without a fresh PMC pass publishes no stale traffic.
     kernel=None: K1 (rx_classify); "tx_cksum": K2."""
+    sha = lib_sha256()
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
+            continue
+        if d.get("librxgpu_sha256") != sha:
             continue
         w = d.get("workloads", {}).get(name)
         if w is not None:
@@ -193,88 +243,260 @@ def pmc_traffic(name, kernel=None):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline(name, budget_s):
-    """The oracle (C restatement of the reference path, linked-list lookups,
-    -O2, one core — the reference runs one pkt_process lcore) on a bounded
-    sample of the same workload, cycled until ~budget_s of CPU work."""
+# Oracle legs (test infrastructure: the checker, and the CPU baseline)
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_bind as O  # cpu_baseline leg only
-    w = rxdist.WORKLOADS[name]
-    cfg = rxdist.gen_cfg(name)
-    sample = {"cfg2": 1 << 20, "cfg3": 1 << 16, "cfg4": 1 << 16, "cfg5": 1 << 12}[name]
-    pk, off, ln = R.gen_host(cfg, 0, sample, w["unit_log2"])
-    udp, tcb = R.gen_flows(cfg)
-    tb = O.Tables(udp, tcb)
-    # calibrate on a slice, then size the run to the budget (256 frames: the
-    # list scans cost ~3 ms per lookup at cfg5's 1M tcbs)
-    t0 = time.perf_counter()
-    k = min(sample, 256)
-    tb.classify(pk, off[:k], ln[:k], w["unit_log2"])
-    per = (time.perf_counter() - t0) / k
-    total = max(k, int(budget_s / max(per, 1e-9)))
-    done, t0 = 0, time.perf_counter()
-    while done < total:
-        m = min(sample, total - done)
-        tb.classify(pk, off[:m], ln[:m], w["unit_log2"])
-        done += m
-    el = time.perf_counter() - t0
-    cpu = platform.processor() or platform.machine()
+    import oracle_bind as O  # parity + cpu_baseline legs only
+    return O
+
+
+_TABLES = {}
+
+
+def oracle_tables(name, udp, tcb, opt="O2"):
+    """the reference's head-inserted lists, built once per workload and build"""
+    O = _oracle()
+    key = (name, opt)
+    if key not in _TABLES:
+        _TABLES[key] = O.Tables(udp, tcb, which=O.lib if opt == "O2" else O.lib_O0())
+    return _TABLES[key]
+
+
+def regen(cfg, gidx, ul):
+    """frames gidx[k] of a workload's burst, regenerated on the CPU (the
+    pktgen is a pure function of (cfg, i)), one slot_bytes slot each"""
+    slot = cfg.slot_bytes
+    buf = np.zeros(len(gidx) * slot + 64, np.uint8)
+    lens = np.zeros(len(gidx), np.uint16)
+    for j, i in enumerate(gidx):
+        p, _, l = R.gen_host(cfg, int(i), 1, ul)
+        buf[j * slot:j * slot + slot] = p[:slot]
+        lens[j] = l[0]
+    offs = (np.arange(len(gidx), dtype=np.uint64) * slot >> ul).astype(np.uint32)
+    return buf, offs, lens
+
+
+def _threaded(fn, parts, threads):
+    """run fn(part) over parts on `threads` host threads (ctypes drops the GIL)"""
+    import concurrent.futures as cf
+    if threads <= 1 or len(parts) <= 1:
+        return [fn(p) for p in parts]
+    with cf.ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(fn, parts))
+
+
+def parity_check(name, cfg, udp, tcb, out, n, gidx, ul, sample, seed, threads=1):
+    """bit-exact check of a seeded sample of this run's verdicts against the
+    oracle on the same frames; returns (checked, mismatches, first mismatch)"""
+    if sample <= 0 or n == 0:
+        return 0, 0, None
+    rng = np.random.default_rng(seed)
+    loc = np.arange(n) if sample >= n else np.sort(rng.choice(n, sample, replace=False))
+    sel = torch.from_numpy(loc.astype(np.int64)).to(out.device)
+    got = out[:n * 16].view(n, 16).index_select(0, sel).cpu().numpy().reshape(-1)
+    got = got.view(R.VERDICT_DTYPE)
+    g = loc if gidx is None else gidx[loc]
+    buf, offs, lens = regen(cfg, g, ul)
+    tb = oracle_tables(name, udp, tcb)
+    parts = np.array_split(np.arange(len(g)), max(1, min(threads, len(g) // 64 or 1)))
+    want = np.concatenate(_threaded(lambda ix: tb.classify(buf, offs[ix], lens[ix], ul), parts,
+                                    threads))
+    bad = np.nonzero(np.any(got.view(np.uint8).reshape(-1, 16) !=
+                            want.view(np.uint8).reshape(-1, 16), axis=1))[0]
+    first = None
+    if len(bad):
+        k = int(bad[0])
+        first = dict(frame=int(g[k]), got=str(got[k]), want=str(want[k]))
+    return len(g), int(len(bad)), first
+
+
+def host_cores():
+    """the host CPU as the bench sees it: nproc, the affinity mask, the cgroup
+    quota, the thread budget (OMP_NUM_THREADS: the GPU box's CPU share per
+    GPU) and the model"""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit():
+        use = max(1, min(use, int(share)))
+    model = platform.processor() or platform.machine()
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
+                model = line.split(":", 1)[1].strip()
                 break
     except OSError:
         pass
-    return dict(value=round(done / el / 1e6, 4), unit="Mpps", cores=1, kind="port",
-                sample=f"{done} frames ({sample} distinct, cycled) of {name}: {w['desc']}; "
-                       f"oracle/ref_cpu.c -O2, list-scan lookups, 1 thread; host {cpu}, "
-                       f"nproc {os.cpu_count()}",
-                seconds=round(el, 2))
+    return dict(nproc=nproc, affinity=aff, cgroup_quota=quota, threads=use, model=model)
 
 
-def cpu_baseline_mt(name, budget_s, threads):
-    """the same oracle on `threads` host cores, the
-    sample split into one contiguous shard per thread (every verdict depends
-    only on its own frame, so any split is an RSS-style shard).  ctypes drops
-    the GIL inside the C call, so the threads run in parallel."""
-    import threading
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_bind as O  # cpu_baseline leg only
+CPU_SAMPLE = {"cfg1": 100000, "cfg2": 1 << 20, "cfg3": 1 << 16, "cfg4": 1 << 16,
+              "cfg5": 1 << 14}
+
+
+def cpu_rate(tb, pk, off, ln, ul, budget_s, threads=1):
+    """frames/s of the oracle over the sample, cycled until ~budget_s of
+    work per thread; threads > 1: the sample RSS-split over the threads (the
+    same 5-tuple sharding as the GPUs, rxg_rss_split), one shard per thread"""
+    k = min(len(off), 256)  # calibrate (the list scans cost ~3 ms per lookup at 1M tcbs)
+    t0 = time.perf_counter()
+    tb.classify(pk, off[:k], ln[:k], ul)
+    per = (time.perf_counter() - t0) / k
+    target = max(k, int(budget_s / max(per, 1e-9)))
+    if threads <= 1:
+        shards = [np.arange(len(off))]
+    else:
+        first, perm = R.rss_split(pk, off, ln, ul, threads)
+        shards = [perm[first[s]:first[s + 1]] for s in range(threads)]
+        shards = [s for s in shards if len(s)]
+
+    def work(ix):
+        o, l = np.ascontiguousarray(off[ix]), np.ascontiguousarray(ln[ix])
+        done = 0
+        while done < target:
+            m = min(len(ix), target - done)
+            tb.classify(pk, o[:m], l[:m], ul)
+            done += m
+        return done
+    t0 = time.perf_counter()
+    done = _threaded(work, shards, threads)
+    el = time.perf_counter() - t0
+    return sum(done) / el, sum(done), el
+
+
+def cpu_baseline(name, budget_s, cores):
+    """SURVEY.md §8(d) / BASELINE.md §3: the oracle (the reference algorithm:
+    list-scan lookups, per-word checksum; printf disabled) at -O2 and at -O0
+    (the reference's own build flags), on 1 core (the reference's single
+    pkt_process lcore, netfamily.c:427) and on every usable host core with
+    the sample RSS-sharded; a bounded, cycled sample of the same workload."""
     w = rxdist.WORKLOADS[name]
     cfg = rxdist.gen_cfg(name)
-    sample = {"cfg2": 1 << 20, "cfg3": 1 << 16, "cfg4": 1 << 16, "cfg5": 1 << 12}[name]
-    pk, off, ln = R.gen_host(cfg, 0, sample, w["unit_log2"])
+    ul = w["unit_log2"]
+    sample = min(CPU_SAMPLE[name], w["n"])
+    pk, off, ln = R.gen_host(cfg, 0, sample, ul)
     udp, tcb = R.gen_flows(cfg)
-    tb = O.Tables(udp, tcb)
-    k = min(sample, 256)
-    t0 = time.perf_counter()
-    tb.classify(pk, off[:k], ln[:k], w["unit_log2"])
-    per = (time.perf_counter() - t0) / k  # one core
-    per_thread = max(k, int(budget_s / max(per, 1e-9)))
-    bounds = np.linspace(0, sample, threads + 1).astype(np.int64)
-    done = [0] * threads
+    res = {}
+    for opt in ("O2", "O0"):
+        tb = oracle_tables(name, udp, tcb, opt)
+        r1, d1, e1 = cpu_rate(tb, pk, off, ln, ul, budget_s)
+        rn, dn, en = cpu_rate(tb, pk, off, ln, ul, budget_s / 2, cores["threads"])
+        res[opt] = dict(one_core=dict(mpps=round(r1 / 1e6, 4), frames=d1, seconds=round(e1, 2)),
+                        all_cores=dict(mpps=round(rn / 1e6, 4), frames=dn, seconds=round(en, 2),
+                                       threads=cores["threads"]))
+    sampled = "sampled: " if name in ("cfg4", "cfg5") else ""
+    return dict(
+        value=res["O2"]["one_core"]["mpps"], unit="Mpps", cores=1, kind="port",
+        sample=f"{sampled}{sample} distinct frames of {name} ({w['desc']}), cycled to the time "
+               f"budget; oracle/ref_cpu.c (list-scan lookups, printf off); value = -O2 on 1 "
+               f"core; all_cores = {cores['threads']} threads over an RSS split of the sample "
+               f"(host: {cores['model']}, nproc {cores['nproc']}, affinity {cores['affinity']}, "
+               f"cgroup quota {cores['cgroup_quota']}, threads capped at the box's CPU share)",
+        O2=res["O2"], O0=res["O0"], host=cores)
 
-    def work(i):
-        lo, hi = int(bounds[i]), int(bounds[i + 1])
-        o, l = off[lo:hi], ln[lo:hi]
-        n = 0
-        while n < per_thread:
-            tb.classify(pk, o, l, w["unit_log2"])
-            n += hi - lo
-        done[i] = n
 
-    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+def run_cfg1(local, dev, steps, warmup, budget_s, cores):
+    """BASELINE configs[0]: 100K x 64 B UDP from a pcap, one flow.  The frames
+    go through a pcap file (rxg_pcap_write / rxg_pcap_read_burst), then through
+    the host-buffer path (rxg_classify_span: PCIe both ways) with every verdict
+    checked against the oracle, then device-resident (rxg_classify_dev); the
+    oracle times the same pcap burst at -O2 and -O0 on 1 core."""
+    import tempfile
+    w = rxdist.WORKLOADS["cfg1"]
+    cfg = rxdist.gen_cfg("cfg1")
+    n, ul = w["n"], w["unit_log2"]
+    hp, ho, hl = R.gen_host(cfg, 0, n, ul)
+    path = os.path.join(tempfile.gettempdir(), f"rxg_cfg1_{os.getpid()}.pcap")
+    R.pcap_write(path, hp, ho, hl, ul)
+    pc = R.Pcap(path)
+    buf = torch.zeros(n * 64 + 64, dtype=torch.uint8).pin_memory()
+    poff = torch.zeros(n, dtype=torch.int32).pin_memory()
+    pln = torch.zeros(n, dtype=torch.int16).pin_memory()
+    got_n, span = pc.read_burst_into(buf.numpy(), poff.numpy().view(np.uint32),
+                                     pln.numpy().view(np.uint16), ul)
+    pc.close()
+    os.unlink(path)
+    assert got_n == n, (got_n, n)
+    udp, tcb = R.gen_flows(cfg)
+    out = torch.zeros(n * 16, dtype=torch.uint8).pin_memory()
+    ctx = R.Context(local, max_pkts=n, max_bytes=span + 64)
+    ctx.flows_sync(udp, tcb)
+    args = (buf.data_ptr(), span, poff.data_ptr(), pln.data_ptr(), n, ul, out.data_ptr())
+    ctx.classify_span(*args)
+    got = out.numpy().view(R.VERDICT_DTYPE).copy()
+    bufn, offn, lnn = buf.numpy(), poff.numpy().view(np.uint32), pln.numpy().view(np.uint16)
+    want = oracle_tables("cfg1", udp, tcb).classify(bufn, offn, lnn, ul)
+    bad = int(np.any(got.view(np.uint8).reshape(-1, 16) != want.view(np.uint8).reshape(-1, 16),
+                     axis=1).sum())
+    for _ in range(3):
+        ctx.classify_span(*args)
     t0 = time.perf_counter()
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    el = time.perf_counter() - t0
-    return dict(value=round(sum(done) / el / 1e6, 4), unit="Mpps", cores=threads, kind="port",
-                sample=f"{sum(done)} frames of {name} ({sample} distinct, {threads} contiguous "
-                       f"shards cycled); oracle/ref_cpu.c -O2, list-scan lookups, "
-                       f"{threads} threads", seconds=round(el, 2))
+    for _ in range(steps):
+        ctx.classify_span(*args)
+    e2e_ms = (time.perf_counter() - t0) / steps * 1e3
+    # device-resident: the same burst in HBM
+    d_pk, d_off, d_ln = buf.to(dev), poff.to(dev), pln.to(dev)
+    d_out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup + 20):
+        ctx.classify_dev(d_pk, d_off, d_ln, n, ul, 64, d_out, None, stream=sh)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        ctx.classify_dev(d_pk, d_off, d_ln, n, ul, 64, d_out, None, stream=sh)
+    b.record()
+    torch.cuda.synchronize(dev)
+    dev_ms = a.elapsed_time(b) / steps
+    dev_bad = int((d_out.cpu().numpy().view(R.VERDICT_DTYPE).tobytes() != want.tobytes()))
+    ctx.close()
+    res = dict(workload="cfg1", desc=w["desc"], frames=n,
+               parity=dict(checked=n, mismatches=bad, device_path_equal=(dev_bad == 0),
+                           sample="every frame of the pcap burst vs oracle/ref_cpu.c"),
+               rc0_frac=round(float((got["rc"] == 0).mean()), 4),
+               pcie_inclusive=dict(ms_per_burst=round(e2e_ms, 4), mpps=round(n / e2e_ms / 1e3, 2)),
+               device_resident=dict(ms_per_burst=round(dev_ms, 5), mpps=round(n / dev_ms / 1e3, 1)))
+    if budget_s > 0:
+        cpu = {}
+        for opt in ("O2", "O0"):
+            tb = oracle_tables("cfg1", udp, tcb, opt)
+            r1, d1, e1 = cpu_rate(tb, bufn, offn, lnn, ul, budget_s)
+            cpu[opt] = dict(mpps=round(r1 / 1e6, 4), frames=d1, seconds=round(e1, 2))
+        res["cpu_baseline"] = dict(
+            value=cpu["O2"]["mpps"], unit="Mpps", cores=1, kind="port",
+            sample=f"the same pcap burst ({n} frames), cycled; oracle/ref_cpu.c front end "
+                   f"(udp.c:11-19 lookup + verdict), 1 thread; host {cores['model']}",
+            O2=cpu["O2"], O0=cpu["O0"])
+    return res
+
+
+def hbm_copy_peak(dev, nbytes=4 << 30, reps=10):
+    """device-to-device copy rate on this box (read + write bytes / s): the
+    measured ceiling beside the 8 TB/s spec"""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / ms / 1e6, 1)
 
 
 # ---------------------------------------------------------------------------
@@ -438,16 +660,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2,cfg3,cfg4,cfg5",
                     help="BASELINE configs to run; the first is the headline line (cfg2 = configs[1])")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="host threads for the all-cores CPU baseline (the GPU box's CPU share "
-                         "is 16 per GPU; 0/1 = skip)")
+    ap.add_argument("--no-cfg1", action="store_true",
+                    help="skip BASELINE configs[0] (pcap, 1 flow; rank 0 at N = 1 only)")
+    ap.add_argument("--cpu-budget", type=float, default=4.0,
+                    help="seconds of oracle work per CPU-baseline leg (headline workload)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--parity-sample", type=int, default=4096,
+                    help="verdicts per rank and workload checked against the oracle after the "
+                         "timed steps (0 = none)")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
     ap.add_argument("--no-tx", action="store_true", help="skip timing the TX checksum kernel")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; "
-                    "gloo only to rehearse N > 1 on one GPU)")
+    ap.add_argument("--collective", default="rxg", choices=["rxg", "torch"],
+                    help="N > 1 count all-reduce: rxg = RCCL through librxgpu's C ABI "
+                         "(rxg_group); torch = torch.distributed's nccl (RCCL) backend")
+    ap.add_argument("--backend", default="gloo", help="torch.distributed backend of the control "
+                    "plane (rendezvous, barriers, max-over-ranks timing)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
     ap.add_argument("--ramp-ms", type=float, default=200.0,
@@ -462,15 +690,28 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.backend != "nccl":  # rehearsal: ranks may share a GPU
-        local = local % max(torch.cuda.device_count(), 1)
+    ndev = torch.cuda.device_count()
+    if world > 1 and ndev < world:  # rehearsal with ranks sharing GPUs (never RCCL then)
+        local = local % max(ndev, 1)
+    group = nccl_group = None
+    collective = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        if a.backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.distributed.init_process_group(a.backend)
+        torch.distributed.init_process_group(a.backend)
+        if a.collective == "rxg" and ndev >= world:
+            try:  # rank 0 makes the RCCL id, gloo hands it to every rank
+                obj = [R.group_id() if rank == 0 else None]
+                torch.distributed.broadcast_object_list(obj, src=0)
+                group = R.Group(local, world, rank, obj[0])
+                collective = "rccl (rxg_group_open / rxg_counts_allreduce, C ABI)"
+            except Exception as e:  # reported in the line, never silent
+                log(f"rank {rank}: rxg_group_open failed ({e}); using torch.distributed nccl")
+                group = None
+        if group is None:
+            nccl_group = torch.distributed.new_group(
+                backend="nccl" if ndev >= world else "gloo")
+            collective = "torch.distributed " + ("nccl (rccl)" if ndev >= world else "gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -486,17 +727,29 @@ def main():
     if a.sweep:
         sweep(ctx, a.sweep.split(","), a.steps, a.warmup, dev, a.sweep_variants, a.sweep_counts)
         return
+    cores = host_cores()
+    oracle_threads = max(1, cores["threads"] // max(1, min(world, 8)))
     names = [s.strip() for s in a.workload.split(",") if s.strip()]
-    results = {nm: run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev) for nm in names}
+    results = {}
+    for nm in names:
+        coll = None
+        if world > 1:
+            u, t = R.gen_flows(rxdist.gen_cfg(nm))
+            coll = collective_fn(group, nccl_group, len(u) + len(t))
+        results[nm] = run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev, coll,
+                                   a.parity_sample, oracle_threads)
+        log(nm, json.dumps({k: v for k, v in results[nm].items() if k != "desc"}))
     head = results[names[0]]
 
-    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(names[0], a.cpu_budget)
-        cpu_mt = cpu_baseline_mt(names[0], a.cpu_budget / 2, a.cpu_threads) \
-            if a.cpu_threads > 1 else None
-        for nm in names[1:]:
-            results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget / 2)
+        for i, nm in enumerate(names):
+            results[nm]["cpu_baseline"] = cpu_baseline(nm, a.cpu_budget if i == 0
+                                                       else a.cpu_budget / 2, cores)
+    cfg1 = None
+    if rank == 0 and world == 1 and not a.no_cfg1:
+        cfg1 = run_cfg1(local, dev, a.steps, a.warmup, 0 if a.no_cpu else a.cpu_budget / 2, cores)
+        log("cfg1", json.dumps(cfg1))
+    copy_peak = hbm_copy_peak(dev) if rank == 0 and world == 1 else None
 
     if a.e2e and rank == 0:
         pk = pcie_peaks(local)
@@ -507,6 +760,8 @@ def main():
             log("e2e", json.dumps(r))
             results[nm]["e2e_pcie"] = r
 
+    parity_bad = sum(r["parity"]["mismatches"] for r in results.values()) + \
+        (cfg1["parity"]["mismatches"] if cfg1 else 0)
     if rank == 0:
         line = {
             "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
@@ -521,28 +776,40 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (deterministic counter-based pktgen, generated in HBM)",
-            "config": {"workload": f"{names[0]}: {head['desc']}", "frames_per_gpu": head["n_per_gpu"],
-                       "flows": head["nflows"], "parallelism": f"rss-shard x{world}"},
+            "data": "synthetic (deterministic counter-based pktgen, generated in HBM; cfg1 "
+                    "through a pcap file)",
+            "config": {"workload": f"{names[0]}: {head['desc']}",
+                       "frames_per_step": head["frames_per_step"], "flows": head["nflows"],
+                       "parallelism": f"rss-split x{world}" if world > 1 else "1 GPU",
+                       "collective": collective},
             "gb_per_s": round(head["gbps"], 2),
             "roofline": head["roofline"],
-            "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_mt,
+            "cpu_baseline": head.get("cpu_baseline"),
+            "parity": head["parity"],
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
+            "hbm_copy_peak_gbs": copy_peak,
+            "librxgpu_sha256": lib_sha256()[:16],
         }
         if "tx_cksum" in head:
             line["tx_cksum"] = head["tx_cksum"]
         if "e2e_pcie" in head:
             line["e2e_pcie"] = head["e2e_pcie"]
             line["pcie_peaks"] = head["pcie_peaks"]
+        if cfg1:
+            line["cfg1"] = cfg1
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
         print(json.dumps(line), flush=True)
     ctx.close()
+    if group is not None:
+        group.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    if parity_bad:
+        log(f"bench: {parity_bad} verdicts differ from the oracle")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

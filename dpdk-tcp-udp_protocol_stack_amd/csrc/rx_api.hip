@@ -25,6 +25,16 @@ hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *l
                            uint32_t unit_log2, uint32_t len_hint, uint32_t variant,
                            uint32_t bpc_cap, hipStream_t s);
 uint32_t tx_num_variants();
+size_t rx_split_ws_bytes(uint32_t n, uint32_t nsh);
+hipError_t rx_split_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                           uint32_t n, uint32_t unit_log2, uint32_t nsh, uint32_t *first,
+                           uint32_t *perm, void *ws, hipStream_t s);
+size_t rx_gather_ws_bytes(uint32_t count);
+hipError_t rx_gather_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                            uint32_t unit_log2, const uint32_t *idx, uint32_t count, uint8_t *dst,
+                            uint64_t cap, uint32_t *dst_off, uint16_t *dst_len, void *ws,
+                            hipStream_t s);
+int rx_group_allreduce_u64(rxg_group *g, void *d, uint32_t n, hipStream_t s);
 
 static thread_local std::string g_last_hip;
 
@@ -32,6 +42,39 @@ int rx_set_hip_error(hipError_t e) {
     if (e == hipSuccess) return RXG_OK;
     g_last_hip = std::string(hipGetErrorName(e)) + ": " + hipGetErrorString(e);
     return RXG_EHIP;
+}
+
+void rx_set_last_error(const std::string &msg) { g_last_hip = msg; }
+
+hipError_t rx_occupancy(const void *fn, uint32_t threads, size_t lds, int *cu, int *occ) {
+    struct entry {
+        int dev;
+        const void *fn;
+        uint32_t threads;
+        size_t lds;
+        int cu, occ;
+    };
+    static thread_local std::vector<entry> cache;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    for (const entry &x : cache)
+        if (x.dev == dev && x.fn == fn && x.threads == threads && x.lds == lds) {
+            *cu = x.cu;
+            *occ = x.occ;
+            return hipSuccess;
+        }
+    entry x{dev, fn, threads, lds, 0, 0};
+    if ((e = hipDeviceGetAttribute(&x.cu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+        return e;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&x.occ, fn, (int)threads, lds)) !=
+        hipSuccess)
+        return e;
+    if (x.occ < 1) x.occ = 1;
+    cache.push_back(x);
+    *cu = x.cu;
+    *occ = x.occ;
+    return hipSuccess;
 }
 
 #define HIPCHK(x)                                                                                  \
@@ -126,6 +169,13 @@ struct rxg_ctx {
     uint32_t ft_load_log2 = RX_FT_LOAD_LOG2;           // rxg_tune_flow_load
     uint32_t *d_ws = nullptr; // launch workspace (binned lists, count slabs), grown on demand
     size_t d_ws_cap = 0;
+    // bursts on different streams share d_ws: a launch that uses it on another
+    // stream than the last one waits for that one's event first
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_used = false;
+    void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
+    size_t d_aux_cap = 0;
     // context-owned per-flow counts (host-buffer path)
     unsigned long long *d_counts = nullptr;
     uint32_t counts_cap = 0;
@@ -178,6 +228,8 @@ const char *rxg_strerror(int err) {
         return "burst exceeds the context's staging capacity or 32-bit offsets";
     case RXG_EHIP:
         return "HIP runtime error (see rxg_last_hip_error)";
+    case RXG_ECOMM:
+        return "RCCL error (see rxg_last_hip_error)";
     default:
         return "unknown error";
     }
@@ -213,6 +265,8 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
         if ((rc = rx_set_hip_error(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))))
             break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_listen, 65536 * sizeof(uint32_t))))) break;
+        if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming))))
+            break;
         c->max_pkts = max_pkts;
         c->max_bytes = (max_bytes + 15) & ~15ull;
         if (max_pkts && c->max_bytes) {
@@ -259,7 +313,9 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_listen);
     (void)hipFree(c->d_counts);
     (void)hipFree(c->d_ws);
+    (void)hipFree(c->d_aux);
     (void)hipFree(c->d_udpc);
+    if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
     for (rxg_ctx::slot &sl : c->slots) {
         (void)hipFree(sl.d_pkts);
         (void)hipFree(sl.d_off);
@@ -418,15 +474,35 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
     // workspace (binned lists, count slabs): grown on demand, so size it once
     // per burst shape before any graph capture
-    if (size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr)) {
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr);
+    if (ws) {
+        if (ws > c->d_ws_cap && c->ws_used) HIPCHK(hipEventSynchronize(c->ws_ev)); // in use
         int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
         if (rc) return rc;
+        if (c->ws_used && c->ws_stream != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
     }
     rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft, reinterpret_cast<uint4 *>(d_out),
-                              reinterpret_cast<unsigned long long *>(d_counts),
-                              (hipStream_t)stream, c->d_ws));
+    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+                              reinterpret_cast<uint4 *>(d_out),
+                              reinterpret_cast<unsigned long long *>(d_counts), s, c->d_ws));
+    if (ws) {
+        HIPCHK(hipEventRecord(c->ws_ev, s));
+        c->ws_stream = s;
+        c->ws_used = true;
+    }
     return RXG_OK;
+}
+
+// Frames of a host burst into a slot: exactly `span` bytes cross PCIe (the
+// caller's buffer may end there), and the device copy is zero-filled up to the
+// next 16-B boundary, which the kernels read as the frame's padding.
+static hipError_t copy_in_frames(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts,
+                                 uint64_t span) {
+    hipError_t e = hipMemcpyAsync(sl.d_pkts, pkts, span, hipMemcpyHostToDevice, c->s_h2d);
+    const uint64_t pad = ((span + 15) & ~15ull) - span;
+    if (e == hipSuccess && pad) e = hipMemsetAsync(sl.d_pkts + span, 0, pad, c->s_h2d);
+    return e;
 }
 
 // burst -> slot: device-side ordering only (the host blocks in rxg_wait):
@@ -437,7 +513,7 @@ static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint6
                        uint32_t off_unit_log2, rxg_verdict *out, uint64_t ticket) {
     const bool reused = sl.ticket != 0;
     if (reused) HIPCHK(hipStreamWaitEvent(c->s_h2d, sl.ev_k, 0));
-    HIPCHK(hipMemcpyAsync(sl.d_pkts, pkts, span, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(copy_in_frames(c, sl, pkts, span));
     HIPCHK(hipMemcpyAsync(sl.d_off, off, n * 4ull, hipMemcpyHostToDevice, c->s_h2d));
     HIPCHK(hipMemcpyAsync(sl.d_len, len, n * 2ull, hipMemcpyHostToDevice, c->s_h2d));
     HIPCHK(hipEventRecord(sl.ev_in, c->s_h2d));
@@ -445,16 +521,25 @@ static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint6
     if (reused) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
-    if (size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, c->d_counts != nullptr)) {
+    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, c->d_counts != nullptr);
+    if (ws) {
         if (ws > c->d_ws_cap) { // grows only between bursts: drain the kernels using it
             HIPCHK(hipStreamSynchronize(c->stream));
+            if (c->ws_used) HIPCHK(hipEventSynchronize(c->ws_ev));
             int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
             if (rc) return rc;
         }
+        if (c->ws_used && c->ws_stream != c->stream)
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ws_ev, 0));
     }
     rx_set_bpc_cap(c->tune_bpc);
     HIPCHK(rx_classify_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, g, p, fpg, pipe,
                               c->ft, sl.d_out, c->d_counts, c->stream, c->d_ws));
+    if (ws) {
+        HIPCHK(hipEventRecord(c->ws_ev, c->stream));
+        c->ws_stream = c->stream;
+        c->ws_used = true;
+    }
     HIPCHK(hipEventRecord(sl.ev_k, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
     HIPCHK(hipMemcpyAsync(out, sl.d_out, n * 16ull, hipMemcpyDeviceToHost, c->s_d2h));
@@ -484,8 +569,8 @@ int rxg_submit(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint3
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
     const uint64_t t = c->next_ticket++;
-    rc = submit_slot(c, c->slots[t % RXG_PIPE_DEPTH], pkts, (span_bytes + 15) & ~15ull, off, len,
-                     n, off_unit_log2, out, t);
+    rc = submit_slot(c, c->slots[t % RXG_PIPE_DEPTH], pkts, span_bytes, off, len, n,
+                     off_unit_log2, out, t);
     if (rc == RXG_OK && ticket) *ticket = t;
     return rc;
 }
@@ -572,17 +657,18 @@ int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t 
     int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
-    const uint64_t span = (span_bytes + 15) & ~15ull;
+    const uint64_t span = span_bytes;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
     if (sl.ticket) HIPCHK(hipStreamWaitEvent(c->s_h2d, sl.ev_k, 0));
-    HIPCHK(hipMemcpyAsync(sl.d_pkts, pkts, span, hipMemcpyHostToDevice, c->s_h2d));
+    HIPCHK(copy_in_frames(c, sl, pkts, span));
     HIPCHK(hipMemcpyAsync(sl.d_off, off, n * 4ull, hipMemcpyHostToDevice, c->s_h2d));
     HIPCHK(hipMemcpyAsync(sl.d_len, len, n * 2ull, hipMemcpyHostToDevice, c->s_h2d));
     HIPCHK(hipEventRecord(sl.ev_in, c->s_h2d));
     HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_in, 0));
     if (sl.ticket) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
-    HIPCHK(tx_cksum_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, (uint32_t)(span / n),
+    HIPCHK(tx_cksum_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2,
+                           (uint32_t)(span / n),
                            c->tune_tx, c->tune_tx_bpc, c->stream));
     HIPCHK(hipEventRecord(sl.ev_k, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
@@ -590,6 +676,69 @@ int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t 
     HIPCHK(hipEventRecord(sl.ev_done, c->s_d2h));
     sl.ticket = t;
     HIPCHK(hipEventSynchronize(sl.ev_done));
+    return RXG_OK;
+}
+
+int rxg_rss_split_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                      const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t n_shards,
+                      uint32_t *d_first, uint32_t *d_perm, void *stream) {
+    if (!c || !d_first || n_shards == 0 || n_shards > RXG_MAX_SHARDS) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n && (!d_pkts || !d_off || !d_len || !d_perm)) return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t ws = rx_split_ws_bytes(n, n_shards);
+    if (ws > c->d_aux_cap) { // grows between bursts only
+        HIPCHK(hipDeviceSynchronize());
+        int rc = ensure_dev(&c->d_aux, &c->d_aux_cap, ws);
+        if (rc) return rc;
+    }
+    HIPCHK(rx_split_launch(d_pkts, d_off, d_len, n, off_unit_log2, n_shards, d_first, d_perm,
+                           c->d_aux, s));
+    return RXG_OK;
+}
+
+int rxg_gather_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                   const uint16_t *d_len, uint32_t off_unit_log2, const uint32_t *d_idx,
+                   uint32_t count, uint8_t *d_dst, uint64_t dst_cap, uint32_t *d_dst_off,
+                   uint16_t *d_dst_len, uint64_t *span, void *stream) {
+    if (!c) return RXG_EINVAL;
+    if (span) *span = 0;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (count == 0) return RXG_OK;
+    if (!d_pkts || !d_off || !d_len || !d_idx || !d_dst || !d_dst_off || !d_dst_len)
+        return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t ws = rx_gather_ws_bytes(count);
+    if (ws > c->d_aux_cap) {
+        HIPCHK(hipDeviceSynchronize());
+        int rc = ensure_dev(&c->d_aux, &c->d_aux_cap, ws);
+        if (rc) return rc;
+    }
+    HIPCHK(rx_gather_launch(d_pkts, d_off, d_len, off_unit_log2, d_idx, count, d_dst, dst_cap,
+                            d_dst_off, d_dst_len, c->d_aux, s));
+    // the packed size (64-B units) sits after the per-chunk sums
+    const size_t nchunks = (ws - 8) / 8;
+    uint64_t units = 0;
+    HIPCHK(hipMemcpyAsync(&units, reinterpret_cast<uint64_t *>(c->d_aux) + nchunks, 8,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (span) *span = units << 6;
+    if ((units << 6) > dst_cap || units > 0xFFFFFFFFull) return RXG_ERANGE;
+    return RXG_OK;
+}
+
+int rxg_ctx_counts_allreduce(rxg_ctx *c, rxg_group *g) {
+    if (!c || !g) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t nf = c->ft.nu + c->ft.nt;
+    int rc = rx_group_allreduce_u64(g, c->d_counts, nf, c->stream); // after the bursts' kernels
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;
 }
 

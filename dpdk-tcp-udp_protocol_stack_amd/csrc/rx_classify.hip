@@ -406,28 +406,14 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
                     const uint32_t *n_dev = nullptr) {
     constexpr uint32_t TILE = (256 / G) * FPG;
     const size_t lds = (size_t)lds_bins * 4u;
-    // resident blocks: one wave of blocks, equal shares, no tail (cached per LDS size)
-    static int cu = 0;
-    static int cached_occ[2] = {0, 0};
-    static size_t cached_lds[2] = {~(size_t)0, ~(size_t)0};
-    if (cu == 0) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-    }
-    const int slot = lds ? 1 : 0;
-    if (cached_lds[slot] != lds) {
-        int occ = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), 256, lds);
-        if (e != hipSuccess) return e;
-        cached_occ[slot] = occ > 0 ? occ : 1;
-        cached_lds[slot] = lds;
-    }
+    // resident blocks: one wave of blocks, equal shares, no tail
+    int cu = 0, bpc = 0;
+    hipError_t e = rx_occupancy(
+        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), 256,
+        lds, &cu, &bpc);
+    if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
-    uint64_t occ = (uint64_t)cached_occ[slot];
+    uint64_t occ = (uint64_t)bpc;
     if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
@@ -832,28 +818,13 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
                        (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u) + (PIPE == 12 ? 16384u : 0u);
-    static int cu = 0;
-    static int cached_occ[2] = {0, 0};
-    static size_t cached_lds[2] = {~(size_t)0, ~(size_t)0};
-    if (cu == 0) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-    }
-    const int slot = lds ? 1 : 0;
-    if (cached_lds[slot] != lds) {
-        int occ = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
-            lds);
-        if (e != hipSuccess) return e;
-        cached_occ[slot] = occ > 0 ? occ : 1;
-        cached_lds[slot] = lds;
-    }
+    int cu = 0, bpc = 0;
+    hipError_t e = rx_occupancy(
+        reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
+        lds, &cu, &bpc);
+    if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + 255) / 256;
-    uint64_t occ = (uint64_t)cached_occ[slot];
+    uint64_t occ = (uint64_t)bpc;
     if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;

@@ -39,6 +39,12 @@ struct rx_ft_dev {
 #define RX_UDPC_MAX_FLOWS 1024u // load <= 1/2: <= 2048 slots = 16 KiB of LDS
 #define RX_FT_LOAD_LOG2 2u      // exact-key tables: load <= 1/4 by default (rxg_tune_flow_load)
 
+// Host: CU count of the calling thread's current device and the resident
+// blocks per CU of kernel `fn` (`threads` per block, `lds` bytes of dynamic
+// LDS) on it.  Cached per thread and keyed by (device, kernel, lds), so rx
+// threads with their own contexts (and devices) never share mutable state.
+hipError_t rx_occupancy(const void *fn, uint32_t threads, size_t lds, int *cu, int *occ);
+
 RX_HD uint32_t rx_hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = 0x9E3779B9u ^ a;
     h *= 0x85EBCA6Bu;
@@ -87,6 +93,20 @@ RX_HD uint32_t rx_rss_hash(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t 
     }
     return r;
 }
+
+// RSS hash of one frame from its first 40 bytes as little-endian dwords w[0..9]
+// (bytes past the captured length already zero): the queue key a multi-queue
+// NIC hashes — (sip, dip, sport, dport) for IPv4 TCP/UDP, (sip, dip) for other
+// IPv4 — and 0 (queue 0) for non-IPv4 frames, which carry no IP tuple.
+RX_HD uint32_t rx_rss_frame(const uint32_t *w) {
+    if ((w[3] & 0xFFFFu) != 0x0008u) return 0; // ether_type bytes {08, 00}
+    const uint32_t proto = w[5] >> 24;          // byte 23
+    const uint32_t sip = (w[6] >> 16) | (w[7] << 16), dip = (w[7] >> 16) | (w[8] << 16);
+    const bool l4 = proto == 6u || proto == 17u;
+    return rx_rss_hash(sip, dip, l4 ? (w[8] >> 16) : 0u, l4 ? (w[9] & 0xFFFFu) : 0u);
+}
+
+#define RX_MAX_SHARDS 64u
 
 // ---------------------------------------------------------------------------
 // Counter-based RNG: value k of frame i is a pure function of (seed, i, k).
@@ -180,6 +200,10 @@ RX_HD rx_frame_plan rx_gen_plan(const rxg_gen_cfg &cfg, uint64_t i) {
                 pl.kind = 0;
                 pl.sip = rnd_sip;
                 pl.sport = rnd_sport;
+                if (cfg.src_ip && !unknown) { // one client 5-tuple (BASELINE configs[0])
+                    pl.sip = cfg.src_ip;
+                    pl.sport = rx_hton16(cfg.src_port);
+                }
                 if (unknown) {
                     pl.dport = rx_hton16(7); // no socket bound to :7
                 } else {

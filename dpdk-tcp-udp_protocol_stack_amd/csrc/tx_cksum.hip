@@ -152,18 +152,10 @@ template <int G, int P, int FPG, int WB = 0>
 hipError_t launch_tx(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, uint32_t bpc_cap, hipStream_t s) {
     constexpr uint32_t TILE = (256 / G) * FPG;
-    static int cu = 0, occ = 0;
-    if (cu == 0) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(tx_cksum_kernel<G, P, FPG, WB>), 256, 0);
-        if (e != hipSuccess) return e;
-        if (occ < 1) occ = 1;
-    }
+    int cu = 0, occ = 0;
+    hipError_t e = rx_occupancy(reinterpret_cast<const void *>(tx_cksum_kernel<G, P, FPG, WB>),
+                                256, 0, &cu, &occ);
+    if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
     uint64_t bpc = (uint64_t)occ;
     if (bpc_cap && bpc > bpc_cap) bpc = bpc_cap;

@@ -83,7 +83,8 @@ class GenCfg(C.Structure):
         ("n_tcp", C.c_uint32), ("local_ip", C.c_uint32), ("udp_base_port", C.c_uint16),
         ("tcp_port", C.c_uint16), ("bad_cksum_per10k", C.c_uint32),
         ("unknown_per10k", C.c_uint32), ("other_per10k", C.c_uint32), ("shard", C.c_uint32),
-        ("n_shards", C.c_uint32), ("packed", C.c_uint32),
+        ("n_shards", C.c_uint32), ("packed", C.c_uint32), ("src_ip", C.c_uint32),
+        ("src_port", C.c_uint16), ("_pad", C.c_uint16),
     ]
 
 
@@ -138,20 +139,34 @@ _pcap_read = _sig("rxg_pcap_read_burst", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _
 _pcap_write = _sig("rxg_pcap_write", _i32, C.c_char_p, _vp, _vp, _vp, _u32, _u32)
 _tx_cksum_dev = _sig("rxg_tx_cksum_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp)
 _tx_cksum = _sig("rxg_tx_cksum", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32)
+_rss_split = _sig("rxg_rss_split", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+_rss_split_dev = _sig("rxg_rss_split_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
+                      _vp)
+_gather_dev = _sig("rxg_gather_dev", _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _vp, _u64, _vp, _vp,
+                   C.POINTER(_u64), _vp)
+_group_id = _sig("rxg_group_id", _i32, _vp)
+_group_open = _sig("rxg_group_open", _i32, C.POINTER(_vp), _i32, _u32, _u32, _vp)
+_group_close = _sig("rxg_group_close", None, _vp)
+_counts_allreduce = _sig("rxg_counts_allreduce", _i32, _vp, _vp, _u32, _vp)
+_ctx_counts_allreduce = _sig("rxg_ctx_counts_allreduce", _i32, _vp, _vp)
 PIPE_DEPTH = 3
+MAX_SHARDS = 64
+GROUP_ID_BYTES = 128
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
-            "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum"]
+            "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum", "rxg_rss_split",
+            "rxg_rss_split_dev", "rxg_gather_dev", "rxg_group_id", "rxg_group_open",
+            "rxg_group_close", "rxg_counts_allreduce", "rxg_ctx_counts_allreduce"]
 
 
 class RxgError(RuntimeError):
     def __init__(self, rc: int, what: str):
         msg = _strerror(rc).decode()
-        if rc == -1000:
+        if rc in (-1000, -1001):
             msg += " [" + _last_hip().decode() + "]"
         super().__init__(f"{what}: {msg} ({rc})")
         self.rc = rc
@@ -309,6 +324,29 @@ class Context:
                "rxg_process_mbufs")
         return out
 
+    def rss_split_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, n_shards: int,
+                      d_first, d_perm, stream=None):
+        """RSS split of a device burst: d_first (n_shards + 1 u32) and d_perm (n u32)"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        _check(_rss_split_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, n_shards,
+                              p(d_first), p(d_perm), stream), "rxg_rss_split_dev")
+
+    def gather_dev(self, d_pkts, d_off, d_len, off_unit_log2: int, d_idx, count: int, d_dst,
+                   dst_cap: int, d_dst_off, d_dst_len, stream=None) -> int:
+        """pack frames d_idx[0..count) into d_dst (64-B units); returns the bytes used"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        span = _u64()
+        _check(_gather_dev(self._h, p(d_pkts), p(d_off), p(d_len), off_unit_log2, p(d_idx), count,
+                           p(d_dst), dst_cap, p(d_dst_off), p(d_dst_len), C.byref(span), stream),
+               "rxg_gather_dev")
+        return span.value
+
+    def counts_allreduce(self, group: "Group"):
+        """sum the context-owned counts over the group's ranks (synchronous)"""
+        _check(_ctx_counts_allreduce(self._h, group._h), "rxg_ctx_counts_allreduce")
+
     def flow_counts(self) -> np.ndarray:
         n = self.num_flows
         out = np.zeros(max(n, 1), np.uint64)
@@ -370,11 +408,58 @@ def rss_hash(sip: int, dip: int, sport: int, dport: int) -> int:
     return _rss(sip, dip, sport, dport)
 
 
+def rss_split(pkts: np.ndarray, off: np.ndarray, lens: np.ndarray, off_unit_log2: int,
+              n_shards: int):
+    """host RSS split (rxg_rss_split): (first[n_shards + 1], perm[n])"""
+    pkts = np.ascontiguousarray(pkts, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    lens = np.ascontiguousarray(lens, np.uint16)
+    first = np.zeros(n_shards + 1, np.uint32)
+    perm = np.zeros(max(len(off), 1), np.uint32)
+    _check(_rss_split(_ptr(pkts), _ptr(off), _ptr(lens), len(off), off_unit_log2, n_shards,
+                      _ptr(first), _ptr(perm)), "rxg_rss_split")
+    return first, perm[:len(off)]
+
+
+def group_id() -> bytes:
+    """rank 0: a fresh communicator id to hand to every rank (rxg_group_id)"""
+    b = (C.c_uint8 * GROUP_ID_BYTES)()
+    _check(_group_id(b), "rxg_group_id")
+    return bytes(b)
+
+
+class Group:
+    """rxg_group: the node's GPUs as one RCCL communicator (one rank per process)"""
+
+    def __init__(self, device: int, nranks: int, rank: int, gid: bytes):
+        assert len(gid) == GROUP_ID_BYTES
+        h = _vp()
+        buf = (C.c_uint8 * GROUP_ID_BYTES)(*gid)
+        _check(_group_open(C.byref(h), device, nranks, rank, buf), "rxg_group_open")
+        self._h = h
+
+    def allreduce(self, d_counts, n: int, stream=None):
+        """in-place sum of a device u64[n] vector over the ranks, async on stream"""
+        p = d_counts if isinstance(d_counts, int) else d_counts.data_ptr()
+        _check(_counts_allreduce(self._h, p, n, stream), "rxg_counts_allreduce")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _group_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def make_gen_cfg(**kw) -> GenCfg:
     d = dict(seed=0x5EED0001, size_mode=0, frame_len=64, slot_bytes=64, proto_mode=0, n_udp=1024,
              n_tcp=0, local_ip=ip_raw("192.168.100.77"), udp_base_port=20000, tcp_port=9999,
              bad_cksum_per10k=100, unknown_per10k=50, other_per10k=50, shard=0, n_shards=1,
-             packed=0)
+             packed=0, src_ip=0, src_port=0)
     d.update(kw)
     return GenCfg(**d)
 

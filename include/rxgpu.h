@@ -121,7 +121,8 @@ enum {
     RXG_ENOMEM = -12,
     RXG_ENODEV = -19,
     RXG_ERANGE = -34,
-    RXG_EHIP = -1000 /* HIP runtime error (details: rxg_last_hip_error) */
+    RXG_EHIP = -1000, /* HIP runtime error (details: rxg_last_hip_error) */
+    RXG_ECOMM = -1001 /* RCCL error (details: rxg_last_hip_error) */
 };
 
 typedef struct rxg_ctx rxg_ctx;
@@ -242,6 +243,59 @@ uint32_t rxg_ft_lookup_tcp(const rxg_ctx *ctx, uint32_t sip, uint32_t dip, uint1
  * network byte order, as a multi-queue NIC computes it; shard = hash % n. */
 uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
 
+/* ---- multi-GPU: RSS split, shard gather, per-flow count all-reduce ------
+ * The reference runs one rx queue (ng_init_port, netfamily.c:38-39) and one
+ * pkt_process lcore (netfamily.c:427) over the burst it dequeues at
+ * netfamily.c:147.  Across G GPUs of a node the burst is split by RSS, as the
+ * multi-queue NIC the README assumes (README.md:13) would: each GPU holds a
+ * replica of the flow tables (rxg_flows_sync with the same lists) and
+ * classifies its shard; the per-flow counts are the only exchange. */
+#define RXG_MAX_SHARDS 64
+
+/* Shard of a frame = rxg_rss_hash(sip, dip, sport, dport) % n_shards for IPv4
+ * TCP/UDP, rxg_rss_hash(sip, dip, 0, 0) % n_shards for other IPv4, 0 for
+ * non-IPv4 frames (bytes past the captured length read as 0).  perm[] gets
+ * the frame indices grouped by shard, in burst order inside a shard;
+ * first[s] = start of shard s in perm, first[n_shards] = n (n_shards + 1
+ * entries).  Host form: host buffers, synchronous.  Device form: device
+ * buffers, asynchronous on `stream` (workspace grown on demand, between
+ * bursts). */
+int rxg_rss_split(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                  uint32_t off_unit_log2, uint32_t n_shards, uint32_t *first, uint32_t *perm);
+int rxg_rss_split_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                      const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t n_shards,
+                      uint32_t *d_first, uint32_t *d_perm, void *stream);
+
+/* Gather frames d_idx[0..count) of a device burst into a packed device burst
+ * (the DMA of one RSS queue's frames into its ring): frame k at
+ * d_dst + (d_dst_off[k] << 6), 64-B aligned, zero-filled to its 64-B end,
+ * d_dst_len[k] = its captured length (so the result is classified with
+ * off_unit_log2 = 6).  *span = bytes the packed burst occupies.  Synchronises
+ * `stream` (setup-time operation); RXG_ERANGE if the packed burst exceeds
+ * dst_cap (frames past dst_cap are not copied). */
+int rxg_gather_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                   const uint16_t *d_len, uint32_t off_unit_log2, const uint32_t *d_idx,
+                   uint32_t count, uint8_t *d_dst, uint64_t dst_cap, uint32_t *d_dst_off,
+                   uint16_t *d_dst_len, uint64_t *span, void *stream);
+
+/* A communicator over the GPUs of the node (RCCL over xGMI), one rank per
+ * GPU/process.  Rank 0 makes the id with rxg_group_id and the caller hands it
+ * to every rank by its own means (a file, a socket, MPI, torch.distributed);
+ * every rank then calls rxg_group_open with it (collective: returns once all
+ * nranks have joined). */
+#define RXG_GROUP_ID_BYTES 128
+typedef struct rxg_group rxg_group;
+int rxg_group_id(uint8_t id[RXG_GROUP_ID_BYTES]);
+int rxg_group_open(rxg_group **g, int device, uint32_t nranks, uint32_t rank,
+                   const uint8_t id[RXG_GROUP_ID_BYTES]);
+void rxg_group_close(rxg_group *g);
+/* Sum of a device u64 count vector over the ranks, in place, asynchronous on
+ * `stream` (every rank must call it with the same n). */
+int rxg_counts_allreduce(rxg_group *g, uint64_t *d_counts, uint32_t n, void *stream);
+/* The same for the context-owned counts (rxg_classify / rxg_process_mbufs),
+ * after every burst submitted so far; synchronous. */
+int rxg_ctx_counts_allreduce(rxg_ctx *ctx, rxg_group *g);
+
 /* ---- pcap ingest (the NIC stand-in: rte_eth_rx_burst into the in-ring,
  * netfamily.c:438-440) -------------------------------------------------- */
 /* Classic libpcap files, LINKTYPE_ETHERNET, either byte order, us or ns
@@ -285,6 +339,11 @@ typedef struct rxg_gen_cfg {
     uint32_t packed;        /* 0: frame i in slot i (slot_bytes apart); 1: frames packed
                                back to back at 64-B alignment (what rxg_process_mbufs
                                staging produces); slot_bytes then bounds one frame */
+    uint32_t src_ip;        /* network order; != 0: every UDP frame to a bound socket
+                               comes from src_ip:src_port (one 5-tuple, e.g. the echo
+                               client of BASELINE configs[0]); 0: random sources */
+    uint16_t src_port;      /* host order */
+    uint16_t _pad;
 } rxg_gen_cfg;
 
 /* Flow set the generator assumes (the sockets/tcbs a test or bench binds). */

@@ -1,11 +1,18 @@
 """N > 1 path on CPU: world_size 2 over gloo (127.0.0.1).
 
-Each rank generates its RSS shard of a workload (the same pktgen the GPU
-bench uses), computes its per-flow counts (here with the oracle: no GPU in
-this container), and reduces them with rxdist.allreduce_counts, the single
-collective of the rx path.  Checks: every rank's frames hash to that rank,
-and the reduced counts equal the sum of the per-shard histograms computed
-independently in one process."""
+SURVEY.md §8(e)'s rule, on one burst: every rank splits the SAME burst with
+the RSS split of librxgpu (rxg_rss_split: the multi-queue NIC the reference's
+README assumes, README.md:13, in place of its single queue, netfamily.c:38-39),
+classifies its own shard, and reduces its per-flow counts with the path's one
+collective.  Checks: the per-shard verdicts, put back in burst order through
+the split's permutation, equal the verdicts of the unsharded burst; the
+all-reduced counts equal the unsharded histogram; every frame of a shard
+hashes to that shard by the oracle's independent Toeplitz restatement.
+
+No GPU here, so each shard is classified by the oracle (the checker) and the
+counts are reduced over gloo; the same split + classify + RCCL reduce runs on
+the GPU in tests/test_multigpu.py (one GPU, two contexts) and in bench.py
+--gpus N (one rank per GPU)."""
 import os
 import socket
 
@@ -22,34 +29,39 @@ import rxgpu as R
 N_FRAMES = 3000
 
 
-def _shard(name, rank, world):
-    cfg = rxdist.gen_cfg(name, rank, world, n_udp=256, n_tcp=255)
+def _burst(name):
+    cfg = rxdist.gen_cfg(name, n_udp=256, n_tcp=255)
     pk, off, ln = R.gen_host(cfg, 0, N_FRAMES, 6)
     udp, tcb = R.gen_flows(cfg)
-    v, cnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
-    return cfg, pk, off, v, cnt
+    return pk, off, ln, udp, tcb
+
+
+def _frame_shard(pk, o, l, world):
+    """independent shard rule: oracle Toeplitz over the frame's tuple"""
+    b = pk[int(o) << 6:(int(o) << 6) + 48].tobytes()
+    b = b[:int(l)] + b"\0" * (48 - min(int(l), 48))
+    if b[12:14] != b"\x08\x00":
+        return 0
+    sip, dip = int.from_bytes(b[26:30], "little"), int.from_bytes(b[30:34], "little")
+    l4 = b[23] in (6, 17)
+    sp = int.from_bytes(b[34:36], "little") if l4 else 0
+    dp = int.from_bytes(b[36:38], "little") if l4 else 0
+    return O.rss_hash(sip, dip, sp, dp) % world
 
 
 def _worker(rank, world, port, name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg, pk, off, v, cnt = _shard(name, rank, world)
-        # every IP frame of this rank carries a tuple whose RSS hash picks this rank
-        bad = 0
-        for k in range(N_FRAMES):
-            b = pk[int(off[k]) << 6:(int(off[k]) << 6) + 64].tobytes()
-            if b[12:14] != b"\x08\x00":
-                continue
-            sip, dip = int.from_bytes(b[26:30], "little"), int.from_bytes(b[30:34], "little")
-            l4 = b[23] in (6, 17)
-            sp = int.from_bytes(b[34:36], "little") if l4 else 0
-            dp = int.from_bytes(b[36:38], "little") if l4 else 0
-            bad += O.rss_hash(sip, dip, sp, dp) % world != rank
+        pk, off, ln, udp, tcb = _burst(name)
+        first, perm = R.rss_split(pk, off, ln, 6, world)
+        mine = perm[first[rank]:first[rank + 1]]
+        bad = sum(_frame_shard(pk, off[i], ln[i], world) != rank for i in mine)
+        v, cnt = O.Tables(udp, tcb).classify(pk, off[mine], ln[mine], 6, counts=True)
         t = torch.from_numpy(cnt.astype(np.int64))
         work = rxdist.allreduce_counts(t, world, async_op=True)
         work.wait()
-        q.put((rank, bad, t.numpy().copy()))
+        q.put((rank, bad, mine.copy(), v.tobytes(), t.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -61,7 +73,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("name", ["cfg2", "cfg4"])
-def test_two_rank_shard_and_count_reduce(name):
+def test_two_rank_split_parity_and_count_reduce(name):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -73,9 +85,43 @@ def test_two_rank_shard_and_count_reduce(name):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process reference: the per-shard histograms, summed
-    want = sum(_shard(name, r, world)[4].astype(np.int64) for r in range(world))
-    for rank, bad, got in out:
+    pk, off, ln, udp, tcb = _burst(name)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    got = np.zeros(N_FRAMES, R.VERDICT_DTYPE)
+    seen = np.zeros(N_FRAMES, np.int64)
+    for rank, bad, mine, vb, cnt in out:
         assert bad == 0, f"rank {rank}: {bad} frames outside its RSS shard"
-        assert np.array_equal(got, want), rank
-    assert want.sum() > 0.9 * world * N_FRAMES
+        assert np.all(np.diff(mine.astype(np.int64)) > 0), "shard not in burst order"
+        got[mine] = np.frombuffer(vb, R.VERDICT_DTYPE)
+        seen[mine] += 1
+        assert np.array_equal(cnt, wcnt.astype(np.int64)), rank
+    assert np.all(seen == 1), "the shards do not partition the burst"
+    assert got.tobytes() == want.tobytes()
+    sizes = sorted(len(o[2]) for o in out)
+    assert sizes[0] > 0.3 * N_FRAMES, sizes  # both shards carry traffic
+
+
+@pytest.mark.parametrize("nsh", [1, 2, 3, 8, 64])
+def test_host_split_matches_oracle_shards(nsh):
+    """rxg_rss_split on mixed traffic (ARP/ICMP, runts, truncated captures):
+    each shard is exactly the frames the oracle's Toeplitz puts there, in
+    burst order, and first[] delimits them"""
+    cfg = rxdist.gen_cfg("cfg4", n_udp=300, n_tcp=300, other_per10k=800)
+    pk, off, ln = R.gen_host(cfg, 7, 2000, 6)
+    rng = np.random.default_rng(nsh)
+    ln = ln.copy()
+    cut = rng.random(2000) < 0.05
+    ln[cut] = rng.integers(0, 40, cut.sum())  # captures that end inside the tuple
+    first, perm = R.rss_split(pk, off, ln, 6, nsh)
+    assert first[0] == 0 and first[nsh] == 2000
+    want = np.array([_frame_shard(pk, off[i], ln[i], nsh) for i in range(2000)])
+    for s in range(nsh):
+        sl = perm[first[s]:first[s + 1]]
+        assert np.array_equal(sl, np.nonzero(want == s)[0]), s
+
+
+def test_split_rejects_bad_shard_counts():
+    pk, off, ln = R.gen_host(rxdist.gen_cfg("cfg2"), 0, 10, 6)
+    for nsh in (0, R.MAX_SHARDS + 1):
+        with pytest.raises(R.RxgError):
+            R.rss_split(pk, off, ln, 6, nsh)

@@ -132,3 +132,83 @@ def test_pcap_pipeline_matches_oracle(tmp_path):
         pc.close()
     finally:
         ctx.close()
+
+
+def test_cfg1_generator_is_one_flow():
+    """BASELINE configs[0]: 100K x 64 B UDP, every frame the echo client's
+    5-tuple 10.0.0.1:5555 -> 192.168.100.77:8889 (netfamily.c:227-229), every
+    frame delivered to the one socket by the oracle"""
+    cfg = rxdist.gen_cfg("cfg1")
+    pk, off, ln = R.gen_host(cfg, 0, 5000, 6)
+    fr = pk.reshape(5000, 64)
+    assert np.all(ln == 64)
+    assert np.all(fr[:, 26:30] == np.frombuffer(bytes([10, 0, 0, 1]), np.uint8))
+    assert np.all(fr[:, 30:34] == np.frombuffer(bytes([192, 168, 100, 77]), np.uint8))
+    assert np.all(fr[:, 34:36] == np.frombuffer((5555).to_bytes(2, "big"), np.uint8))
+    assert np.all(fr[:, 36:38] == np.frombuffer((8889).to_bytes(2, "big"), np.uint8))
+    udp, tcb = R.gen_flows(cfg)
+    assert len(udp) == 1 and len(tcb) == 0
+    v = O.Tables(udp, tcb).classify(pk, off, ln, 6)
+    assert np.all(v["rc"] == 0) and np.all(v["flow_id"] == 0) and np.all(v["payload_len"] == 22)
+
+
+@pytest.mark.gpu
+def test_cfg1_pcap_through_gpu_matches_oracle(tmp_path):
+    """cfg1 end to end: the 100K frames written with rxg_pcap_write, read back
+    with rxg_pcap_read_burst into pinned memory, classified by rxg_classify
+    (host-buffer path): every verdict equals the oracle's on the same bytes"""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a GPU (no fallback path exists)")
+    w = rxdist.WORKLOADS["cfg1"]
+    cfg = rxdist.gen_cfg("cfg1")
+    n = w["n"]
+    pk, off, ln = R.gen_host(cfg, 0, n, 6)
+    p = str(tmp_path / "cfg1.pcap")
+    R.pcap_write(p, pk, off, ln, 6)
+    pc = R.Pcap(p)
+    buf = torch.zeros(n * 64 + 64, dtype=torch.uint8).pin_memory()
+    po = torch.zeros(n, dtype=torch.int32).pin_memory()
+    pl = torch.zeros(n, dtype=torch.int16).pin_memory()
+    got_n, span = pc.read_burst_into(buf.numpy(), po.numpy().view(np.uint32),
+                                     pl.numpy().view(np.uint16), 6)
+    pc.close()
+    assert got_n == n and span == n * 64
+    udp, tcb = R.gen_flows(cfg)
+    with R.Context(0, max_pkts=n, max_bytes=span) as ctx:
+        ctx.flows_sync(udp, tcb)
+        got = ctx.classify(buf.numpy()[:span], po.numpy().view(np.uint32),
+                           pl.numpy().view(np.uint16), 6)
+        want = O.Tables(udp, tcb).classify(buf.numpy()[:span], po.numpy().view(np.uint32),
+                                           pl.numpy().view(np.uint16), 6)
+        assert got.tobytes() == want.tobytes()
+        assert np.all(got["rc"] == 0)
+        assert np.array_equal(ctx.flow_counts(), np.array([n], np.uint64))
+
+
+@pytest.mark.gpu
+def test_host_buffers_end_exactly_at_the_last_frame():
+    """a host burst whose buffer ends at the last frame's last byte (not on a
+    16-B boundary): the copy in reads no byte past it, the TX copy back writes
+    no byte past it (guard bytes after a view of exactly span bytes)"""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a GPU (no fallback path exists)")
+    frames = [F.udp_frame("10.0.0.1", 5555, "192.168.100.77", 8889, b"x" * k) for k in (5, 9, 30)]
+    buf, off, lens = F.pack_frames(frames, 4)
+    span = (int(off[-1]) << 4) + int(lens[-1])
+    assert span % 16
+    store = np.full(span + 32, 0xEE, np.uint8)  # guard bytes after the burst
+    store[:span] = buf[:span]
+    udp = np.zeros(1, R.UDP_SOCK_DTYPE)
+    udp[0] = (R.ip_raw("192.168.100.77"), R.port_raw(8889), 17, 0)
+    with R.Context(0, max_pkts=16, max_bytes=4096) as ctx:
+        ctx.flows_sync(udp, None)
+        got = ctx.classify(store[:span], off, lens, 4)
+        want = O.Tables(udp, np.zeros(0, R.TCB_DTYPE)).classify(buf, off, lens, 4)
+        assert got.tobytes() == want.tobytes()
+        tx = store.copy()
+        R._check(R._tx_cksum(ctx._h, tx.ctypes.data, span, off.ctypes.data, lens.ctypes.data,
+                             len(off), 4), "rxg_tx_cksum")
+        assert np.all(tx[span:] == 0xEE), "TX copy back wrote past the burst"
+        assert np.array_equal(tx[:span], O.tx_cksum(buf, off, lens, 4)[:span])

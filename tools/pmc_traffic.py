@@ -24,9 +24,9 @@ def collect(workload, counter, outdir):
     d = os.path.join(outdir, f"pmc_{workload}_{counter}")
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "3",
-           "--warmup", "1", "--no-cpu"]
+           "--warmup", "1", "--no-cpu", "--no-cfg1", "--parity-sample", "0"]
     env = dict(os.environ, TMPDIR="/tmp")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     if r.returncode != 0:
         sys.stderr.write(r.stdout[-3000:] + r.stderr[-3000:])
         raise SystemExit(r.returncode)
@@ -46,7 +46,11 @@ def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     wls = (sys.argv[2] if len(sys.argv) > 2 else "cfg2,cfg3").split(",")
     outdir = os.path.join(ROOT, "gpurun_out")
-    res = {"tag": tag, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+    import hashlib
+    sha = hashlib.sha256(open(os.path.join(ROOT, "dpdk-tcp-udp_protocol_stack_amd", "librxgpu.so"),
+                              "rb").read()).hexdigest()
+    # bench.py publishes roofline.traffic only from a summary of the same library
+    res = {"tag": tag, "librxgpu_sha256": sha, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
            "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per rx_classify_kernel dispatch "
            "(median over dispatches)", "workloads": {}}
     for w in wls:
