@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "rx_common.h"
@@ -150,6 +151,30 @@ static void build_udpc(const ft_host &u, uint32_t nu, std::vector<uint2> *out, u
     }
 }
 
+// UDP direct port table (rx_common.h): the address most sockets are bound to
+// gets a u32[65536] entry per port (flow id, or RX_PORT_NONE); a port that also
+// has a socket on another address is flagged RX_PORT_HASHED, and lookups for
+// those other addresses probe the hashed table, which holds every key.
+static uint32_t build_udp_port(const ft_host &u, std::vector<uint32_t> *port) {
+    std::unordered_map<uint32_t, uint32_t> dips; // dip -> sockets bound to it
+    for (uint32_t i = 0; i + 1 < u.slots.size(); ++i)
+        if (u.slots[i].w != RX_SLOT_EMPTY) ++dips[u.slots[i].x];
+    uint32_t dip = 0, best = 0;
+    for (const auto &d : dips)
+        if (d.second > best || (d.second == best && d.first < dip)) best = d.second, dip = d.first;
+    port->assign(65536, RX_PORT_NONE);
+    for (uint32_t i = 0; i + 1 < u.slots.size(); ++i) { // (the last slot mirrors slot 0)
+        const uint4 &sl = u.slots[i];
+        if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> newest flow
+        uint32_t &e = (*port)[sl.y & 0xFFFFu];
+        if (sl.x == dip)
+            e = (e & RX_PORT_HASHED) | sl.w;
+        else
+            e |= RX_PORT_HASHED;
+    }
+    return dip;
+}
+
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -162,6 +187,10 @@ struct rxg_ctx {
     uint2 *d_udpc = nullptr;
     size_t d_udp_cap = 0, d_tcp_cap = 0, d_udpc_cap = 0;
     uint32_t *d_listen = nullptr;
+    std::vector<uint32_t> h_udp_port; // UDP direct port table (empty: not built)
+    uint32_t udp_dip = 0;
+    uint32_t *d_udp_port = nullptr;
+    uint32_t tune_tables = 0; // rxg_tune_tables flags
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
@@ -311,6 +340,7 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_udp);
     (void)hipFree(c->d_tcp);
     (void)hipFree(c->d_listen);
+    (void)hipFree(c->d_udp_port);
     (void)hipFree(c->d_counts);
     (void)hipFree(c->d_ws);
     (void)hipFree(c->d_aux);
@@ -351,6 +381,9 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
     c->h_udp.build(ue, c->ft_load_log2);
     c->h_tcp.build(te, c->ft_load_log2);
     build_udpc(c->h_udp, nu, &c->h_udpc, &c->udpc_probe);
+    c->h_udp_port.clear();
+    if (!ue.empty() && !(c->tune_tables & RXG_TT_NO_UDP_PORT))
+        c->udp_dip = build_udp_port(c->h_udp, &c->h_udp_port);
     c->h_listen.assign(65536, RXG_FLOW_NONE);
     for (uint32_t i = 0; i < nt; ++i)
         if (t[i].status == RXG_TCP_STATUS_LISTEN) c->h_listen[t[i].dport] = i;
@@ -382,6 +415,14 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
         c->ft.udpc = c->d_udpc;
         c->ft.udpc_mask = (uint32_t)c->h_udpc.size() - 1;
         c->ft.udpc_probe = c->udpc_probe;
+    }
+    c->ft.udp_port = nullptr;
+    if (!c->h_udp_port.empty()) {
+        if (!c->d_udp_port) HIPCHK(hipMalloc(&c->d_udp_port, 65536 * sizeof(uint32_t)));
+        HIPCHK(hipMemcpy(c->d_udp_port, c->h_udp_port.data(), 65536 * sizeof(uint32_t),
+                         hipMemcpyHostToDevice));
+        c->ft.udp_port = c->d_udp_port;
+        c->ft.udp_dip = c->udp_dip;
     }
     c->ft.udp = c->d_udp;
     c->ft.tcp = c->d_tcp;
@@ -437,6 +478,12 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
     return RXG_OK;
 }
 
+int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
+    if (!c || (flags & ~(uint32_t)RXG_TT_NO_UDP_PORT)) return RXG_EINVAL;
+    c->tune_tables = flags;
+    return RXG_OK;
+}
+
 int rxg_tune_flow_load(rxg_ctx *c, uint32_t load_log2) {
     if (!c || load_log2 > 4) return RXG_EINVAL;
     c->ft_load_log2 = load_log2 ? load_log2 : RX_FT_LOAD_LOG2;
@@ -446,7 +493,11 @@ int rxg_tune_flow_load(rxg_ctx *c, uint32_t load_log2) {
 uint32_t rxg_num_flows(const rxg_ctx *c) { return c ? c->ft.nu + c->ft.nt : 0; }
 
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *c, uint32_t dip, uint16_t dport) {
-    return c ? c->h_udp.lookup(dip, dport, 17u) : RXG_FLOW_NONE;
+    if (!c) return RXG_FLOW_NONE;
+    uint32_t f;
+    if (!c->h_udp_port.empty() && rx_udp_port_decide(c->h_udp_port[dport], dip, c->udp_dip, &f))
+        return f;
+    return c->h_udp.lookup(dip, dport, 17u);
 }
 
 uint32_t rxg_ft_lookup_tcp(const rxg_ctx *c, uint32_t sip, uint32_t dip, uint16_t sport,

@@ -39,6 +39,8 @@
 //   the 4 slots of a bucket in one coalesced access and __ballot the compare.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rx_common.h"
 #include "rx_device.h"
 
@@ -263,11 +265,16 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
     for (int f = 0; f < FPG; ++f) {
         probe[f] = S.valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
         const bool udp = cls[f] == RXG_CLS_UDP;
+        flow[f] = RXG_FLOW_NONE;
+        // UDP through the direct port table (one entry, the same for the whole
+        // group); only keys it cannot decide go on to the hashed probe
+        if (probe[f] && udp && ft.udp_port &&
+            rx_udp_port_decide(ft.udp_port[dport[f]], ka[f], ft.udp_dip, &flow[f]))
+            probe[f] = false;
         const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
         slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
         sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
         if (probe[f] && gl < RX_WINDOW) sl[f] = ld_slot((udp ? ft.udp : ft.tcp) + ((slot[f] + gl) & mask));
-        flow[f] = RXG_FLOW_NONE;
     }
 #pragma unroll
     for (int f = 0; f < FPG; ++f) {
@@ -295,7 +302,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             s = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
             if (gl < RX_WINDOW) s = ld_slot(tbl + ((b + gl) & mask));
         }
-        if (probe[f] && cls[f] == RXG_CLS_TCP && flow[f] == RXG_FLOW_NONE)
+        if (S.valid[f] && cls[f] == RXG_CLS_TCP && ok[f] && flow[f] == RXG_FLOW_NONE)
             flow[f] = ft.listen[dport[f]];
     }
 
@@ -329,13 +336,15 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
             v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
             stg16(&out[S.pf[f]], v);
-            if (counts && rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE) {
-                const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
+            const bool counted = rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE;
+            const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
+            if (counts && counted) {
                 if (lds_bins)
                     atomicAdd(&hist[idx], 1u);
                 else
                     atomicAdd(&counts[idx], 1ull);
             }
+            if (ft.count_idx) ft.count_idx[S.pf[f]] = counted ? idx : 0xFFFFFFFFu;
         }
     }
 }
@@ -590,7 +599,9 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
         const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
         const uint4 *tbl = is_udp ? ft.udp : ft.tcp;
         const uint32_t mask = is_udp ? ft.udp_mask : ft.tcp_mask;
-        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        if (is_udp && ft.udp_port && rx_udp_port_decide(ft.udp_port[dport], dip, ft.udp_dip, &flow))
+            maxp = 0; // decided by the direct port table
         uint32_t i = rx_hash3(ka, kb, kc) & mask;
         for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) { // ~1.2 trips expected
             const uint4 sl = ld_slot(tbl + i);
@@ -666,6 +677,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         else
             lane_store<ST_NT>(out, L.p, v);
         lane_count(idx, counts, hist, lds_bins);
+        if (ft.count_idx) ft.count_idx[L.p] = idx;
     }
 }
 
@@ -721,6 +733,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             pend_p = L.p;
             pend_valid = L.valid;
             lane_count(idx, counts, hist, lds_bins);
+            if (ft.count_idx && L.valid) ft.count_idx[L.p] = idx;
             L.p = np;
             L.valid = nvalid;
             L.fb = pkts + ((uint64_t)noff << unit_log2);
@@ -1071,12 +1084,21 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
     const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
     const bool probe0 = probe && maxp > 0 && !(ABL & 1);
-    const uint4 *sp0 = probe0 ? (is_udp ? ft.udp : ft.tcp) +
-                                    (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
-                              : reinterpret_cast<const uint4 *>(fb);
+    // the port entry, loaded with the head: UDP's direct port table entry
+    // (which decides most UDP keys without the hashed table), TCP's listener
+    // (tcp_stream_search pass 2, used on an exact-key miss)
+    const bool udp_port = is_udp && ft.udp_port != nullptr;
+    const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+    const uint32_t pe = ptab[l4 ? dport : 0u];
+    // and the hashed table's home slot (not needed by a port-decided UDP key:
+    // a dummy load of the frame's own head then)
+    const bool hash0 = probe0 && !udp_port;
+    const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
+                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                             : reinterpret_cast<const uint4 *>(fb);
     const uint4 sl0 = ld_slot(sp0);
     uint4 sl1 = sl0;
-    if constexpr (PW == 2) sl1 = ld_slot(sp0 + (probe0 ? 1 : 0));
+    if constexpr (PW == 2) sl1 = ld_slot(sp0 + (hash0 ? 1 : 0));
 
     uint4 h1 = c[1], h2 = c[2], h3 = c[3];
     h1.x = 0;
@@ -1137,14 +1159,16 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     uint32_t flow = RXG_FLOW_NONE;
     int32_t rc = RXG_RC_KNI;
     auto probe_flow = [&]() {
-        if (probe0) {
+        bool hashed = probe0;
+        if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
+        if (hashed) {
             // slot index and table recomputed from the keys (HO = 2 keeps only
             // the keys and the first slot live across the stream)
             const uint4 *tb = is_udp ? ft.udp : ft.tcp;
             const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
             const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
             uint32_t pj = rx_hash3(ka, kb, kc) & mk;
-            uint4 sl = sl0;
+            uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
             for (uint32_t pr = 0;;) {
                 if (sl.w == RX_SLOT_EMPTY) break;
                 if (sl.x == ka && sl.y == kb && sl.z == kc) {
@@ -1154,7 +1178,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 if (++pr >= mp) break;
                 pj = (pj + 1) & mk;
                 if constexpr (PW == 2) {
-                    if (pr == 1) {
+                    if (pr == 1 && hash0) {
                         sl = sl1;
                         continue;
                     }
@@ -1163,7 +1187,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             }
         }
         if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
-        if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = ft.listen[kc >> 16];
+        if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
         if (is_udp)
             rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
                                        : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
@@ -1270,8 +1294,10 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
         vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
         stg16(&out[p], vd);
-        if (rc == RXG_RC_OK && flow != RXG_FLOW_NONE)
-            lane_count((is_tcp ? ft.nu : 0u) + flow, counts, hist, lds_bins);
+        const uint32_t cidx =
+            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+        lane_count(cidx, counts, hist, lds_bins);
+        if (ft.count_idx) ft.count_idx[p] = cidx;
     }
     if (lds_bins) {
         __syncthreads();
@@ -1296,98 +1322,135 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 }
 
 // ---------------------------------------------------------------------------
-// Per-flow counts for 8192 < flows <= 65536 (too many for a per-block LDS
+// Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
-// memory-side request): a slab histogram over the stored verdicts.  Pass 1:
-// block b (1024 threads, one per CU: 128 KiB of LDS) adds its <= 65535
-// verdicts into 16-bit LDS bins over all flows (two per dword; a bin cannot
-// carry into its neighbour below 65536 adds) and writes the bins out as slab
-// b.  Pass 2: one thread per bin pair sums the slab column and adds it to
-// counts (each pair owned by one thread: plain read-modify-write).
+// memory-side request): the classify kernel writes one 4-B count index per
+// frame (ft.count_idx), and a slab histogram sums them.  Pass 1: block b
+// (1024 threads, one per CU: 128 KiB of LDS) adds the indices of its <= 65536
+// frames that fall in its 65536-flow range (blockIdx.y) into 16-bit LDS bins,
+// two per dword (lo = even flow, hi = odd), and writes the bins out as slab
+// b.  A bin can only overflow when all 65536 frames of the block are one flow;
+// the block then sees its exact tally of counted frames differ from the sum
+// of its bins, moves that flow's count to one global add and zeroes its word.
+// Pass 2: a thread per 4 bin pairs sums that column over the slabs (16-B
+// loads, 16 waves over the slabs) and adds it to counts.
 constexpr uint32_t SLAB_MAX_FLOWS = 65536;
-constexpr uint32_t SLAB_MIN_FLOWS = 8193; // below: LDS histogram in the classify kernel
+constexpr uint32_t SLAB_MIN_FLOWS = 8193;   // below: LDS histogram in the classify kernel
+constexpr uint32_t SLAB_MAX_FRAMES = 65536; // per slab block (the overflow rule above)
 
-__global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint4 *__restrict__ vd, uint32_t n,
-                                                              uint32_t per, uint32_t nu,
+__global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__restrict__ cidx,
+                                                              uint32_t n, uint32_t per,
                                                               uint32_t words,
-                                                              uint32_t *__restrict__ slab) {
+                                                              uint32_t *__restrict__ slab,
+                                                              unsigned long long *__restrict__ counts) {
     // blockIdx.y = flow range: flows [y * 65536, y * 65536 + 2 * words)
     __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
-    for (uint32_t i = threadIdx.x; i < words; i += 1024) bins[i] = 0;
+    __shared__ uint32_t tally, any, sum;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < words; i += 1024) bins[i] = 0;
+    if (tid == 0) tally = any = sum = 0;
     __syncthreads();
     const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
-    auto count = [&](const uint4 v) {
-        const uint32_t rc = v.z >> 24, cls = (v.z >> 16) & 0xFFu;
-        if (rc == 0u && v.x != RXG_FLOW_NONE && (cls == RXG_CLS_UDP || cls == RXG_CLS_TCP)) {
-            const uint32_t f = (cls == RXG_CLS_TCP ? nu : 0u) + v.x - f0;
-            if (f < 2u * words) atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
+    uint32_t mine = 0, last = 0;
+    auto count = [&](uint32_t x) {
+        const uint32_t f = x - f0; // ~0u and other ranges: f >= 2 * words
+        if (f < 2u * words) {
+            atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
+            ++mine;
+            last = f;
         }
     };
-    // four verdicts in flight per thread; non-temporal: read once per range
-    uint64_t i = b0 + threadIdx.x;
-    for (; i + 3 * 1024 < b1; i += 4 * 1024) {
+    // 16 indices per thread per trip (four 16-B loads in flight); b0 is a
+    // multiple of 4 (per is), so the vector loads are aligned
+    uint64_t i = b0 + 4ull * tid;
+    for (; i + 4 * 3 * 1024 + 3 < b1; i += 4ull * 4 * 1024) {
         uint4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i + u * 1024));
+        for (int u = 0; u < 4; ++u)
+            v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * 4096));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) count(v[u]);
+        for (int u = 0; u < 4; ++u) count(v[u].x), count(v[u].y), count(v[u].z), count(v[u].w);
     }
-    for (; i < b1; i += 1024) count(ldg16<true>(reinterpret_cast<const uint8_t *>(vd + i)));
+    for (; i < b1; i += 4ull * 1024)
+        for (uint64_t k = i; k < i + 4 && k < b1; ++k) count(cidx[k]);
+    if (mine) {
+        atomicAdd(&tally, mine);
+        any = last; // some counted flow of this block (any writer will do)
+    }
     __syncthreads();
+    uint32_t part = 0;
+    for (uint32_t k = tid; k < words; k += 1024) part += (bins[k] & 0xFFFFu) + (bins[k] >> 16);
+    if (part) atomicAdd(&sum, part);
+    __syncthreads();
+    if (sum != tally) { // every counted frame of the block was flow `any`: 65536 adds
+        if (tid == 0) {
+            atomicAdd(&counts[(uint64_t)f0 + any], (unsigned long long)tally);
+            bins[any >> 1] = 0;
+        }
+        __syncthreads();
+    }
     uint32_t *dst = slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words;
-    for (uint32_t k = threadIdx.x; k < words; k += 1024) dst[k] = bins[k];
+    for (uint32_t k = tid; k < words; k += 1024) dst[k] = bins[k];
 }
 
-// block = 64 bin pairs (one per lane) x 16 waves, each wave summing every
-// 16th slab with 8 loads in flight; the 16 partial sums meet in LDS
+// block = 64 lanes x 4 bin pairs (one 16-B column piece per lane) x 16 waves,
+// wave w summing slabs w, w + 16, ... with 4 loads in flight; the 16 partial
+// sums meet in LDS.  words is a multiple of 4 (slab_words).
 __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
                                                                 uint32_t nslabs, uint32_t words,
                                                                 uint32_t nflows,
                                                                 unsigned long long *__restrict__ counts) {
-    __shared__ uint32_t part[2][16][64];
+    __shared__ uint4 part[2][16][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // blockIdx.y = flow range (its slabs, its 65536 counts)
     slab += (uint64_t)blockIdx.y * nslabs * words;
     counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
     nflows -= blockIdx.y * SLAB_MAX_FLOWS;
-    const uint32_t w = blockIdx.x * 64 + lane;
+    const uint32_t w = (blockIdx.x * 64 + lane) * 4; // first of this lane's 4 words
     const uint32_t wc = w < words ? w : 0;
-    uint32_t lo = 0, hi = 0;
+    uint4 lo = make_uint4(0, 0, 0, 0), hi = lo;
+    auto add = [&](uint4 x) {
+        lo.x += x.x & 0xFFFFu, hi.x += x.x >> 16;
+        lo.y += x.y & 0xFFFFu, hi.y += x.y >> 16;
+        lo.z += x.z & 0xFFFFu, hi.z += x.z >> 16;
+        lo.w += x.w & 0xFFFFu, hi.w += x.w >> 16;
+    };
     uint32_t b = wv;
-    for (; b + 16 * 7 < nslabs; b += 16 * 8) {
-        uint32_t x[8];
+    for (; b + 16 * 3 < nslabs; b += 16 * 4) {
+        uint4 x[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = slab[(uint64_t)(b + 16 * u) * words + wc];
+        for (int u = 0; u < 4; ++u)
+            x[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)(b + 16 * u) * words + wc));
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            lo += x[u] & 0xFFFFu;
-            hi += x[u] >> 16;
-        }
+        for (int u = 0; u < 4; ++u) add(x[u]);
     }
-    for (; b < nslabs; b += 16) {
-        const uint32_t x = slab[(uint64_t)b * words + wc];
-        lo += x & 0xFFFFu;
-        hi += x >> 16;
-    }
+    for (; b < nslabs; b += 16)
+        add(ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)b * words + wc)));
     part[0][wv][lane] = lo;
     part[1][wv][lane] = hi;
     __syncthreads();
     if (wv == 0 && w < words) {
-        lo = hi = 0;
+        lo = hi = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            lo += part[0][k][lane];
-            hi += part[1][k][lane];
+            const uint4 a = part[0][k][lane], c = part[1][k][lane];
+            lo.x += a.x, lo.y += a.y, lo.z += a.z, lo.w += a.w;
+            hi.x += c.x, hi.y += c.y, hi.z += c.z, hi.w += c.w;
         }
-        if (lo) counts[2 * w] += lo;
-        if (hi && 2 * w + 1 < nflows) counts[2 * w + 1] += hi;
+        const uint32_t l[4] = {lo.x, lo.y, lo.z, lo.w}, h[4] = {hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t f = 2 * (w + k);
+            if (l[k] && f < nflows) counts[f] += l[k];
+            if (h[k] && f + 1 < nflows) counts[f + 1] += h[k];
+        }
     }
 }
 
 // Flows above 65536: the count is split into ranges of 65536 flows
-// (blockIdx.y), each range's blocks scanning every verdict; up to
+// (blockIdx.y), each range's blocks scanning every index; up to
 // SLAB_MAX_RANGES ranges, beyond that global atomics in the classify kernel.
 constexpr uint32_t SLAB_MAX_RANGES = 32;
 
@@ -1395,27 +1458,21 @@ static uint32_t slab_ranges(const rx_ft_dev &ft) {
     return (ft.nu + ft.nt + SLAB_MAX_FLOWS - 1) / SLAB_MAX_FLOWS;
 }
 
-// 16-bit bin pairs per slab: all flows for one range, a whole range otherwise
+// 16-bit bin pairs per slab (a multiple of 4): all flows for one range, a
+// whole range otherwise
 static uint32_t slab_words(const rx_ft_dev &ft) {
-    return slab_ranges(ft) > 1 ? SLAB_MAX_FLOWS / 2 : (ft.nu + ft.nt + 1) / 2;
+    return slab_ranges(ft) > 1 ? SLAB_MAX_FLOWS / 2 : (((ft.nu + ft.nt + 1) / 2 + 3) & ~3u);
 }
 
-// slab geometry: one range, a multiple of 256 blocks (whole waves of one block
-// per CU); several ranges, as few slabs per range as the 16-bit bins allow;
-// <= 65535 verdicts each
+// slab geometry: one range, enough slabs to fill the CUs (>= 16384 frames
+// each, so the slabs stay small beside the indices); several ranges, as few
+// slabs per range as the 16-bit bins allow; <= 65536 frames per slab and a
+// multiple of 4 (aligned 16-B index loads)
 static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
-    if (nranges > 1) {
-        const uint64_t nb = ((uint64_t)n + 65534) / 65535;
-        *nslabs = (uint32_t)(nb ? nb : 1);
-        *per = (uint32_t)(((uint64_t)n + *nslabs - 1) / *nslabs);
-        if (*per == 0) *per = 1;
-        return;
-    }
-    const uint64_t waves = ((uint64_t)n + 256ull * 65535 - 1) / (256ull * 65535);
-    uint64_t nb = 256 * (waves ? waves : 1);
-    uint64_t pr = ((uint64_t)n + nb - 1) / nb;
-    if (pr == 0) pr = 1;
-    nb = ((uint64_t)n + pr - 1) / pr;
+    uint64_t pr = nranges > 1 ? SLAB_MAX_FRAMES
+                              : std::max<uint64_t>(((uint64_t)n + 255) / 256, 16384);
+    pr = std::min<uint64_t>((pr + 3) & ~3ull, SLAB_MAX_FRAMES);
+    const uint64_t nb = ((uint64_t)n + pr - 1) / pr;
     *nslabs = (uint32_t)(nb ? nb : 1);
     *per = (uint32_t)pr;
 }
@@ -1425,17 +1482,17 @@ static bool use_slab(const rx_ft_dev &ft, bool counts) {
     return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS * SLAB_MAX_RANGES;
 }
 
-static hipError_t launch_count_slab(const uint4 *out, uint32_t n, const rx_ft_dev &ft,
+static hipError_t launch_count_slab(const uint32_t *cidx, uint32_t n, const rx_ft_dev &ft,
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
     slab_geometry(n, nr, &nslabs, &per);
-    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs, nr), dim3(1024), 0, s, out, n, per, ft.nu,
-                       words, slab);
+    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs, nr), dim3(1024), 0, s, cidx, n, per,
+                       words, slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words + 63) / 64, nr), dim3(1024), 0, s, slab,
-                       nslabs, words, nf, counts);
+    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0, s,
+                       slab, nslabs, words, nf, counts);
     return hipGetLastError();
 }
 
@@ -1540,26 +1597,36 @@ void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
 
 // workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
 // frame), then the count slabs
+// workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
+// frame), then the count indices (4 B per frame) and the count slabs
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts) {
     size_t b = (g == 0 && pipe == 20) ? 16 + 8ull * n : 0;
     if (use_slab(ft, counts)) {
         uint32_t nslabs, per;
         slab_geometry(n, slab_ranges(ft), &nslabs, &per);
-        b = ((b + 255) & ~(size_t)255) + (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
+        b = ((b + 255) & ~(size_t)255) + (((size_t)n * 4 + 255) & ~(size_t)255) +
+            (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
     }
     return b;
 }
 
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
-                              uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
+                              uint32_t pipe, const rx_ft_dev &ft_in, uint4 *out,
                               unsigned long long *counts, hipStream_t s, uint32_t *ws) {
     if (n == 0) return hipSuccess;
-    const uint32_t nflows = ft.nu + ft.nt;
-    const bool slab = use_slab(ft, counts != nullptr);
+    const uint32_t nflows = ft_in.nu + ft_in.nt;
+    const bool slab = use_slab(ft_in, counts != nullptr);
+    if (slab && !ws) return hipErrorInvalidValue;
     unsigned long long *kcounts = slab ? nullptr : counts; // slab: counted after classify
     const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
+    // workspace: [binned lists][count indices][slabs]
+    const size_t lists = (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
+    uint32_t *cidx = slab ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists)
+                          : nullptr;
+    rx_ft_dev ft = ft_in;
+    ft.count_idx = cidx;
     hipError_t e = hipErrorInvalidValue;
     if (g == 0 && pipe == 20) { // size-class binned (workspace: 16 B + 8 B per frame)
         e = launch_binned(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, ws);
@@ -1576,9 +1643,6 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
             }
     }
     if (e != hipSuccess || !slab) return e;
-    if (!ws) return hipErrorInvalidValue;
-    const size_t lists = (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
-    return launch_count_slab(out, n, ft, counts,
-                             reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists),
-                             s);
+    uint32_t *slabs = cidx + ((((size_t)n * 4 + 255) & ~(size_t)255) / 4);
+    return launch_count_slab(cidx, n, ft, counts, slabs, s);
 }

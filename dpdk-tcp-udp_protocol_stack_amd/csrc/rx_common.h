@@ -35,7 +35,33 @@ struct rx_ft_dev {
     // by the lane kernel: slot = {dip, dport | flow << 16}, empty = y ~0u
     const uint2 *udpc;
     uint32_t udpc_mask, udpc_probe;
+    // UDP direct port table (null: not built): u32[65536] indexed by the raw
+    // dst port, for sockets bound to udp_dip (the address most sockets share:
+    // the host's own); see rx_udp_port_decide
+    const uint32_t *udp_port;
+    uint32_t udp_dip;
+    // per-launch output, set by rx_classify_launch on its copy: on the slab
+    // count path every kernel writes frame i's count index (UDP flow k -> k,
+    // TCP flow k -> nu + k; 0xFFFFFFFF = not counted) to count_idx[i], which
+    // the slab pass reads instead of the 16-B verdicts; null otherwise
+    uint32_t *count_idx;
 };
+#define RX_PORT_NONE 0x7FFFFFFFu   // udp_port entry: no socket (udp_dip, port)
+#define RX_PORT_HASHED 0x80000000u // some socket on this port is bound to another ip
+
+// UDP lookup (get_hostinfo_fromip_port, common.c:97-108) through the port
+// table entry e = udp_port[dport]: true = decided (*flow set); false = the key
+// must be probed in the hashed table (a socket on this port has another ip)
+RX_HD bool rx_udp_port_decide(uint32_t e, uint32_t dip, uint32_t udp_dip, uint32_t *flow) {
+    if (dip == udp_dip) {
+        const uint32_t f = e & RX_PORT_NONE;
+        *flow = f == RX_PORT_NONE ? RXG_FLOW_NONE : f;
+        return true;
+    }
+    if (e & RX_PORT_HASHED) return false;
+    *flow = RXG_FLOW_NONE;
+    return true;
+}
 #define RX_UDPC_MAX_FLOWS 1024u // load <= 1/2: <= 2048 slots = 16 KiB of LDS
 #define RX_FT_LOAD_LOG2 2u      // exact-key tables: load <= 1/4 by default (rxg_tune_flow_load)
 

@@ -122,6 +122,8 @@ _tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
 _tune_grid = _sig("rxg_tune_grid", _i32, _vp, _u32)
 _tune_tx = _sig("rxg_tune_tx", _i32, _vp, _u32, _u32)
 _tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
+_tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
+TT_NO_UDP_PORT = 0x1
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
@@ -155,7 +157,7 @@ GROUP_ID_BYTES = 128
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum", "rxg_rss_split",
@@ -251,6 +253,11 @@ class Context:
         """exact-key flow tables at load <= 2**-load_log2 from the next
         flows_sync (0 = default); verdicts do not depend on it"""
         _check(_tune_flow_load(self._h, load_log2), "rxg_tune_flow_load")
+
+    def tune_tables(self, flags: int = 0):
+        """flow-table layout flags (TT_*) from the next flows_sync; verdicts do
+        not depend on them"""
+        _check(_tune_tables(self._h, flags), "rxg_tune_tables")
 
     @property
     def num_flows(self) -> int:

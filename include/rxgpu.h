@@ -228,6 +228,12 @@ int rxg_tune_tx(rxg_ctx *ctx, uint32_t variant, uint32_t blocks_per_cu);
  * and probe length do. */
 int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
 
+/* Tuning hook: flow-table layout flags, applied by the next rxg_flows_sync
+ * (0 = the default layout).  RXG_TT_NO_UDP_PORT: no direct UDP port table;
+ * every UDP lookup probes the hashed table.  Verdicts do not depend on it. */
+#define RXG_TT_NO_UDP_PORT 0x1u
+int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
+
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);

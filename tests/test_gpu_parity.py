@@ -159,17 +159,32 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
 
 
+@pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
-@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (8, 2, 2, 0),
-                                     (1, 4, 1, 0), (4, 1, 2, 0)])
-def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2):
-    """verdicts and counts do not depend on the flow-table load factor
-    (rxg_tune_flow_load): longer probe chains at <= 1/2, sparse tables at <= 1/16"""
+@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
+                                     (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
+def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
+    """verdicts and counts do not depend on the flow-table layout: load factor
+    (rxg_tune_flow_load: longer probe chains at <= 1/2, sparse tables at
+    <= 1/16) and the direct UDP port table (rxg_tune_tables), with sockets on
+    two addresses sharing ports (port-table entries flagged for the hashed
+    probe)"""
     cfg = rxdist.gen_cfg("cfg4", n_udp=3000, n_tcp=3000)
     pk, off, ln = R.gen_host(cfg, 11, 6000, 6)
     udp, tcb = R.gen_flows(cfg)
+    # a second address binds every 7th port too (newest wins for its own key)
+    extra = udp[::7].copy()
+    extra["localip"] = R.ip_raw("10.9.9.9")
+    udp = np.concatenate([udp, extra])
+    pk = pk.copy()  # every third UDP frame addressed to the second address
+    other = np.frombuffer(bytes([10, 9, 9, 9]), np.uint8)
+    for k in range(0, len(off), 3):
+        b = int(off[k]) << 6
+        if pk[b + 12] == 8 and pk[b + 13] == 0 and pk[b + 23] == 17:
+            pk[b + 30:b + 34] = other
     want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
     ctx.tune_flow_load(load_log2)
+    ctx.tune_tables(tables)
     ctx.tune(*variant)
     try:
         ctx.flows_sync(udp, tcb)
@@ -177,6 +192,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2):
     finally:
         ctx.tune(0)
         ctx.tune_flow_load(0)
+        ctx.tune_tables(0)
     assert got.tobytes() == want.tobytes(), (variant, load_log2, _mismatch_report(got, want))
     assert np.array_equal(cnt, wcnt)
 
@@ -428,3 +444,32 @@ def test_unknown_variant_fails_loudly(ctx, torch_dev):
         ctx.tune(0)
     got = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0)
     assert got.tobytes() == O.Tables(udp, tcb).classify(pk, off, ln, 6).tobytes()
+
+
+@pytest.mark.parametrize("target", [4000, 4001])
+def test_count_slab_bin_overflow(ctx, torch_dev, target):
+    """the slab count's 16-bit bins overflow only when every frame of a
+    65536-frame slab is one flow: 70000 UDP sockets (two count ranges, slabs
+    of 65536 frames), 140000 copies of one datagram to socket `target` (even
+    and odd flow: the low and the high bin of a pair) — counts stay exact"""
+    torch, dev = torch_dev
+    nu = 70000
+    udp = np.zeros(nu, R.UDP_SOCK_DTYPE)
+    ips = 0x0A000000 + np.arange(nu) // 1000  # 10.0.0.0 + k / 1000, ports 20000 + k % 1000
+    udp["localip"] = np.array([int.from_bytes(int(x).to_bytes(4, "big"), "little") for x in ips],
+                              np.uint32)
+    udp["localport"] = [R.port_raw(20000 + k % 1000) for k in range(nu)]
+    udp["protocol"] = 17
+    ip = ".".join(str(b) for b in (0x0A000000 + target // 1000).to_bytes(4, "big"))
+    f = F.udp_frame("10.1.2.3", 5555, ip, 20000 + target % 1000, b"z" * 20)
+    n = 140000
+    buf, off, lens = F.pack_frames([f], 6)
+    pk = np.tile(buf[:64], n)
+    off = np.arange(n, dtype=np.uint32)
+    lens = np.full(n, len(f), np.uint16)
+    ctx.flows_sync(udp, None)
+    got, cnt = _dev_classify(torch_dev, ctx, pk, off, lens, 6, 64, counts=True)
+    assert np.all(got["rc"] == 0) and np.all(got["flow_id"] == target)
+    want = np.zeros(nu, np.uint64)
+    want[target] = n
+    assert np.array_equal(cnt, want)

@@ -74,16 +74,19 @@ def _random_flows(rng, nu, nt, dup_frac=0.1):
     return udp, tcb
 
 
+@pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [0, 1, 4])
 @pytest.mark.parametrize("nu,nt", [(0, 0), (1, 1), (1024, 4097), (5000, 300), (20000, 65536)])
-def test_flow_table_matches_list_scan(nu, nt, load_log2):
+def test_flow_table_matches_list_scan(nu, nt, load_log2, tables):
     """the hash tables (at every load factor rxg_tune_flow_load allows to be
-    set) answer like the reference's first-match list scans"""
+    set, with and without the direct UDP port table) answer like the
+    reference's first-match list scans"""
     rng = np.random.default_rng(nu * 7 + nt)
     udp, tcb = _random_flows(rng, nu, nt)
     ora = O.Tables(udp, tcb)
     with R.Context(R.HOST_ONLY) as c:
         c.tune_flow_load(load_log2)
+        c.tune_tables(tables)
         c.flows_sync(udp, tcb)
         assert c.num_flows == nu + nt
         qs = 3000

@@ -20,6 +20,9 @@ step() { # name timeout cmd...
 
 step pytest_gpu 420 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -n "${AB:-}" ]; then
+  step ab 400 python tools/ab_tables.py "$AB" ${AB_ROUNDS:-5} || exit $?
+fi
 if [ -n "${SWEEP:-}" ]; then
   step sweep 300 python bench.py --sweep "$SWEEP" --steps 10 --warmup 3 || exit $?
 fi
