@@ -265,12 +265,13 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
     for (int f = 0; f < FPG; ++f) {
         probe[f] = S.valid[f] && (cls[f] == RXG_CLS_UDP || (cls[f] == RXG_CLS_TCP && ok[f]));
         const bool udp = cls[f] == RXG_CLS_UDP;
-        flow[f] = RXG_FLOW_NONE;
         // UDP through the direct port table (one entry, the same for the whole
         // group); only keys it cannot decide go on to the hashed probe
+        uint32_t fd = RXG_FLOW_NONE;
         if (probe[f] && udp && ft.udp_port &&
-            rx_udp_port_decide(ft.udp_port[dport[f]], ka[f], ft.udp_dip, &flow[f]))
+            rx_udp_port_decide(ft.udp_port[dport[f]], ka[f], ft.udp_dip, &fd))
             probe[f] = false;
+        flow[f] = fd;
         const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
         slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
         sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);

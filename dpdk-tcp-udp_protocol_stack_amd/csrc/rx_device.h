@@ -10,14 +10,24 @@
 namespace {
 
 // ---- intra-group broadcast / reduction (group = G aligned lanes) ----------
+// A cross-lane result is pinned by an empty asm: under register pressure the
+// compiler may otherwise REMATERIALISE the DPP / ds_swizzle inside a later
+// divergent region (e.g. the group's lane-0 verdict store), where the source
+// lanes are inactive and the read returns 0 — observed on gfx950 / ROCm 7.2
+// as UDP dgram_len read as 0 by the (8,1,2) variant at the 8-wave register cap.
+__device__ __forceinline__ uint32_t pin(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 template <int G, int K>
 __device__ __forceinline__ uint32_t gbcast(uint32_t x) {
     static_assert(K < G, "lane out of group");
     if constexpr (G == 4) {
-        return __builtin_amdgcn_update_dpp(0u, x, K * 0x55, 0xF, 0xF, false); // quad_perm [K,K,K,K]
+        return pin(__builtin_amdgcn_update_dpp(0u, x, K * 0x55, 0xF, 0xF, false)); // quad_perm [K,K,K,K]
     } else if constexpr (G <= 32) {
         // ds_swizzle bitmask mode: lane' = (lane & and) | or, within 32 lanes
-        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (0x1F & ~(G - 1)) | (K << 5));
+        return pin((uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (0x1F & ~(G - 1)) | (K << 5)));
     } else {
         return __builtin_amdgcn_readlane(x, K);
     }
@@ -31,7 +41,7 @@ __device__ __forceinline__ uint32_t gsum(uint32_t x) {
     if constexpr (G >= 16) x += __builtin_amdgcn_update_dpp(0u, x, 0x140, 0xF, 0xF, false); // row_mirror
     if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 10)); // xor 16
     if constexpr (G == 64) x = __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 32);
-    return x;
+    return pin(x);
 }
 
 typedef unsigned short rx_us2 __attribute__((ext_vector_type(2)));
