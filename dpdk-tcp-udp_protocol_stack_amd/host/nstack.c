@@ -73,6 +73,11 @@ static int ring_peek(struct nring *r, void **p) {
     *p = r->slot[r->head];
     return 0;
 }
+static int ring_peek_at(struct nring *r, uint32_t k, void **p) {
+    if (k >= r->count) return -ENOENT;
+    *p = r->slot[(r->head + k) % r->cap];
+    return 0;
+}
 static int ring_dequeue(struct nring *r, void **p) {
     if (!r->count) return -ENOENT;
     *p = r->slot[r->head];
@@ -153,6 +158,8 @@ static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
 static rxg_ctx *g_ctx;
 static int g_dirty = 1;
+static uint64_t g_snap_gen; /* generation of the snapshot the flow ids refer to */
+static int g_burst_stale;   /* the burst's verdicts were made for an older snapshot */
 static uint64_t g_stat[5];
 static unsigned int g_isn_seed; /* tcp_stream_create seeds rand_r with time(NULL) (tcp.c:30-31) */
 
@@ -253,6 +260,7 @@ static int snapshot(void) {
     }
     s_nu = nu;
     s_nt = nt;
+    g_snap_gen++; /* flow ids of earlier snapshots may now name other blocks */
     int rc = rxg_flows_sync(g_ctx, s_udp, nu, s_tcb, nt);
     if (rc == RXG_OK) g_dirty = 0;
     return rc;
@@ -834,7 +842,7 @@ static int deliver_tcp(const rxg_mbuf *m, const rxg_verdict *v) {
     const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
     const uint32_t cap = m->data_len;
     struct tcp_stream *s;
-    if (g_burst_mutated)
+    if (g_burst_mutated || g_burst_stale)
         s = tcb_search(cap >= 30 ? rd32(f + 26) : 0, cap >= 34 ? rd32(f + 30) : 0,
                        cap >= 36 ? rd16(f + 34) : 0, cap >= 38 ? rd16(f + 36) : 0);
     else
@@ -845,17 +853,34 @@ static int deliver_tcp(const rxg_mbuf *m, const rxg_verdict *v) {
     return RXG_RC_OK;
 }
 
-/* udp.c:25-52 for one verdict (g_lock held) */
-static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v) {
+/* get_hostinfo_fromip_port (common.c:97-108) over the live list */
+static struct localhost *udp_search(uint32_t dip, uint16_t dport) {
+    for (struct localhost *h = g_pstHost; h; h = h->next)
+        if (h->localip == dip && h->localport == dport && h->protocol == IPPROTO_UDP) return h;
+    return NULL;
+}
+
+/* udp.c:25-52 for one verdict (g_lock held).  A verdict made for an older
+ * snapshot (g_burst_stale) is looked up again on the live list: its flow id
+ * may name another socket once one has been closed. */
+static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v, int *rc) {
     if (v->cls == RXG_CLS_TCP) return 0;
     if (v->cls != RXG_CLS_UDP) {
         g_stat[3]++;
         return 0;
     }
-    if (v->rc != RXG_RC_OK || v->flow_id >= s_nu) return 0;
-    struct localhost *h = s_udp_cb[v->flow_id];
     const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
     const uint32_t cap = m->data_len;
+    struct localhost *h;
+    if (g_burst_stale) {
+        h = udp_search(cap >= 34 ? rd32(f + 30) : 0, cap >= 38 ? rd16(f + 36) : 0);
+        *rc = !h ? RXG_RC_UDP_NO_SOCKET
+                 : ((v->flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        if (*rc != RXG_RC_OK) return 0;
+    } else {
+        if (v->rc != RXG_RC_OK || v->flow_id >= s_nu) return 0;
+        h = s_udp_cb[v->flow_id];
+    }
     struct offload *o = calloc(1, sizeof(*o));
     if (!o) return 0;
     o->sip = cap >= 30 ? rd32(f + 26) : 0;
@@ -923,19 +948,24 @@ static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, i
         if (v[i].cls == RXG_CLS_TCP)
             rc = deliver_tcp(m[i], &v[i]);
         else
-            delivered += deliver_one(m[i], &v[i]);
+            delivered += deliver_one(m[i], &v[i], &rc);
         if (rc_out) rc_out[i] = rc;
     }
+    g_burst_stale = 0;
     return delivered;
 }
 
-int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out) {
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
+                   int *rc_out) {
     if (!m || !v) return n ? RXG_EINVAL : 0;
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && g_dirty) rc = snapshot();
     int delivered = 0;
-    if (rc == RXG_OK) delivered = deliver_burst(m, n, v, rc_out);
+    if (rc == RXG_OK) {
+        g_burst_stale = gen != g_snap_gen; /* classified against another snapshot */
+        delivered = deliver_burst(m, n, v, rc_out);
+    }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
 }
@@ -957,6 +987,52 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     return rc == RXG_OK ? delivered : rc;
 }
 
+int nstack_tcb_state(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int32_t *status,
+                     uint32_t *rcv_nxt, uint32_t *snd_nxt, int32_t *fd) {
+    pthread_mutex_lock(&g_lock);
+    int rc = -1;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
+        if (s->sip == sip && s->dip == dip && s->sport == sport && s->dport == dport) {
+            if (status) *status = (int32_t)s->status;
+            if (rcv_nxt) *rcv_nxt = s->rcv_nxt;
+            if (snd_nxt) *snd_nxt = s->snd_nxt;
+            if (fd) *fd = s->fd;
+            rc = 0;
+            break;
+        }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+int nstack_tcb_sndq(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, uint32_t k,
+                    uint8_t *flags, uint32_t *acknum) {
+    pthread_mutex_lock(&g_lock);
+    int rc = -1;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
+        if (s->sip == sip && s->dip == dip && s->sport == sport && s->dport == dport) {
+            pthread_mutex_lock(&s->mutex);
+            void *p = NULL;
+            if (ring_peek_at(s->sndbuf, k, &p) == 0) {
+                const struct tcp_fragment *f = p;
+                if (flags) *flags = f->tcp_flags;
+                if (acknum) *acknum = f->acknum;
+                rc = 0;
+            }
+            pthread_mutex_unlock(&s->mutex);
+            break;
+        }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+uint32_t nstack_tcb_count(void) {
+    pthread_mutex_lock(&g_lock);
+    uint32_t n = 0;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) n++;
+    pthread_mutex_unlock(&g_lock);
+    return n;
+}
+
 int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status) {
     pthread_mutex_lock(&g_lock);
     struct tcp_stream *s = tcb_new(sip, dip, sport, dport, status);
@@ -972,13 +1048,14 @@ int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, i
 }
 
 int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
-                 uint32_t *nt) {
+                 uint32_t *nt, uint64_t *gen) {
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && g_dirty) rc = snapshot();
     if (rc == RXG_OK) {
         if (nu) *nu = s_nu;
         if (nt) *nt = s_nt;
+        if (gen) *gen = g_snap_gen;
         if (u) memcpy(u, s_udp, (size_t)(s_nu < cap_u ? s_nu : cap_u) * sizeof(*u));
         if (t) memcpy(t, s_tcb, (size_t)(s_nt < cap_t ? s_nt : cap_t) * sizeof(*t));
     }

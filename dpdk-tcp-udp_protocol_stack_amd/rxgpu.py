@@ -526,9 +526,12 @@ class NStack:
                    ("nsendto", ssz, [_i32, _vp, C.c_size_t, _i32, _vp, _u32]),
                    ("nclose", _i32, [_i32]),
                    ("nstack_rx_burst", _i32, [_vp, _u32, _vp, _vp]),
-                   ("nstack_deliver", _i32, [_vp, _u32, _vp, _vp]),
+                   ("nstack_deliver", _i32, [_vp, _u32, _vp, _u64, _vp]),
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
-                   ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp]),
+                   ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
+                   ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
+                   ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
+                   ("nstack_tcb_count", _u32, []),
                    ("nstack_stat", _u64, [_i32]),
                    ("nstack_set_local", _i32, [_u32, _vp]),
                    ("nstack_arp_insert", _i32, [_u32, _vp]),
@@ -567,10 +570,12 @@ class NStack:
         r = self.lib.nrecvfrom(fd, buf, n, flags, C.byref(a), C.byref(al))
         return r, buf.raw[:max(r, 0)], a
 
-    def recv(self, fd, n, flags=MSG_DONTWAIT):
+    def recv(self, fd, n, flags=MSG_DONTWAIT, full=False):
+        """(return value, bytes); full=True: the whole n-byte buffer (a split
+        read returns the remaining length, common.c:493, after copying n bytes)"""
         buf = C.create_string_buffer(max(n, 1))
         r = self.lib.nrecv(fd, buf, n, flags)
-        return r, buf.raw[:max(r, 0)]
+        return r, (buf.raw[:n] if full else buf.raw[:max(r, 0)])
 
     def sendto(self, fd, data: bytes, ip, port):
         a = sockaddr(ip, port)
@@ -586,14 +591,37 @@ class NStack:
         return self.lib.nstack_tcb_add(ip_raw(sip), ip_raw(dip), port_raw(sport),
                                        port_raw(dport), status)
 
-    def flows(self):
-        nu, nt = C.c_uint32(), C.c_uint32()
-        _check(self.lib.nstack_flows(None, 0, C.byref(nu), None, 0, C.byref(nt)), "nstack_flows")
+    def flows(self, with_gen: bool = False):
+        """the snapshot lists (and, with_gen, their generation for deliver)"""
+        nu, nt, gen = C.c_uint32(), C.c_uint32(), _u64()
+        _check(self.lib.nstack_flows(None, 0, C.byref(nu), None, 0, C.byref(nt), None),
+               "nstack_flows")
         u = np.zeros(nu.value, UDP_SOCK_DTYPE)
         t = np.zeros(nt.value, TCB_DTYPE)
         _check(self.lib.nstack_flows(_ptr(u) if len(u) else None, len(u), None,
-                                     _ptr(t) if len(t) else None, len(t), None), "nstack_flows")
-        return u, t
+                                     _ptr(t) if len(t) else None, len(t), None, C.byref(gen)),
+               "nstack_flows")
+        return (u, t, gen.value) if with_gen else (u, t)
+
+    def tcb_state(self, sip, dip, sport, dport):
+        """(status, rcv_nxt, snd_nxt, fd) of the tcb with this raw 4-tuple, or None"""
+        st, rn, sn, fd = C.c_int32(), C.c_uint32(), C.c_uint32(), C.c_int32()
+        if self.lib.nstack_tcb_state(sip, dip, sport, dport, C.byref(st), C.byref(rn),
+                                     C.byref(sn), C.byref(fd)):
+            return None
+        return st.value, rn.value, sn.value, fd.value
+
+    def tcb_sndq(self, sip, dip, sport, dport):
+        """[(tcp_flags, acknum)] queued in the tcb's send ring, oldest first"""
+        out, k = [], 0
+        fl, ack = C.c_uint8(), C.c_uint32()
+        while self.lib.nstack_tcb_sndq(sip, dip, sport, dport, k, C.byref(fl), C.byref(ack)) == 0:
+            out.append((fl.value, ack.value))
+            k += 1
+        return out
+
+    def tcb_count(self):
+        return self.lib.nstack_tcb_count()
 
     @staticmethod
     def mbufs(frames: list[bytes]):
@@ -607,11 +635,15 @@ class NStack:
         arr = (C.POINTER(Mbuf) * len(ms))(*[C.pointer(m) for m in ms])
         return arr, (bufs, ms)
 
-    def deliver(self, frames: list[bytes], verdicts: np.ndarray, rcs: np.ndarray | None = None) -> int:
-        """apply verdicts; rcs (int32[n], optional) receives the per-frame return codes"""
+    def deliver(self, frames: list[bytes], verdicts: np.ndarray, rcs: np.ndarray | None = None,
+                gen: int | None = None) -> int:
+        """apply verdicts made for the snapshot of generation `gen` (None = the
+        current one); rcs (int32[n], optional) receives the per-frame return codes"""
+        if gen is None:
+            gen = self.flows(with_gen=True)[2]
         arr, keep = self.mbufs(frames)
         verdicts = np.ascontiguousarray(verdicts, VERDICT_DTYPE)
-        r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts), _ptr(rcs))
+        r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts), gen, _ptr(rcs))
         if r < 0:
             _check(r, "nstack_deliver")
         return r

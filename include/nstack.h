@@ -71,19 +71,35 @@ int nclose(int fd);
  * Returns the number of UDP datagrams delivered, or a negative RXG_E* code. */
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 
-/* Delivery half only: apply verdicts computed by rxg_* for the current
- * control-block snapshot to the frames (UDP -> socket receive rings, TCP ->
- * state machine).  rc_out (nullable) as for nstack_rx_burst. */
-int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out);
+/* Delivery half only: apply verdicts computed by rxg_* to the frames (UDP ->
+ * socket receive rings, TCP -> state machine).  `gen` = the snapshot
+ * generation nstack_flows returned with the lists the verdicts were
+ * classified against: if the lists changed since (a socket or tcb closed,
+ * which renumbers later blocks), every frame of the burst is looked up again
+ * on the live lists, as the reference's per-frame lookups would, instead of
+ * trusting stale flow ids.  rc_out (nullable) as for nstack_rx_burst. */
+int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
+                   int *rc_out);
 
 /* Install a tcb as tcp_stream_create + LL_ADD do on a SYN (tcp.c:3-52) and
  * wake a blocked naccept (tcp.c:108-116).  All values raw network order. */
 int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status);
 
 /* The current control-block snapshot in creation order (what rxg_flows_sync
- * receives).  Counts are always written; arrays up to their capacities. */
+ * receives) and its generation (nullable; for nstack_deliver).  Counts are
+ * always written; arrays up to their capacities. */
 int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
-                 uint32_t *nt);
+                 uint32_t *nt, uint64_t *gen);
+
+/* Diagnostics (tests): the tcb with this exact 4-tuple (raw network order):
+ * status, rcv_nxt, snd_nxt, fd; and the k-th fragment queued in its send
+ * ring (TCP flags, acknum).  0 = found, -1 = none.  nstack_tcb_count = tcbs
+ * in the list (listeners included). */
+int nstack_tcb_state(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int32_t *status,
+                     uint32_t *rcv_nxt, uint32_t *snd_nxt, int32_t *fd);
+int nstack_tcb_sndq(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, uint32_t k,
+                    uint8_t *flags, uint32_t *acknum);
+uint32_t nstack_tcb_count(void);
 
 /* ---- TX (the udp_out / tcp_out pass of the protocol loop, netfamily.c:205-206)
  * Local identity: gLocalIp (netfamily.c:11) and the port MAC g_stCpuMac

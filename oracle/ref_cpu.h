@@ -48,6 +48,28 @@ void oracle_tx_cksum(uint8_t *pkts, const uint32_t *off, const uint16_t *len, ui
 /* Toeplitz RSS (same definition as rxg_rss_hash, written independently) */
 uint32_t oracle_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
 
+/* ---- delivery half (ref_stack.c): the socket layer and the per-frame
+ * udp_process / tcp_process effects, in the reference's list shapes.
+ * Blocking calls return -2 where the reference would wait. */
+typedef struct oracle_stack oracle_stack;
+oracle_stack *oracle_stack_new(void);
+void oracle_stack_free(oracle_stack *st);
+int oracle_nsocket(oracle_stack *st, int type); /* 1 SOCK_STREAM, 2 SOCK_DGRAM */
+int oracle_nbind(oracle_stack *st, int fd, uint32_t ip, uint16_t port);
+int oracle_nlisten(oracle_stack *st, int fd);
+int oracle_naccept(oracle_stack *st, int fd, uint32_t *sip, uint16_t *sport);
+int oracle_nclose(oracle_stack *st, int fd);
+int oracle_rx(oracle_stack *st, const uint8_t *frame, uint32_t caplen);
+long oracle_nrecvfrom(oracle_stack *st, int fd, uint8_t *buf, size_t len, uint32_t *sip,
+                      uint16_t *sport);
+long oracle_nrecv(oracle_stack *st, int fd, uint8_t *buf, size_t len);
+int oracle_tcb_state(const oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t sport,
+                     uint16_t dport, int32_t *status, uint32_t *rcv_nxt, uint32_t *snd_nxt,
+                     int32_t *fd);
+int oracle_tcb_sndq(const oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t sport,
+                    uint16_t dport, uint32_t k, uint8_t *flags, uint32_t *acknum);
+uint32_t oracle_tcb_count(const oracle_stack *st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,3 +120,95 @@ def tx_cksum(pkts: np.ndarray, off: np.ndarray, lens: np.ndarray, off_unit_log2:
 
 def rss_hash(sip, dip, sport, dport):
     return lib.oracle_rss_hash(sip, dip, sport, dport)
+
+
+# ---- the delivery half (oracle/ref_stack.c) -------------------------------
+def _stack_sigs(l):
+    vp, u32, u16, i32, sz, lng = C.c_void_p, C.c_uint32, C.c_uint16, C.c_int32, C.c_size_t, C.c_long
+    for name, res, args in [
+            ("oracle_stack_new", vp, []), ("oracle_stack_free", None, [vp]),
+            ("oracle_nsocket", C.c_int, [vp, C.c_int]),
+            ("oracle_nbind", C.c_int, [vp, C.c_int, u32, u16]),
+            ("oracle_nlisten", C.c_int, [vp, C.c_int]),
+            ("oracle_naccept", C.c_int, [vp, C.c_int, vp, vp]),
+            ("oracle_nclose", C.c_int, [vp, C.c_int]),
+            ("oracle_rx", C.c_int, [vp, vp, u32]),
+            ("oracle_nrecvfrom", lng, [vp, C.c_int, vp, sz, vp, vp]),
+            ("oracle_nrecv", lng, [vp, C.c_int, vp, sz]),
+            ("oracle_tcb_state", C.c_int, [vp, u32, u32, u16, u16, vp, vp, vp, vp]),
+            ("oracle_tcb_sndq", C.c_int, [vp, u32, u32, u16, u16, u32, vp, vp]),
+            ("oracle_tcb_count", u32, [vp])]:
+        f = getattr(l, name)
+        f.restype, f.argtypes = res, args
+
+
+_stack_sigs(lib)
+WOULD_BLOCK = -2
+
+
+class Stack:
+    """the reference's socket layer + per-frame udp_process/tcp_process effects
+    (oracle/ref_stack.c); a blocking call returns WOULD_BLOCK (-2)"""
+
+    def __init__(self):
+        self.h = lib.oracle_stack_new()
+
+    def __del__(self):
+        if getattr(self, "h", None) and lib is not None:
+            lib.oracle_stack_free(self.h)
+            self.h = None
+
+    def socket(self, type_):
+        return lib.oracle_nsocket(self.h, type_)
+
+    def bind(self, fd, ip_raw, port_raw):
+        return lib.oracle_nbind(self.h, fd, ip_raw, port_raw)
+
+    def listen(self, fd):
+        return lib.oracle_nlisten(self.h, fd)
+
+    def accept(self, fd):
+        sip, sport = C.c_uint32(), C.c_uint16()
+        r = lib.oracle_naccept(self.h, fd, C.byref(sip), C.byref(sport))
+        return r, sip.value, sport.value
+
+    def close(self, fd):
+        return lib.oracle_nclose(self.h, fd)
+
+    def rx(self, frame: bytes):
+        b = C.create_string_buffer(bytes(frame), len(frame) + 1)
+        return lib.oracle_rx(self.h, b, len(frame))
+
+    def recvfrom(self, fd, n):
+        buf = C.create_string_buffer(max(n, 1))
+        sip, sport = C.c_uint32(), C.c_uint16()
+        r = lib.oracle_nrecvfrom(self.h, fd, buf, n, C.byref(sip), C.byref(sport))
+        return r, buf.raw[:max(r, 0)], sip.value, sport.value
+
+    def recv(self, fd, n):
+        """(return value, the whole n-byte buffer: a split read returns the
+        REMAINING length, common.c:493, after copying n bytes)"""
+        buf = C.create_string_buffer(max(n, 1))
+        r = lib.oracle_nrecv(self.h, fd, buf, n)
+        return r, buf.raw[:n]
+
+    def tcb_state(self, sip, dip, sport, dport):
+        """(status, rcv_nxt, snd_nxt or None while it is the random ISN, fd) or None"""
+        st, rn, sn, fd = C.c_int32(), C.c_uint32(), C.c_uint32(), C.c_int32()
+        r = lib.oracle_tcb_state(self.h, sip, dip, sport, dport, C.byref(st), C.byref(rn),
+                                 C.byref(sn), C.byref(fd))
+        if r < 0:
+            return None
+        return st.value, rn.value, (sn.value if r == 1 else None), fd.value
+
+    def tcb_sndq(self, sip, dip, sport, dport):
+        out, k = [], 0
+        fl, ack = C.c_uint8(), C.c_uint32()
+        while lib.oracle_tcb_sndq(self.h, sip, dip, sport, dport, k, C.byref(fl),
+                                  C.byref(ack)) == 0:
+            out.append((fl.value, ack.value))
+            k += 1
+        return out
+
+    def tcb_count(self):
+        return lib.oracle_tcb_count(self.h)

@@ -22,6 +22,7 @@ def test_host_code_under_asan_ubsan(tmp_path):
            "-g", "-O1"]
     objs = []
     for src, cc, std in [("oracle/ref_cpu.c", "gcc", "-std=gnu11"),
+                         ("oracle/ref_stack.c", "gcc", "-std=gnu11"),
                          ("dpdk-tcp-udp_protocol_stack_amd/host/nstack.c", "gcc", "-std=gnu11"),
                          ("tests/san/san_harness.c", "gcc", "-std=gnu11"),
                          ("dpdk-tcp-udp_protocol_stack_amd/csrc/rx_pcap.cpp", "g++", "-std=c++17")]:
