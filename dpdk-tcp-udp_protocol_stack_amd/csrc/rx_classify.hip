@@ -1327,17 +1327,17 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
 // memory-side request): the classify kernel writes one 4-B count index per
 // frame (ft.count_idx), and a slab histogram sums them.  Pass 1: block b
-// (1024 threads, one per CU: 128 KiB of LDS) adds the indices of its <= 65536
-// frames that fall in its 65536-flow range (blockIdx.y) into 16-bit LDS bins,
-// two per dword (lo = even flow, hi = odd), and writes the bins out as slab
-// b.  A bin can only overflow when all 65536 frames of the block are one flow;
-// the block then sees its exact tally of counted frames differ from the sum
-// of its bins, moves that flow's count to one global add and zeroes its word.
-// Pass 2: a thread per 4 bin pairs sums that column over the slabs (16-B
-// loads, 16 waves over the slabs) and adds it to counts.
+// (1024 threads, one per CU: 128 KiB of LDS) adds the indices of its share of
+// the frames that fall in its 65536-flow range (blockIdx.y) into 16-bit LDS
+// bins, two per dword (lo = even flow, hi = odd), and writes the bins out as
+// slab b.  A bin overflows only when more than 65535 of the block's frames
+// are one flow: the sum of the bins then differs from the block's exact tally
+// of counted frames (each wrap loses 65535 or 65536), and the block zeroes
+// its slab and adds its frames with global atomics instead (pathological
+// traffic only).  Pass 2: a thread per 4 bin pairs sums that column over the
+// slabs (16-B loads) and adds it to counts.
 constexpr uint32_t SLAB_MAX_FLOWS = 65536;
 constexpr uint32_t SLAB_MIN_FLOWS = 8193;   // below: LDS histogram in the classify kernel
-constexpr uint32_t SLAB_MAX_FRAMES = 65536; // per slab block (the overflow rule above)
 
 __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__restrict__ cidx,
                                                               uint32_t n, uint32_t per,
@@ -1346,21 +1346,20 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__r
                                                               unsigned long long *__restrict__ counts) {
     // blockIdx.y = flow range: flows [y * 65536, y * 65536 + 2 * words)
     __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
-    __shared__ uint32_t tally, any, sum;
+    __shared__ uint32_t tally, sum;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < words; i += 1024) bins[i] = 0;
-    if (tid == 0) tally = any = sum = 0;
+    if (tid == 0) tally = sum = 0;
     __syncthreads();
     const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
-    uint32_t mine = 0, last = 0;
+    uint32_t mine = 0;
     auto count = [&](uint32_t x) {
         const uint32_t f = x - f0; // ~0u and other ranges: f >= 2 * words
         if (f < 2u * words) {
             atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
             ++mine;
-            last = f;
         }
     };
     // 16 indices per thread per trip (four 16-B loads in flight); b0 is a
@@ -1376,24 +1375,20 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__r
     }
     for (; i < b1; i += 4ull * 1024)
         for (uint64_t k = i; k < i + 4 && k < b1; ++k) count(cidx[k]);
-    if (mine) {
-        atomicAdd(&tally, mine);
-        any = last; // some counted flow of this block (any writer will do)
-    }
+    if (mine) atomicAdd(&tally, mine);
     __syncthreads();
     uint32_t part = 0;
     for (uint32_t k = tid; k < words; k += 1024) part += (bins[k] & 0xFFFFu) + (bins[k] >> 16);
     if (part) atomicAdd(&sum, part);
     __syncthreads();
-    if (sum != tally) { // every counted frame of the block was flow `any`: 65536 adds
-        if (tid == 0) {
-            atomicAdd(&counts[(uint64_t)f0 + any], (unsigned long long)tally);
-            bins[any >> 1] = 0;
-        }
-        __syncthreads();
-    }
+    const bool wrapped = sum != tally; // block-uniform
     uint32_t *dst = slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words;
-    for (uint32_t k = tid; k < words; k += 1024) dst[k] = bins[k];
+    for (uint32_t k = tid; k < words; k += 1024) dst[k] = wrapped ? 0u : bins[k];
+    if (wrapped)
+        for (uint64_t k = b0 + tid; k < b1; k += 1024) {
+            const uint32_t f = cidx[k] - f0;
+            if (f < 2u * words) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
+        }
 }
 
 // block = 64 lanes x 4 bin pairs (one 16-B column piece per lane) x 16 waves,
@@ -1450,6 +1445,46 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
     }
 }
 
+// few slabs (the multi-range geometry): one thread per 4 bin pairs sums every
+// slab of its range, 8 loads in flight; 256-thread blocks of 1024 pairs
+__global__ __launch_bounds__(256) void rx_count_reduce_few_kernel(
+    const uint32_t *__restrict__ slab, uint32_t nslabs, uint32_t words, uint32_t nflows,
+    unsigned long long *__restrict__ counts) {
+    slab += (uint64_t)blockIdx.y * nslabs * words;
+    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
+    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
+    const uint32_t w = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (w >= words) return;
+    uint32_t l[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0};
+    uint32_t b = 0;
+    for (; b + 8 <= nslabs; b += 8) {
+        uint4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            x[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)(b + u) * words + w));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            l[0] += x[u].x & 0xFFFFu, h[0] += x[u].x >> 16;
+            l[1] += x[u].y & 0xFFFFu, h[1] += x[u].y >> 16;
+            l[2] += x[u].z & 0xFFFFu, h[2] += x[u].z >> 16;
+            l[3] += x[u].w & 0xFFFFu, h[3] += x[u].w >> 16;
+        }
+    }
+    for (; b < nslabs; ++b) {
+        const uint4 x = ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)b * words + w));
+        l[0] += x.x & 0xFFFFu, h[0] += x.x >> 16;
+        l[1] += x.y & 0xFFFFu, h[1] += x.y >> 16;
+        l[2] += x.z & 0xFFFFu, h[2] += x.z >> 16;
+        l[3] += x.w & 0xFFFFu, h[3] += x.w >> 16;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t f = 2 * (w + k);
+        if (l[k] && f < nflows) counts[f] += l[k];
+        if (h[k] && f + 1 < nflows) counts[f + 1] += h[k];
+    }
+}
+
 // Flows above 65536: the count is split into ranges of 65536 flows
 // (blockIdx.y), each range's blocks scanning every index; up to
 // SLAB_MAX_RANGES ranges, beyond that global atomics in the classify kernel.
@@ -1465,14 +1500,13 @@ static uint32_t slab_words(const rx_ft_dev &ft) {
     return slab_ranges(ft) > 1 ? SLAB_MAX_FLOWS / 2 : (((ft.nu + ft.nt + 1) / 2 + 3) & ~3u);
 }
 
-// slab geometry: one range, enough slabs to fill the CUs (>= 16384 frames
-// each, so the slabs stay small beside the indices); several ranges, as few
-// slabs per range as the 16-bit bins allow; <= 65536 frames per slab and a
-// multiple of 4 (aligned 16-B index loads)
+// slab geometry: about one 1024-thread block per CU in all (256 blocks over
+// the ranges), >= 16384 frames per slab so the slabs stay small beside the
+// indices, a multiple of 4 frames (aligned 16-B index loads)
 static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
-    uint64_t pr = nranges > 1 ? SLAB_MAX_FRAMES
-                              : std::max<uint64_t>(((uint64_t)n + 255) / 256, 16384);
-    pr = std::min<uint64_t>((pr + 3) & ~3ull, SLAB_MAX_FRAMES);
+    const uint64_t want = std::max<uint64_t>(1, 256 / nranges);
+    uint64_t pr = std::max<uint64_t>(((uint64_t)n + want - 1) / want, 16384);
+    pr = (pr + 3) & ~3ull;
     const uint64_t nb = ((uint64_t)n + pr - 1) / pr;
     *nslabs = (uint32_t)(nb ? nb : 1);
     *per = (uint32_t)pr;
@@ -1492,8 +1526,12 @@ static hipError_t launch_count_slab(const uint32_t *cidx, uint32_t n, const rx_f
                        words, slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0, s,
-                       slab, nslabs, words, nf, counts);
+    if (nslabs <= 64)
+        hipLaunchKernelGGL(rx_count_reduce_few_kernel, dim3((words / 4 + 255) / 256, nr), dim3(256),
+                           0, s, slab, nslabs, words, nf, counts);
+    else
+        hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0,
+                           s, slab, nslabs, words, nf, counts);
     return hipGetLastError();
 }
 

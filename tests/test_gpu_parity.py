@@ -446,23 +446,23 @@ def test_unknown_variant_fails_loudly(ctx, torch_dev):
     assert got.tobytes() == O.Tables(udp, tcb).classify(pk, off, ln, 6).tobytes()
 
 
+@pytest.mark.parametrize("nu,n", [(70000, 140000), (2000000, 600000)])
 @pytest.mark.parametrize("target", [4000, 4001])
-def test_count_slab_bin_overflow(ctx, torch_dev, target):
-    """the slab count's 16-bit bins overflow only when every frame of a
-    65536-frame slab is one flow: 70000 UDP sockets (two count ranges, slabs
-    of 65536 frames), 140000 copies of one datagram to socket `target` (even
-    and odd flow: the low and the high bin of a pair) — counts stay exact"""
+def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
+    """every frame to one UDP socket (`target`: an even and an odd flow, the
+    low and the high 16-bit bin of a pair): 70000 sockets (two count ranges,
+    no bin reaches 65536) and 2M sockets (32 ranges: slabs of 75000 frames,
+    so the bin wraps and the slab's global-atomic fallback counts) — counts
+    stay exact"""
     torch, dev = torch_dev
-    nu = 70000
     udp = np.zeros(nu, R.UDP_SOCK_DTYPE)
-    ips = 0x0A000000 + np.arange(nu) // 1000  # 10.0.0.0 + k / 1000, ports 20000 + k % 1000
-    udp["localip"] = np.array([int.from_bytes(int(x).to_bytes(4, "big"), "little") for x in ips],
-                              np.uint32)
-    udp["localport"] = [R.port_raw(20000 + k % 1000) for k in range(nu)]
+    ips = (0x0A000000 + np.arange(nu, dtype=np.uint64) // 1000).astype(np.uint32)
+    udp["localip"] = ips.byteswap()  # 10.0.0.0 + k / 1000 in network order
+    ports = (20000 + np.arange(nu) % 1000).astype(np.uint16)
+    udp["localport"] = ports.byteswap()  # ports 20000 + k % 1000
     udp["protocol"] = 17
     ip = ".".join(str(b) for b in (0x0A000000 + target // 1000).to_bytes(4, "big"))
     f = F.udp_frame("10.1.2.3", 5555, ip, 20000 + target % 1000, b"z" * 20)
-    n = 140000
     buf, off, lens = F.pack_frames([f], 6)
     pk = np.tile(buf[:64], n)
     off = np.arange(n, dtype=np.uint32)

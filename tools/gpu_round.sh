@@ -34,6 +34,9 @@ if [ "${PROF:-1}" = 1 ]; then
   step rocprof 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
       -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
 fi
+if [ "${TXPMC:-0}" = 1 ]; then
+  step pmc_tx 400 python tools/pmc_tx.py $TAG || exit $?
+fi
 if [ "${PMC:-0}" = 1 ]; then
   step pmc 600 python tools/pmc_traffic.py $TAG ${PMC_WL:-cfg2,cfg3} || exit $?
 fi
