@@ -20,11 +20,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def collect(workload, counter, outdir):
-    d = os.path.join(outdir, f"pmc_{workload}_{counter}")
+def collect(workload, counter, outdir, variant=""):
+    d = os.path.join(outdir, f"pmc_{workload}_{counter}{'_' + variant.replace(',', '-') if variant else ''}")
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "3",
            "--warmup", "1", "--no-cpu", "--no-cfg1", "--parity-sample", "0"]
+    if variant:  # a forced kernel variant (tuning comparisons)
+        cmd += ["--variant", variant]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     if r.returncode != 0:
@@ -45,6 +47,7 @@ def collect(workload, counter, outdir):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     wls = (sys.argv[2] if len(sys.argv) > 2 else "cfg2,cfg3").split(",")
+    variant = sys.argv[3] if len(sys.argv) > 3 else ""  # e.g. 0,0,0,40
     outdir = os.path.join(ROOT, "gpurun_out")
     import hashlib
     sha = hashlib.sha256(open(os.path.join(ROOT, "dpdk-tcp-udp_protocol_stack_amd", "librxgpu.so"),
@@ -54,8 +57,8 @@ def main():
            "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per rx_classify_kernel dispatch "
            "(median over dispatches)", "workloads": {}}
     for w in wls:
-        fetch, ff = collect(w, "FETCH_SIZE", outdir)
-        write, wf = collect(w, "WRITE_SIZE", outdir)
+        fetch, ff = collect(w, "FETCH_SIZE", outdir, variant)
+        write, wf = collect(w, "WRITE_SIZE", outdir, variant)
         if not fetch["rx_classify"] or not write["rx_classify"]:
             raise SystemExit(f"no rx_classify_kernel rows for {w}: {ff} {wf}")
 
@@ -70,6 +73,8 @@ def main():
             res["workloads"][w]["tx_cksum"] = summary("tx_cksum")
         print(w, res["workloads"][w], flush=True)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    if variant:
+        res["variant"] = variant
     with open(os.path.join(outdir, f"pmc_{tag}.json"), "w") as fh:
         json.dump(res, fh, indent=1)
 

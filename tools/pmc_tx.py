@@ -40,7 +40,7 @@ def main():
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 if row.get("Counter_Name") == "WRITE_SIZE" and "tx_cksum" in row["Kernel_Name"]:
-                    k = row["Kernel_Name"].split("(")[0].replace("void (anonymous namespace)::", "")
+                    k = row["Kernel_Name"].replace("void (anonymous namespace)::", "").split("(")[0]
                     vals[k].append(float(row["Counter_Value"]))
         out = {}
         for k, v in vals.items():
