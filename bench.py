@@ -230,8 +230,8 @@ def pmc_traffic(name, kernel=None):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("librxgpu_sha256") != sha:
-            continue
+        if d.get("librxgpu_sha256") != sha or d.get("variant"):
+            continue  # another library build, or a forced (tuning) kernel variant
         w = d.get("workloads", {}).get(name)
         if w is not None:
             if kernel is not None:

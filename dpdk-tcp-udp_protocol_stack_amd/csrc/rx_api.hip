@@ -448,7 +448,7 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
     if (lanes_per_frame == 0 &&
-        (pipeline == 20 || (pipeline >= 30 && pipeline <= 49) || pipeline == 130)) {
+        (pipeline == 20 || (pipeline >= 30 && pipeline <= 39) || pipeline == 130)) {
         c->tune_g = 0; // size-class binned path (20) / stream kernel (30..39, 130)
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;

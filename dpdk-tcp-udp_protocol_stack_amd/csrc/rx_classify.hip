@@ -1009,12 +1009,7 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
-// NTH: frame heads loaded non-temporal (they are read once and need not stay
-// in L2, which then keeps more flow-table lines), and the tail stream skips
-// the chunks that hold frame heads (a per-block LDS bitmap, spans up to
-// ST_SKIP_CHUNKS) instead of reading them again from memory
-constexpr uint32_t ST_SKIP_CHUNKS = 8192;
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool NTH = false>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1024,15 +1019,12 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16]; // [row j][wave w]
     __shared__ unsigned long long s_lo, s_hi;
     __shared__ uint32_t s_tail;
-    __shared__ uint32_t s_hb[NTH ? ST_SKIP_CHUNKS / 32 : 1]; // head chunks of the span (NTH)
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (tid == 0) {
         s_lo = ~0ull;
         s_hi = 0;
         s_tail = 0;
     }
-    if constexpr (NTH)
-        for (uint32_t i = tid; i < ST_SKIP_CHUNKS / 32; i += 256) s_hb[i] = 0;
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
 
     const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
@@ -1045,7 +1037,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     // ---- head phase -------------------------------------------------------
     uint4 c[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = ldg16<NTH>(fb + (16 * j < cp ? 16 * j : 0));
+    for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
 #pragma unroll
     for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
     const uint32_t et = c[0].w & 0xFFFFu;
@@ -1136,27 +1128,11 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
     // (not streamed: loads of the thread's own frame head, never consumed)
     const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
-    // NTH: mark the span's head chunks (a frame's first 64 B lie in no
-    // frame's tail range, so a skipped chunk changes no prefix difference)
-    const bool skip = NTH && streamed && span <= ST_SKIP_CHUNKS; // block-uniform
-    if constexpr (NTH) {
-        if (skip && valid) {
-            const int64_t rel = (int64_t)(fpos >> 4) - (int64_t)lo;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t r = rel + j;
-                if (r >= 0 && r < (int64_t)span) atomicOr(&s_hb[r >> 5], 1u << (r & 31));
-            }
-        }
-        __syncthreads();
-    }
     auto tile_load = [&](uint4 *v, uint32_t c0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = c0 + j * 256 + tid;
-            bool use = k < span;
-            if constexpr (NTH) use = use && !(skip && ((s_hb[k >> 5] >> (k & 31)) & 1u));
-            v[j] = ldg16<NTS>(sb + ((uint64_t)(use ? k : 0) << 4)); // masked at use
+            v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
         }
     };
     if (part) acc = lane_chunk_sum(acc, pc, ef, e);
@@ -1333,14 +1309,14 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     }
 }
 
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool NTH = false>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, NTH>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -1631,10 +1607,6 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
     // 38/39: pipes 34/30 with one barrier per tail tile (B1)
     {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>}, {0, 1, 1, 39, launch_stream<true, 0, 0, 1, true>},
-    // 40/41: pipes 38/39 with non-temporal heads and the head chunks skipped
-    // in the tail stream (NTH)
-    {0, 1, 1, 40, launch_stream<true, 0, 3, 1, true, true>},
-    {0, 1, 1, 41, launch_stream<true, 0, 0, 1, true, true>},
 };
 
 } // namespace

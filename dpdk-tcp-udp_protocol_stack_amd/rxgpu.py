@@ -62,8 +62,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 30), (0, 0, 0, 31),  # stream kernel
                    (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
-                   (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
-                   (0, 0, 0, 40), (0, 0, 0, 41)]  # + non-temporal heads, head chunks skipped
+                   (0, 0, 0, 38), (0, 0, 0, 39)]  # one barrier per tail tile
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

@@ -200,7 +200,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 @pytest.mark.parametrize("layout", ["packed", "block_shuffled", "scattered", "gapped"])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
-                                     (0, 0, 0, 39), (0, 0, 0, 40), (0, 0, 0, 41), (0, 0, 0, 20),
+                                     (0, 0, 0, 39), (0, 0, 0, 20),
                                      (4, 1, 2, 0)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
