@@ -448,7 +448,7 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
     if (lanes_per_frame == 0 &&
-        (pipeline == 20 || (pipeline >= 30 && pipeline <= 39) || pipeline == 130)) {
+        (pipeline == 20 || (pipeline >= 30 && pipeline <= 49) || pipeline == 130)) {
         c->tune_g = 0; // size-class binned path (20) / stream kernel (30..39, 130)
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;
@@ -479,8 +479,9 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)RXG_TT_NO_UDP_PORT)) return RXG_EINVAL;
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B))) return RXG_EINVAL;
     c->tune_tables = flags;
+    c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
     return RXG_OK;
 }
 

@@ -345,7 +345,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
                 else
                     atomicAdd(&counts[idx], 1ull);
             }
-            if (ft.count_idx) ft.count_idx[S.pf[f]] = counted ? idx : 0xFFFFFFFFu;
+            if (ft.count_idx) rx_put_count_idx(ft, S.pf[f], counted ? idx : 0xFFFFFFFFu);
         }
     }
 }
@@ -678,7 +678,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         else
             lane_store<ST_NT>(out, L.p, v);
         lane_count(idx, counts, hist, lds_bins);
-        if (ft.count_idx) ft.count_idx[L.p] = idx;
+        if (ft.count_idx) rx_put_count_idx(ft, L.p, idx);
     }
 }
 
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             pend_p = L.p;
             pend_valid = L.valid;
             lane_count(idx, counts, hist, lds_bins);
-            if (ft.count_idx && L.valid) ft.count_idx[L.p] = idx;
+            if (ft.count_idx && L.valid) rx_put_count_idx(ft, L.p, idx);
             L.p = np;
             L.valid = nvalid;
             L.fb = pkts + ((uint64_t)noff << unit_log2);
@@ -1027,279 +1027,293 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     }
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
 
-    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
-    const bool valid = p < n;
-    const uint64_t q = valid ? p : 0;
-    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
-    const uint8_t *fb = pkts + fpos;
-    const int32_t cp = valid ? (int32_t)len[q] : 0;
-
-    // ---- head phase -------------------------------------------------------
-    uint4 c[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
-    const uint32_t et = c[0].w & 0xFFFFu;
-    const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
-    const uint32_t proto = c[1].y >> 24;
-    const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
-    const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
-    const uint32_t sport = c[2].x >> 16;
-    const uint32_t dport = c[2].y & 0xFFFFu;
-    const uint32_t dgl = rx_bswap16(c[2].y >> 16);
-    const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
-    uint32_t cl, nd;
-    if (et == 0x0608u) {
-        cl = RXG_CLS_ARP;
-        nd = 42;
-    } else if (et != 0x0008u) {
-        cl = RXG_CLS_NON_IP;
-        nd = 14;
-    } else if (proto == 17u) {
-        cl = RXG_CLS_UDP;
-        nd = 42;
-    } else if (proto == 6u) {
-        cl = RXG_CLS_TCP;
-        nd = 54;
-    } else {
-        cl = RXG_CLS_IPV4_OTHER;
-        nd = 24;
-    }
-    const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
-    const bool l4 = is_udp || is_tcp;
-    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-    const bool do_sum = l4 && tl >= 20u;
-    if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-    int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
-    if (e > cp) e = cp;
-    const int32_t ef = e & ~15; // full tail chunks: [64, ef)
-    const bool part = ef < e && ef >= 64;
-    const bool tail = ef > 64;
-    const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
-    // the last partial chunk (consumed after the stream) and the first probe slot
-    const uint4 pc = ldg16<false>(fb + (part ? ef : 0));
-    const bool probe = valid && l4;
-    const uint32_t ka = is_udp ? dip : sip;
-    const uint32_t kb = is_udp ? dport : dip;
-    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-    const bool probe0 = probe && maxp > 0 && !(ABL & 1);
-    // the port entry, loaded with the head: UDP's direct port table entry
-    // (which decides most UDP keys without the hashed table), TCP's listener
-    // (tcp_stream_search pass 2, used on an exact-key miss)
-    const bool udp_port = is_udp && ft.udp_port != nullptr;
-    const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
-    const uint32_t pe = ptab[l4 ? dport : 0u];
-    // and the hashed table's home slot (not needed by a port-decided UDP key:
-    // a dummy load of the frame's own head then)
-    const bool hash0 = probe0 && !udp_port;
-    const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
-                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
-                             : reinterpret_cast<const uint4 *>(fb);
-    const uint4 sl0 = ld_slot(sp0);
-    uint4 sl1 = sl0;
-    if constexpr (PW == 2) sl1 = ld_slot(sp0 + (hash0 ? 1 : 0));
-
-    uint4 h1 = c[1], h2 = c[2], h3 = c[3];
-    h1.x = 0;
-    h1.y = 0;
-    h1.z &= 0xFFFF0000u;
-    if (is_udp) h2.z &= 0xFFFF0000u;
-    if (is_tcp) h3.x &= 0x0000FFFFu;
-    uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
-    acc = lane_chunk_sum(acc, h2, 32, e);
-    acc = lane_chunk_sum(acc, h3, 48, e);
-    if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
-    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
-
-    // block span of the tail chunks; a span far larger than the tails means
-    // scattered frames (per-thread fallback below)
-    __syncthreads(); // s_lo/s_hi/s_tail initialised
-    if (tail) {
-        atomicMin(&s_lo, (unsigned long long)cs_abs);
-        atomicMax(&s_hi, (unsigned long long)ce_abs);
-        atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
-    }
-    __syncthreads();
-    const uint64_t lo = s_lo, hi = s_hi;
-    const uint32_t tsum = s_tail;
-    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
-    const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
-    // (not streamed: loads of the thread's own frame head, never consumed)
-    const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
-    auto tile_load = [&](uint4 *v, uint32_t c0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k = c0 + j * 256 + tid;
-            v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
-        }
-    };
-    if (part) acc = lane_chunk_sum(acc, pc, ef, e);
-
-    // every verdict field that does not depend on the flow: payload offset and
-    // length, flags (the truncation flag for both UDP outcomes: a delivered
-    // datagram extends the bytes the reference reads to 42 + payload)
-    uint32_t flags = 0, poff = 0, plen = 0;
-    if (is_udp) {
-        poff = 42;
-        plen = dgl > 8u ? dgl - 8u : 0u;
-        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-    } else if (is_tcp) {
-        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-        poff = 34u + 4u * hl;
-        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-        plen = pl < 0 ? 0u : (uint32_t)pl;
-    }
-    const bool trunc = (int32_t)nd > cp;
-    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
-    const uint32_t vy = (poff & 0xFFFFu) | (plen << 16);
-
-    // flow probe (UDP always, TCP speculatively: a bad checksum drops the hit)
-    // and the return code
-    uint32_t flow = RXG_FLOW_NONE;
-    int32_t rc = RXG_RC_KNI;
-    auto probe_flow = [&]() {
-        bool hashed = probe0;
-        if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
-        if (hashed) {
-            // slot index and table recomputed from the keys (HO = 2 keeps only
-            // the keys and the first slot live across the stream)
-            const uint4 *tb = is_udp ? ft.udp : ft.tcp;
-            const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
-            const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
-            uint32_t pj = rx_hash3(ka, kb, kc) & mk;
-            uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
-            for (uint32_t pr = 0;;) {
-                if (sl.w == RX_SLOT_EMPTY) break;
-                if (sl.x == ka && sl.y == kb && sl.z == kc) {
-                    flow = sl.w;
-                    break;
-                }
-                if (++pr >= mp) break;
-                pj = (pj + 1) & mk;
-                if constexpr (PW == 2) {
-                    if (pr == 1 && hash0) {
-                        sl = sl1;
-                        continue;
-                    }
-                }
-                sl = ld_slot(tb + pj);
-            }
-        }
-        if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
-        if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
-        if (is_udp)
-            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                       : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-        if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
-    };
-    uint4 va[4], vb[4];
-    if constexpr (HO == 0) probe_flow();
-    // ---- tail phase -------------------------------------------------------
-    tile_load(va, 0);
-    if constexpr (HO == 1) probe_flow();
-    if (streamed) {
-        const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
-        const uint32_t ce = tail ? (uint32_t)(ce_abs - lo) : 0xFFFFFFFFu;
-        uint32_t es = 0, ee = 0, carry = 0;
-        // one tile: chunk sums, exclusive prefix (wave scans + wave totals via
-        // LDS), then each frame picks up its boundary values
-        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
-            uint32_t sj[4], xj[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
-                xj[j] = wave_incl_scan(sj[j]);
-            }
-            if (lane == 63) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
-            }
+    // one 256-frame tile per trip: one trip per block on a full grid, a
+    // block-strided loop on a resident (persistent) grid
+    const uint64_t ntiles = ((uint64_t)n + 255) / 256;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        if (tile != blockIdx.x) { // re-arm the span state: every read of the last tile's is done
             __syncthreads();
-            if constexpr (B1) { // the previous tile's boundaries (buffer buf ^ 1)
-                const uint32_t p0 = c0 - ST_TILE; // wraps for c0 = 0: no frame matches
-                if (c0 != 0 && cs - p0 < ST_TILE) es = s_pre[buf ^ 1u][cs - p0];
-                if (c0 != 0 && ce - p0 < ST_TILE) ee = s_pre[buf ^ 1u][ce - p0];
+            if (tid == 0) {
+                s_lo = ~0ull;
+                s_hi = 0;
+                s_tail = 0;
             }
-            uint32_t wt[16]; // block-uniform: kept in SGPRs
+        }
+
+        const uint64_t p = tile * 256 + tid;
+        const bool valid = p < n;
+        const uint64_t q = valid ? p : 0;
+        const uint64_t fpos = (uint64_t)off[q] << unit_log2;
+        const uint8_t *fb = pkts + fpos;
+        const int32_t cp = valid ? (int32_t)len[q] : 0;
+
+        // ---- head phase -------------------------------------------------------
+        uint4 c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
+        const uint32_t et = c[0].w & 0xFFFFu;
+        const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
+        const uint32_t proto = c[1].y >> 24;
+        const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
+        const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
+        const uint32_t sport = c[2].x >> 16;
+        const uint32_t dport = c[2].y & 0xFFFFu;
+        const uint32_t dgl = rx_bswap16(c[2].y >> 16);
+        const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+        uint32_t cl, nd;
+        if (et == 0x0608u) {
+            cl = RXG_CLS_ARP;
+            nd = 42;
+        } else if (et != 0x0008u) {
+            cl = RXG_CLS_NON_IP;
+            nd = 14;
+        } else if (proto == 17u) {
+            cl = RXG_CLS_UDP;
+            nd = 42;
+        } else if (proto == 6u) {
+            cl = RXG_CLS_TCP;
+            nd = 54;
+        } else {
+            cl = RXG_CLS_IPV4_OTHER;
+            nd = 24;
+        }
+        const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+        const bool l4 = is_udp || is_tcp;
+        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+        const bool do_sum = l4 && tl >= 20u;
+        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+        int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+        if (e > cp) e = cp;
+        const int32_t ef = e & ~15; // full tail chunks: [64, ef)
+        const bool part = ef < e && ef >= 64;
+        const bool tail = ef > 64;
+        const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
+        // the last partial chunk (consumed after the stream) and the first probe slot
+        const uint4 pc = ldg16<false>(fb + (part ? ef : 0));
+        const bool probe = valid && l4;
+        const uint32_t ka = is_udp ? dip : sip;
+        const uint32_t kb = is_udp ? dport : dip;
+        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        const bool probe0 = probe && maxp > 0 && !(ABL & 1);
+        // the port entry, loaded with the head: UDP's direct port table entry
+        // (which decides most UDP keys without the hashed table), TCP's listener
+        // (tcp_stream_search pass 2, used on an exact-key miss)
+        const bool udp_port = is_udp && ft.udp_port != nullptr;
+        const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+        const uint32_t pe = ptab[l4 ? dport : 0u];
+        // and the hashed table's home slot (not needed by a port-decided UDP key:
+        // a dummy load of the frame's own head then)
+        const bool hash0 = probe0 && !udp_port;
+        const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
+                                       (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                                 : reinterpret_cast<const uint4 *>(fb);
+        const uint4 sl0 = ld_slot(sp0);
+        uint4 sl1 = sl0;
+        if constexpr (PW == 2) sl1 = ld_slot(sp0 + (hash0 ? 1 : 0));
+
+        uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+        h1.x = 0;
+        h1.y = 0;
+        h1.z &= 0xFFFF0000u;
+        if (is_udp) h2.z &= 0xFFFF0000u;
+        if (is_tcp) h3.x &= 0x0000FFFFu;
+        uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
+        acc = lane_chunk_sum(acc, h2, 32, e);
+        acc = lane_chunk_sum(acc, h3, 48, e);
+        if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
+        const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+
+        // block span of the tail chunks; a span far larger than the tails means
+        // scattered frames (per-thread fallback below)
+        __syncthreads(); // s_lo/s_hi/s_tail initialised
+        if (tail) {
+            atomicMin(&s_lo, (unsigned long long)cs_abs);
+            atomicMax(&s_hi, (unsigned long long)ce_abs);
+            atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
+        }
+        __syncthreads();
+        const uint64_t lo = s_lo, hi = s_hi;
+        const uint32_t tsum = s_tail;
+        const bool streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
+        const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
+        // (not streamed: loads of the thread's own frame head, never consumed)
+        const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
+        auto tile_load = [&](uint4 *v, uint32_t c0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
-                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
-                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
-                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
-                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
-            }
-            uint32_t base = carry;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t wb = 0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
-                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
-                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
-            }
-            carry = base;
-            if constexpr (!B1) {
-                __syncthreads();
-                if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
-                if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+                const uint32_t k = c0 + j * 256 + tid;
+                v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
             }
         };
-        // unrolled twice: the A/B tiles swap roles without register moves (a
-        // move would wait for the prefetch it copies); one exit per pair (a
-        // trailing all-masked tile costs no bandwidth: its loads hit chunk 0)
-        uint32_t c0 = 0;
-        for (; c0 < span; c0 += 2 * ST_TILE) {
-            tile_load(vb, c0 + ST_TILE);
-            tile(va, c0, 0);
-            tile_load(va, c0 + 2 * ST_TILE);
-            tile(vb, c0 + ST_TILE, 1);
-        }
-        if constexpr (B1) { // the last tile's boundaries (buffer 1)
-            __syncthreads();
-            const uint32_t p0 = c0 - ST_TILE;
-            if (cs - p0 < ST_TILE) es = s_pre[1][cs - p0];
-            if (ce - p0 < ST_TILE) ee = s_pre[1][ce - p0];
-        }
-        if (ce == span) ee = carry;
-        if (tail) acc += ee - es;
-    } else if (tail) { // scattered frames: this thread sums its own tail
-        for (int32_t s = 64; s < ef; s += 64) {
-            uint4 r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[u] = ldg16<false>(fb + (s + 16 * u < ef ? s + 16 * u : 0));
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (s + 16 * u < ef) acc += chunk_sum(r[u]);
-        }
-    }
+        if (part) acc = lane_chunk_sum(acc, pc, ef, e);
 
-    if constexpr (HO >= 2) probe_flow();
-    // ---- verdict ----------------------------------------------------------
-    uint32_t ck = 0;
-    if (do_sum) {
-        ck = (~fold16(acc)) & 0xFFFFu;
-        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-    }
-    const bool ok = l4 && stored == ck;
-    if (is_tcp) {
-        if (!ok) flow = RXG_FLOW_NONE;
-        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-    }
-    if (valid) {
-        uint4 vd;
-        vd.x = flow;
-        vd.y = vy;
-        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-        stg16(&out[p], vd);
-        const uint32_t cidx =
-            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
-        lane_count(cidx, counts, hist, lds_bins);
-        if (ft.count_idx) ft.count_idx[p] = cidx;
-    }
+        // every verdict field that does not depend on the flow: payload offset and
+        // length, flags (the truncation flag for both UDP outcomes: a delivered
+        // datagram extends the bytes the reference reads to 42 + payload)
+        uint32_t flags = 0, poff = 0, plen = 0;
+        if (is_udp) {
+            poff = 42;
+            plen = dgl > 8u ? dgl - 8u : 0u;
+            if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        } else if (is_tcp) {
+            const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+            poff = 34u + 4u * hl;
+            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+            plen = pl < 0 ? 0u : (uint32_t)pl;
+        }
+        const bool trunc = (int32_t)nd > cp;
+        const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
+        const uint32_t vy = (poff & 0xFFFFu) | (plen << 16);
+
+        // flow probe (UDP always, TCP speculatively: a bad checksum drops the hit)
+        // and the return code
+        uint32_t flow = RXG_FLOW_NONE;
+        int32_t rc = RXG_RC_KNI;
+        auto probe_flow = [&]() {
+            bool hashed = probe0;
+            if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
+            if (hashed) {
+                // slot index and table recomputed from the keys (HO = 2 keeps only
+                // the keys and the first slot live across the stream)
+                const uint4 *tb = is_udp ? ft.udp : ft.tcp;
+                const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
+                const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
+                uint32_t pj = rx_hash3(ka, kb, kc) & mk;
+                uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
+                for (uint32_t pr = 0;;) {
+                    if (sl.w == RX_SLOT_EMPTY) break;
+                    if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                        flow = sl.w;
+                        break;
+                    }
+                    if (++pr >= mp) break;
+                    pj = (pj + 1) & mk;
+                    if constexpr (PW == 2) {
+                        if (pr == 1 && hash0) {
+                            sl = sl1;
+                            continue;
+                        }
+                    }
+                    sl = ld_slot(tb + pj);
+                }
+            }
+            if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+            if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
+            if (is_udp)
+                rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                           : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+            if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+        };
+        uint4 va[4], vb[4];
+        if constexpr (HO == 0) probe_flow();
+        // ---- tail phase -------------------------------------------------------
+        tile_load(va, 0);
+        if constexpr (HO == 1) probe_flow();
+        if (streamed) {
+            const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
+            const uint32_t ce = tail ? (uint32_t)(ce_abs - lo) : 0xFFFFFFFFu;
+            uint32_t es = 0, ee = 0, carry = 0;
+            // one tile: chunk sums, exclusive prefix (wave scans + wave totals via
+            // LDS), then each frame picks up its boundary values
+            auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
+                uint32_t sj[4], xj[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
+                    xj[j] = wave_incl_scan(sj[j]);
+                }
+                if (lane == 63) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+                }
+                __syncthreads();
+                if constexpr (B1) { // the previous tile's boundaries (buffer buf ^ 1)
+                    const uint32_t p0 = c0 - ST_TILE; // wraps for c0 = 0: no frame matches
+                    if (c0 != 0 && cs - p0 < ST_TILE) es = s_pre[buf ^ 1u][cs - p0];
+                    if (c0 != 0 && ce - p0 < ST_TILE) ee = s_pre[buf ^ 1u][ce - p0];
+                }
+                uint32_t wt[16]; // block-uniform: kept in SGPRs
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
+                    wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
+                    wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
+                    wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
+                    wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
+                }
+                uint32_t base = carry;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t wb = 0;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
+                    s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
+                    base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
+                }
+                carry = base;
+                if constexpr (!B1) {
+                    __syncthreads();
+                    if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
+                    if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+                }
+            };
+            // unrolled twice: the A/B tiles swap roles without register moves (a
+            // move would wait for the prefetch it copies); one exit per pair (a
+            // trailing all-masked tile costs no bandwidth: its loads hit chunk 0)
+            uint32_t c0 = 0;
+            for (; c0 < span; c0 += 2 * ST_TILE) {
+                tile_load(vb, c0 + ST_TILE);
+                tile(va, c0, 0);
+                tile_load(va, c0 + 2 * ST_TILE);
+                tile(vb, c0 + ST_TILE, 1);
+            }
+            if constexpr (B1) { // the last tile's boundaries (buffer 1)
+                __syncthreads();
+                const uint32_t p0 = c0 - ST_TILE;
+                if (cs - p0 < ST_TILE) es = s_pre[1][cs - p0];
+                if (ce - p0 < ST_TILE) ee = s_pre[1][ce - p0];
+            }
+            if (ce == span) ee = carry;
+            if (tail) acc += ee - es;
+        } else if (tail) { // scattered frames: this thread sums its own tail
+            for (int32_t s = 64; s < ef; s += 64) {
+                uint4 r[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) r[u] = ldg16<false>(fb + (s + 16 * u < ef ? s + 16 * u : 0));
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (s + 16 * u < ef) acc += chunk_sum(r[u]);
+            }
+        }
+
+        if constexpr (HO >= 2) probe_flow();
+        // ---- verdict ----------------------------------------------------------
+        uint32_t ck = 0;
+        if (do_sum) {
+            ck = (~fold16(acc)) & 0xFFFFu;
+            if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+        }
+        const bool ok = l4 && stored == ck;
+        if (is_tcp) {
+            if (!ok) flow = RXG_FLOW_NONE;
+            rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+        }
+        if (valid) {
+            uint4 vd;
+            vd.x = flow;
+            vd.y = vy;
+            vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+            vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+            stg16(&out[p], vd);
+            const uint32_t cidx =
+                rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+            lane_count(cidx, counts, hist, lds_bins);
+            if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
+        }
+    } // tiles
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -1309,12 +1323,23 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     }
 }
 
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
+// PERS: a resident grid (occupancy x CUs, or the g_bpc_cap) of blocks that
+// loop over the tiles, instead of one block per tile
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
-    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    uint64_t blocks = ((uint64_t)n + 255) / 256;
+    if constexpr (PERS) {
+        int cu = 0, occ = 0;
+        hipError_t e = rx_occupancy(
+            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), 256,
+            (size_t)lds_bins * 4u, &cu, &occ);
+        if (e != hipSuccess) return e;
+        if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
+        blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
+    }
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
@@ -1325,26 +1350,31 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 // ---------------------------------------------------------------------------
 // Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
-// memory-side request): the classify kernel writes one 4-B count index per
-// frame (ft.count_idx), and a slab histogram sums them.  Pass 1: block b
-// (1024 threads, one per CU: 128 KiB of LDS) adds the indices of its share of
-// the frames that fall in its 65536-flow range (blockIdx.y) into 16-bit LDS
-// bins, two per dword (lo = even flow, hi = odd), and writes the bins out as
-// slab b.  A bin overflows only when more than 65535 of the block's frames
-// are one flow: the sum of the bins then differs from the block's exact tally
-// of counted frames (each wrap loses 65535 or 65536), and the block zeroes
-// its slab and adds its frames with global atomics instead (pathological
-// traffic only).  Pass 2: a thread per 4 bin pairs sums that column over the
-// slabs (16-B loads) and adds it to counts.
+// memory-side request): the classify kernel writes one count index per frame
+// (ft.count_idx: 2 B when the flows fit one 65536-flow range, else 4 B), and
+// a slab histogram sums them.  A 2-B index of all ones is flow 65535 or a
+// frame not counted: the slab pass reads that frame's verdict to tell which.  Pass 1: block b (1024 threads, one per CU: 128
+// KiB of LDS) adds the indices of its share of the frames that fall in its
+// 65536-flow range (blockIdx.y) into 16-bit LDS bins, two per dword (lo =
+// even flow, hi = odd), and writes the bins out as slab b.  A bin overflows
+// only when more than 65535 of the block's frames are one flow: the sum of the
+// bins then differs from the block's exact tally of counted frames (each wrap
+// loses 65535 or 65536), and the block zeroes its slab and adds its frames
+// with global atomics instead (pathological traffic only).  Pass 2: a thread
+// per 4 bin pairs sums that column over the slabs (16-B loads) and adds it to
+// counts.
 constexpr uint32_t SLAB_MAX_FLOWS = 65536;
 constexpr uint32_t SLAB_MIN_FLOWS = 8193;   // below: LDS histogram in the classify kernel
 
-__global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__restrict__ cidx,
-                                                              uint32_t n, uint32_t per,
-                                                              uint32_t words,
+template <typename T> // count index: uint16_t (one range, <= 65536 flows) or uint32_t
+__global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict__ cidx,
+                                                              const uint4 *__restrict__ verd,
+                                                              uint32_t nu, uint32_t n, uint32_t per,
+                                                              uint32_t words, uint32_t nflows,
                                                               uint32_t *__restrict__ slab,
                                                               unsigned long long *__restrict__ counts) {
-    // blockIdx.y = flow range: flows [y * 65536, y * 65536 + 2 * words)
+    constexpr uint32_t E = 16 / sizeof(T); // indices per 16-B load
+    // blockIdx.y = flow range: flows [y * 65536, y * 65536 + lim)
     __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
     __shared__ uint32_t tally, sum;
     const uint32_t tid = threadIdx.x;
@@ -1352,29 +1382,66 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__r
     if (tid == 0) tally = sum = 0;
     __syncthreads();
     const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
+    const uint32_t lim = min(nflows - f0, SLAB_MAX_FLOWS);
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
     uint32_t mine = 0;
     auto count = [&](uint32_t x) {
-        const uint32_t f = x - f0; // ~0u and other ranges: f >= 2 * words
-        if (f < 2u * words) {
+        const uint32_t f = x - f0; // not counted (all ones) and other ranges: f >= lim
+        if (f < lim) {
             atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
             ++mine;
         }
     };
-    // 16 indices per thread per trip (four 16-B loads in flight); b0 is a
-    // multiple of 4 (per is), so the vector loads are aligned
-    uint64_t i = b0 + 4ull * tid;
-    for (; i + 4 * 3 * 1024 + 3 < b1; i += 4ull * 4 * 1024) {
+    // a 2-B all-ones index: flow 65535 or not counted, from the frame's verdict
+    auto from_verdict = [&](uint4 v) -> uint32_t {
+        const bool counted = (int8_t)(v.z >> 24) == RXG_RC_OK && v.x != RXG_FLOW_NONE;
+        return counted ? (((v.z >> 16) & 0xFFu) == RXG_CLS_TCP ? nu : 0u) + v.x : ~0u;
+    };
+    auto index_of = [&](uint32_t x, uint64_t k) -> uint32_t {
+        if constexpr (sizeof(T) == 2)
+            if (x == 0xFFFFu) return from_verdict(verd[k]);
+        return x;
+    };
+    // 4E indices per thread per trip (four 16-B loads in flight); b0 is a
+    // multiple of 8 (per is), so the vector loads are aligned
+    uint64_t i = b0 + (uint64_t)E * tid;
+    for (; i + (uint64_t)E * 3 * 1024 + E - 1 < b1; i += (uint64_t)E * 4 * 1024) {
         uint4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * 4096));
+            v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * E * 1024));
+        if constexpr (sizeof(T) == 2) {
+            // an all-ones index is flow 65535 iff the frame's rc is RXG_RC_OK
+            // (rc OK <=> a control block matched): every lane loads one rc
+            // dword per index, its own frame's for all-ones indices and one
+            // shared dword otherwise, so the loads need no branch and all are
+            // in flight before any is consumed
+            const uint32_t *vz = reinterpret_cast<const uint32_t *>(verd) + 2;
+            uint32_t rx[4][8], z[4][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) count(v[u].x), count(v[u].y), count(v[u].z), count(v[u].w);
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    rx[u][j] = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    const uint64_t k = i + (uint64_t)u * E * 1024 + j;
+                    z[u][j] = vz[4 * (rx[u][j] == 0xFFFFu ? k : b0)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    count(rx[u][j] != 0xFFFFu ? rx[u][j]
+                                              : ((int8_t)(z[u][j] >> 24) == RXG_RC_OK ? 0xFFFFu : ~0u));
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) count(v[u].x), count(v[u].y), count(v[u].z), count(v[u].w);
+        }
     }
-    for (; i < b1; i += 4ull * 1024)
-        for (uint64_t k = i; k < i + 4 && k < b1; ++k) count(cidx[k]);
+    for (; i < b1; i += (uint64_t)E * 1024)
+        for (uint64_t k = i; k < i + E && k < b1; ++k) count(index_of(cidx[k], k));
     if (mine) atomicAdd(&tally, mine);
     __syncthreads();
     uint32_t part = 0;
@@ -1386,14 +1453,16 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const uint32_t *__r
     for (uint32_t k = tid; k < words; k += 1024) dst[k] = wrapped ? 0u : bins[k];
     if (wrapped)
         for (uint64_t k = b0 + tid; k < b1; k += 1024) {
-            const uint32_t f = cidx[k] - f0;
-            if (f < 2u * words) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
+            const uint32_t f = index_of(cidx[k], k) - f0;
+            if (f < lim) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
         }
 }
 
 // block = 64 lanes x 4 bin pairs (one 16-B column piece per lane) x 16 waves,
 // wave w summing slabs w, w + 16, ... with 4 loads in flight; the 16 partial
-// sums meet in LDS.  words is a multiple of 4 (slab_words).
+// sums meet in LDS.  words is a multiple of 4 (slab_words).  (Splitting the
+// slabs over 4x the blocks, adding with u64 atomics, was 7 us slower at cfg4:
+// profiles/r02f/ab_count_paths.txt.)
 __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
                                                                 uint32_t nslabs, uint32_t words,
                                                                 uint32_t nflows,
@@ -1506,7 +1575,7 @@ static uint32_t slab_words(const rx_ft_dev &ft) {
 static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
     const uint64_t want = std::max<uint64_t>(1, 256 / nranges);
     uint64_t pr = std::max<uint64_t>(((uint64_t)n + want - 1) / want, 16384);
-    pr = (pr + 3) & ~3ull;
+    pr = (pr + 7) & ~7ull;
     const uint64_t nb = ((uint64_t)n + pr - 1) / pr;
     *nslabs = (uint32_t)(nb ? nb : 1);
     *per = (uint32_t)pr;
@@ -1517,13 +1586,22 @@ static bool use_slab(const rx_ft_dev &ft, bool counts) {
     return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS * SLAB_MAX_RANGES;
 }
 
-static hipError_t launch_count_slab(const uint32_t *cidx, uint32_t n, const rx_ft_dev &ft,
+// u16 count indices: the flows fit one range
+static bool cidx16(const rx_ft_dev &ft) { return ft.nu + ft.nt <= SLAB_MAX_FLOWS; }
+
+static hipError_t launch_count_slab(const void *cidx, const uint4 *verd, uint32_t n, const rx_ft_dev &ft,
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
     slab_geometry(n, nr, &nslabs, &per);
-    hipLaunchKernelGGL(rx_count_slab_kernel, dim3(nslabs, nr), dim3(1024), 0, s, cidx, n, per,
-                       words, slab, counts);
+    if (ft.cidx16)
+        hipLaunchKernelGGL(rx_count_slab_kernel<uint16_t>, dim3(nslabs, nr), dim3(1024), 0, s,
+                           static_cast<const uint16_t *>(cidx), verd, ft.nu, n, per, words, nf,
+                           slab, counts);
+    else
+        hipLaunchKernelGGL(rx_count_slab_kernel<uint32_t>, dim3(nslabs, nr), dim3(1024), 0, s,
+                           static_cast<const uint32_t *>(cidx), verd, ft.nu, n, per, words, nf,
+                           slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (nslabs <= 64)
@@ -1607,6 +1685,9 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
     // 38/39: pipes 34/30 with one barrier per tail tile (B1)
     {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>}, {0, 1, 1, 39, launch_stream<true, 0, 0, 1, true>},
+    // 42/43: pipes 38/39 on a resident grid (blocks loop over tiles)
+    {0, 1, 1, 42, launch_stream<true, 0, 3, 1, true, true>},
+    {0, 1, 1, 43, launch_stream<true, 0, 0, 1, true, true>},
 };
 
 } // namespace
@@ -1635,9 +1716,7 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
 void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
 
 // workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
-// frame), then the count slabs
-// workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
-// frame), then the count indices (4 B per frame) and the count slabs
+// frame), then the count indices (room for 4 B per frame) and the count slabs
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts) {
     size_t b = (g == 0 && pipe == 20) ? 16 + 8ull * n : 0;
@@ -1662,10 +1741,10 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
     const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
     // workspace: [binned lists][count indices][slabs]
     const size_t lists = (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
-    uint32_t *cidx = slab ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists)
-                          : nullptr;
+    uint8_t *cidx = slab ? reinterpret_cast<uint8_t *>(ws) + lists : nullptr;
     rx_ft_dev ft = ft_in;
     ft.count_idx = cidx;
+    ft.cidx16 = slab && cidx16(ft_in) && !ft_in.count_4b;
     hipError_t e = hipErrorInvalidValue;
     if (g == 0 && pipe == 20) { // size-class binned (workspace: 16 B + 8 B per frame)
         e = launch_binned(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, ws);
@@ -1682,6 +1761,6 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
             }
     }
     if (e != hipSuccess || !slab) return e;
-    uint32_t *slabs = cidx + ((((size_t)n * 4 + 255) & ~(size_t)255) / 4);
-    return launch_count_slab(cidx, n, ft, counts, slabs, s);
+    uint32_t *slabs = reinterpret_cast<uint32_t *>(cidx + (((size_t)n * 4 + 255) & ~(size_t)255));
+    return launch_count_slab(cidx, out, n, ft, counts, slabs, s);
 }

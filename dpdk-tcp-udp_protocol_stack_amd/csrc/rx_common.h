@@ -42,10 +42,23 @@ struct rx_ft_dev {
     uint32_t udp_dip;
     // per-launch output, set by rx_classify_launch on its copy: on the slab
     // count path every kernel writes frame i's count index (UDP flow k -> k,
-    // TCP flow k -> nu + k; 0xFFFFFFFF = not counted) to count_idx[i], which
-    // the slab pass reads instead of the 16-B verdicts; null otherwise
-    uint32_t *count_idx;
+    // TCP flow k -> nu + k; all ones = not counted) to count_idx[i], which
+    // the slab pass reads instead of the 16-B verdicts; null otherwise.  u16
+    // indices when cidx16 (at most 65535 flows: one slab range), u32 otherwise
+    void *count_idx;
+    uint32_t cidx16;
+    // rxg_tune_tables(RXG_TT_COUNT_4B): 4-B count indices whatever the flow
+    // count (the round-1 count path, for A/B)
+    uint32_t count_4b;
 };
+
+// frame p's count index (idx = ~0u: not counted) on the slab count path
+RX_HD void rx_put_count_idx(const rx_ft_dev &ft, uint64_t p, uint32_t idx) {
+    if (ft.cidx16)
+        static_cast<uint16_t *>(ft.count_idx)[p] = (uint16_t)idx;
+    else
+        static_cast<uint32_t *>(ft.count_idx)[p] = idx;
+}
 #define RX_PORT_NONE 0x7FFFFFFFu   // udp_port entry: no socket (udp_dip, port)
 #define RX_PORT_HASHED 0x80000000u // some socket on this port is bound to another ip
 

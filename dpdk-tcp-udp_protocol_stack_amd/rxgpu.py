@@ -62,7 +62,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 30), (0, 0, 0, 31),  # stream kernel
                    (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
-                   (0, 0, 0, 38), (0, 0, 0, 39)]  # one barrier per tail tile
+                   (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
+                   (0, 0, 0, 42), (0, 0, 0, 43)]  # the same on a resident grid
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -124,6 +125,7 @@ _tune_tx = _sig("rxg_tune_tx", _i32, _vp, _u32, _u32)
 _tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
 _tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
 TT_NO_UDP_PORT = 0x1
+TT_COUNT_4B = 0x2
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)

@@ -206,7 +206,7 @@ int rxg_tx_cksum(rxg_ctx *ctx, uint8_t *pkts, uint64_t span_bytes, const uint32_
 /* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
  * loaded up front, frames per lane group, pipeline mode; 0xFFFFFFFF = the
  * default pipeline); lanes_per_frame = 0 = automatic from len_hint, except
- * with pipeline 20 (size-class binned path) or 30..39 / 130 (stream kernel
+ * with pipeline 20 (size-class binned path) or 30..43 / 130 (stream kernel
  * variants, csrc/rx_classify.hip k_variants).  Unknown combinations make the
  * next burst fail with RXG_EHIP. */
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
@@ -228,10 +228,13 @@ int rxg_tune_tx(rxg_ctx *ctx, uint32_t variant, uint32_t blocks_per_cu);
  * and probe length do. */
 int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
 
-/* Tuning hook: flow-table layout flags, applied by the next rxg_flows_sync
- * (0 = the default layout).  RXG_TT_NO_UDP_PORT: no direct UDP port table;
- * every UDP lookup probes the hashed table.  Verdicts do not depend on it. */
+/* Tuning hook: flow-table layout flags (0 = the default layout).
+ * RXG_TT_NO_UDP_PORT (applied by the next rxg_flows_sync): no direct UDP port
+ * table; every UDP lookup probes the hashed table.  RXG_TT_COUNT_4B (applied
+ * at once): the 8193..2M-flow count path keeps 4-B count indices even at
+ * <= 65536 flows.  Verdicts and counts depend on neither. */
 #define RXG_TT_NO_UDP_PORT 0x1u
+#define RXG_TT_COUNT_4B 0x2u
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */

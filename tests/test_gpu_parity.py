@@ -200,7 +200,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 @pytest.mark.parametrize("layout", ["packed", "block_shuffled", "scattered", "gapped"])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
-                                     (0, 0, 0, 39), (0, 0, 0, 20),
+                                     (0, 0, 0, 39), (0, 0, 0, 42), (0, 0, 0, 43), (0, 0, 0, 20),
                                      (4, 1, 2, 0)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
@@ -446,23 +446,33 @@ def test_unknown_variant_fails_loudly(ctx, torch_dev):
     assert got.tobytes() == O.Tables(udp, tcb).classify(pk, off, ln, 6).tobytes()
 
 
-@pytest.mark.parametrize("nu,n", [(70000, 140000), (2000000, 600000)])
-@pytest.mark.parametrize("target", [4000, 4001])
-def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
-    """every frame to one UDP socket (`target`: an even and an odd flow, the
-    low and the high 16-bit bin of a pair): 70000 sockets (two count ranges,
-    no bin reaches 65536) and 2M sockets (32 ranges: slabs of 75000 frames,
-    so the bin wraps and the slab's global-atomic fallback counts) — counts
-    stay exact"""
-    torch, dev = torch_dev
+def _udp_socks(nu):
     udp = np.zeros(nu, R.UDP_SOCK_DTYPE)
     ips = (0x0A000000 + np.arange(nu, dtype=np.uint64) // 1000).astype(np.uint32)
     udp["localip"] = ips.byteswap()  # 10.0.0.0 + k / 1000 in network order
     ports = (20000 + np.arange(nu) % 1000).astype(np.uint16)
     udp["localport"] = ports.byteswap()  # ports 20000 + k % 1000
     udp["protocol"] = 17
-    ip = ".".join(str(b) for b in (0x0A000000 + target // 1000).to_bytes(4, "big"))
-    f = F.udp_frame("10.1.2.3", 5555, ip, 20000 + target % 1000, b"z" * 20)
+    return udp
+
+
+def _sock_frame(k, port=None):
+    ip = ".".join(str(b) for b in (0x0A000000 + k // 1000).to_bytes(4, "big"))
+    return F.udp_frame("10.1.2.3", 5555, ip, port or 20000 + k % 1000, b"z" * 20)
+
+
+@pytest.mark.parametrize("nu,n", [(70000, 140000), (2000000, 600000), (65536, 17000000)])
+@pytest.mark.parametrize("target", [4000, 4001, 65535])
+def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
+    """every frame to one UDP socket (`target`: an even and an odd flow, the
+    low and the high 16-bit bin of a pair, and flow 65535, whose 2-B count
+    index is the all-ones one): 70000 sockets (two count ranges, no bin
+    reaches 65536), 2M sockets (32 ranges: slabs of 75000 frames, so the bin
+    wraps and the slab's global-atomic fallback counts) and 65536 sockets (2-B
+    indices, slabs of 66408 frames: the bin wraps) — counts stay exact"""
+    torch, dev = torch_dev
+    udp = _udp_socks(nu)
+    f = _sock_frame(target)
     buf, off, lens = F.pack_frames([f], 6)
     pk = np.tile(buf[:64], n)
     off = np.arange(n, dtype=np.uint32)
@@ -472,4 +482,31 @@ def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
     assert np.all(got["rc"] == 0) and np.all(got["flow_id"] == target)
     want = np.zeros(nu, np.uint64)
     want[target] = n
+    assert np.array_equal(cnt, want)
+
+
+@pytest.mark.parametrize("nu", [65535, 65536])
+def test_count_idx16_all_ones(ctx, torch_dev, nu):
+    """2-B count indices (<= 65536 flows): frames of flow 65535 (when it
+    exists), frames counted nowhere (no socket on the port: rc -3) and frames
+    of flow 7 interleaved; the all-ones index is told apart by the verdict"""
+    torch, dev = torch_dev
+    udp = _udp_socks(nu)
+    fs = [_sock_frame(65535), _sock_frame(0, port=19999), _sock_frame(7)]
+    assert len({len(f) for f in fs}) == 1
+    buf, off, lens = F.pack_frames(fs, 6)
+    reps = 100000
+    pk = np.tile(buf[:64 * 3], reps)
+    n = 3 * reps
+    off = np.arange(n, dtype=np.uint32)
+    lens = np.full(n, len(fs[0]), np.uint16)
+    ctx.flows_sync(udp, None)
+    got, cnt = _dev_classify(torch_dev, ctx, pk, off, lens, 6, 64, counts=True)
+    want_v = O.Tables(udp, np.zeros(0, R.TCB_DTYPE)).classify(pk[:64 * 3], off[:3], lens[:3], 6)
+    assert got[:3].tobytes() == want_v.tobytes()
+    assert list(got["rc"][:3]) == [0 if nu == 65536 else -3, -3, 0]
+    want = np.zeros(nu, np.uint64)
+    want[7] = reps
+    if nu == 65536:
+        want[65535] = reps
     assert np.array_equal(cnt, want)

@@ -7,7 +7,10 @@ rxg_tune_flow_load) and times K1 back to back (HIP events), without and with
 per-flow counts.  Median and min over rounds.  Verdicts are checked equal
 across layouts (they must not depend on the layout).
 
-    python tools/ab_tables.py [cfg4,cfg5] [rounds]
+    python tools/ab_tables.py [cfg4,cfg5] [rounds] [layout,layout...]
+
+count4B = the default layout with 4-B count indices (the round-1 count
+path), against which the counts columns of port+1/4 compare.
 """
 import os
 import sys
@@ -22,12 +25,14 @@ import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
 LAYOUTS = [("port+1/4", 0, 0), ("hash+1/4", R.TT_NO_UDP_PORT, 0), ("port+1/2", 0, 1),
-           ("port+1/8", 0, 3)]
+           ("port+1/8", 0, 3), ("count4B", R.TT_COUNT_4B, 0)]
 
 
 def main():
     names = (sys.argv[1] if len(sys.argv) > 1 else "cfg4").split(",")
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    pick = sys.argv[3].split(",") if len(sys.argv) > 3 else None
+    layouts = [lay for lay in LAYOUTS if pick is None or lay[0] in pick]
     dev = torch.device("cuda", 0)
     ctx = R.Context(0)
     sh = torch.cuda.current_stream(dev).cuda_stream
@@ -45,9 +50,9 @@ def main():
         out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
         ref = None
         cnt = torch.zeros(len(udp) + len(tcb), dtype=torch.int64, device=dev)
-        times = {(lay[0], c): [] for lay in LAYOUTS for c in (False, True)}
+        times = {(lay[0], c): [] for lay in layouts for c in (False, True)}
         for r in range(rounds):
-            for name, flags, load in LAYOUTS:
+            for name, flags, load in layouts:
                 ctx.tune_tables(flags)
                 ctx.tune_flow_load(load)
                 ctx.flows_sync(udp, tcb)
