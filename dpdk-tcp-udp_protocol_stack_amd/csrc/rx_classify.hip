@@ -473,6 +473,21 @@ __device__ __forceinline__ void lane_desc(lane_frame &L, uint64_t p, uint32_t n,
     L.cap = L.valid ? (int32_t)len[q] : 0;
 }
 
+// lane_desc without an index list and without a branch around a load (PIPE
+// 14: a branch here would make the compiler drain the prefetched frame bytes)
+__device__ __forceinline__ void lane_desc_nb(lane_frame &L, uint64_t p, uint32_t n,
+                                             const uint8_t *__restrict__ pkts,
+                                             const uint32_t *__restrict__ off,
+                                             const uint16_t *__restrict__ len, uint32_t unit_log2) {
+    L.valid = p < n;
+    const uint64_t q = L.valid ? p : 0;
+    L.p = q;
+    const uint32_t o = off[q];
+    const uint32_t l = len[q];
+    L.fb = pkts + ((uint64_t)o << unit_log2);
+    L.cap = L.valid ? (int32_t)l : 0;
+}
+
 template <bool NTL>
 __device__ __forceinline__ void lane_load(lane_frame &L) {
 #pragma unroll
@@ -490,6 +505,46 @@ __device__ __forceinline__ void lane_load(lane_frame &L) {
 __device__ __forceinline__ void lane_load_staged(lane_frame &L, const uint8_t *b, uint4 *st,
                                                  uint32_t lane) {
     stage64_load(b, st, lane, L.c);
+}
+
+// Pipelined form of lane_load_staged (PIPE 14): issue the four 16-B loads of
+// L's first 64 B into v and return whether the wave's 64 frames sit in
+// consecutive 64-B slots (wave-uniform).  Coalesced: lane l loads chunk
+// q*64 + l of the wave's 4 KiB; otherwise lane l loads its own frame's chunk q
+// (chunks past caplen read chunk 0 and are masked by lane_verdict).  No branch
+// around the loads.
+__device__ __forceinline__ bool lane_issue(const lane_frame &L, const uint8_t *pkts, uint32_t lane,
+                                           uint4 (&v)[4]) {
+    const uint64_t fpos = (uint64_t)(L.fb - pkts);
+    const uint64_t f0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fpos >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)fpos);
+    // (the 4 KiB must lie inside the buffer: slots 0..62 end where the next
+    // frame starts, slot 63 only if its frame reaches past byte 48)
+    const bool co =
+        __ballot(L.valid && fpos == f0 + 64ull * lane && (lane != 63u || L.cap > 48)) == ~0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint8_t *a = co ? pkts + f0 + 16u * (q * 64u + lane) : L.fb + (16 * q < L.cap ? 16 * q : 0);
+        v[q] = ldg16<true>(a);
+    }
+    return co;
+}
+
+// Consume lane_issue's loads: through the wave's 4-KiB LDS stage, transposed
+// (coalesced: the stage64_load layout) or in place (per-lane), into L.c
+__device__ __forceinline__ void lane_stage(lane_frame &L, const uint4 (&v)[4], bool co, uint4 *st,
+                                           uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t k = q * 64u + lane, f = k >> 2;
+        const uint32_t wc = f * 4u + (((k & 3u) + (f >> 2)) & 3u);
+        const uint32_t wl = lane * 4u + ((q + (lane >> 2)) & 3u);
+        st[co ? wc : wl] = v[q];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) L.c[k] = st[lane * 4u + ((k + (lane >> 2)) & 3u)];
+    __builtin_amdgcn_wave_barrier();
 }
 
 // Parse + checksum + probe + verdict of one lane-owned frame.  `next` (may be
@@ -613,6 +668,10 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
             }
         }
         if (is_tcp && flow == RXG_FLOW_NONE) flow = ft.listen[dport];
+        // consume the listener load inside this branch: left pending, the merge
+        // with the LDS-table path makes the compiler wait for every outstanding
+        // load (vmcnt(0)) before the verdict, draining PIPE 14's prefetch
+        asm volatile("" ::"v"(flow));
     }
 
     int32_t rc;
@@ -694,7 +753,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0 || PIPE == 12, "LDS table: PIPE 0 / 12 only");
+    static_assert(!LDT || PIPE == 0 || PIPE >= 12, "LDS table: PIPE 0 / 12 / 14 / 15 only");
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
@@ -770,6 +829,126 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_load<NTL>(L);
             lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
         }
+    } else if constexpr (PIPE == 14) {
+        // 12, software-pipelined: descriptors two trips ahead, frame bytes one
+        // trip ahead (issued before the current trip is staged and processed),
+        // so a wave keeps its next 4 KiB in flight across its parse / probe /
+        // store instead of waiting descriptor -> frame latency every trip.
+        // Loads are never under a branch (the last trip's prefetch reads the
+        // clamped frame 0 and is dropped): the coalesced-or-per-lane choice is
+        // an address select and a staging-index select (lane_issue /
+        // lane_stage), so the wait counts stay partial.  Three descriptor
+        // sets x two frame-byte sets rotate with period 6, unrolled so no
+        // register moves are needed (a move would wait for the load it
+        // copies).
+        uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                       (tid >> 6) * 256u;
+        const uint32_t lane = tid & 63u;
+        uint64_t base = (uint64_t)blockIdx.x * 256;
+        if (base < n) {
+            lane_frame A, B, D;
+            uint4 va[4], vb[4];
+            lane_desc_nb(A, p, n, pkts, off, len, unit_log2);
+            lane_desc_nb(B, p + stride, n, pkts, off, len, unit_log2);
+            bool ca = lane_issue(A, pkts, lane, va), cb = false;
+            for (;;) {
+                // trip t = A (bytes in va), t+1 = B (descriptors), t+2 -> D
+                lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
+                cb = lane_issue(B, pkts, lane, vb);
+                lane_stage(A, va, ca, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // trip t = B (bytes in vb), t+1 = D, t+2 -> A
+                lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
+                ca = lane_issue(D, pkts, lane, va);
+                lane_stage(B, vb, cb, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // trip t = D (bytes in va), t+1 = A, t+2 -> B
+                lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
+                cb = lane_issue(A, pkts, lane, vb);
+                lane_stage(D, va, ca, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // trip t = A (bytes in vb), t+1 = B, t+2 -> D
+                lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
+                ca = lane_issue(B, pkts, lane, va);
+                lane_stage(A, vb, cb, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // trip t = B (bytes in va), t+1 = D, t+2 -> A
+                lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
+                cb = lane_issue(D, pkts, lane, vb);
+                lane_stage(B, va, ca, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // trip t = D (bytes in vb), t+1 = A, t+2 -> B
+                lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
+                ca = lane_issue(A, pkts, lane, va);
+                lane_stage(D, vb, cb, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                if (base >= n) break;
+                // back at the head's roles: A (bytes in va), B descriptors.  B's
+                // descriptor loads are waited for here, where the count of later
+                // loads is exact; left pending across the back edge, the loop
+                // head's merged state made the compiler wait for everything
+                // (vmcnt(0), draining va) once per 6 trips
+                asm volatile("" ::"v"(B.cap), "v"(B.fb));
+            }
+        }
+    } else if constexpr (PIPE == 15) {
+        // 14 with the frame bytes two trips ahead (three 4-KiB sets per wave in
+        // flight, for lower occupancy: 3 blocks/CU) and the descriptors three
+        // trips ahead.  The frame-byte sets rotate (unrolled x3, no moves); the
+        // descriptors shift down a queue by value each trip: the newest one is
+        // waited for by its move, at the end of the trip that loaded it, where
+        // only younger loads (the frame bytes issued after it) stay in flight.
+        uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                       (tid >> 6) * 256u;
+        const uint32_t lane = tid & 63u;
+        uint64_t base = (uint64_t)blockIdx.x * 256;
+        if (base < n) {
+            lane_frame L0, L1, L2, L3; // trips t .. t+3
+            uint4 va[4], vb[4], vc[4];
+            lane_desc_nb(L0, p, n, pkts, off, len, unit_log2);
+            lane_desc_nb(L1, p + stride, n, pkts, off, len, unit_log2);
+            lane_desc_nb(L2, p + 2 * stride, n, pkts, off, len, unit_log2);
+            bool c0 = lane_issue(L0, pkts, lane, va);
+            bool c1 = lane_issue(L1, pkts, lane, vb);
+            bool c2 = false;
+            // one trip: descriptors of t+3, bytes of t+2 into VN, trip t from VC
+            auto trip = [&](uint4 (&VC)[4], bool cc, uint4 (&VN)[4], bool &cn) -> bool {
+                lane_desc_nb(L3, p + 3 * stride, n, pkts, off, len, unit_log2);
+                cn = lane_issue(L2, pkts, lane, VN);
+                lane_stage(L0, VC, cc, stage, lane);
+                lane_process<ABL, ST_NT, NTL, LDT>(L0, nullptr, ft, out, counts, hist, lds_bins, lt);
+                base += stride;
+                p += stride;
+                L0 = L1;
+                L1 = L2;
+                L2 = L3;
+                return base < n;
+            };
+            for (;;) {
+                if (!trip(va, c0, vc, c2)) break; // bytes of t+2 -> vc
+                if (!trip(vb, c1, va, c0)) break; // t+3 -> va
+                if (!trip(vc, c2, vb, c1)) break; // t+4 -> vb
+            }
+        }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
         uint64_t base = (uint64_t)blockIdx.x * 256;
@@ -830,8 +1009,9 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
+    if ((PIPE == 14 || PIPE == 15) && idx) return hipErrorInvalidValue; // no index-list mode
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
-                       (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u) + (PIPE == 12 ? 16384u : 0u);
+                       (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u) + (PIPE == 12 || PIPE == 14 || PIPE == 15 ? 16384u : 0u);
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
         reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
@@ -1009,7 +1189,7 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1028,10 +1208,13 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
 
     // one 256-frame tile per trip: one trip per block on a full grid, a
-    // block-strided loop on a resident (persistent) grid
+    // block-strided loop on a resident (persistent) grid.  The full grid has
+    // no loop at all: with one, the compiler keeps the re-arm constants in a
+    // scratch spill, written once per thread = 16 B of HBM writes per frame
+    // (PMC r02g: 32 B/frame written instead of the 16-B verdict)
     const uint64_t ntiles = ((uint64_t)n + 255) / 256;
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        if (tile != blockIdx.x) { // re-arm the span state: every read of the last tile's is done
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERS ? gridDim.x : ntiles) {
+        if (PERS && tile != blockIdx.x) { // re-arm the span state: every read of the last tile's is done
             __syncthreads();
             if (tid == 0) {
                 s_lo = ~0ull;
@@ -1334,14 +1517,14 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
     if constexpr (PERS) {
         int cu = 0, occ = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), 256,
+            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS>), 256,
             (size_t)lds_bins * 4u, &cu, &occ);
         if (e != hipSuccess) return e;
         if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
         blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
     }
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -1646,6 +1829,10 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 11, launch_lane<0, 0, true, false>, 6}, // 5 without the LDS UDP table
     // 12 (first entry): 5 with coalesced LDS-staged head loads; 13: 12 without the LDS UDP table
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6},
+    // 14: 12 software-pipelined (descriptors two trips, frame bytes one trip ahead)
+    {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 3},
+    // 15: 14 with the frame bytes two trips ahead
+    {1, 4, 1, 15, launch_lane_udpc<15, 0, true, false>, 3},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},

@@ -159,6 +159,36 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
 
 
+@pytest.mark.parametrize("variant", [(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 15)])
+@pytest.mark.parametrize("n", [1, 63, 300, 70001])
+def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
+    """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
+    path), with counts: ragged bursts (a partial last wave, a partial last
+    trip of the software pipeline), waves whose slots are not consecutive
+    (two descriptors swapped: that wave takes the per-lane path), runts and a
+    caplen of 48 on a wave's last slot (the coalesced 4 KiB must stay inside
+    the buffer), all bit-exact against the oracle"""
+    cfg = rxdist.gen_cfg("cfg2")
+    pk, off, ln = R.gen_host(cfg, 5, n, 6)
+    udp, tcb = R.gen_flows(cfg)
+    ln = ln.copy()
+    off = off.copy()
+    if n > 300:
+        off[[130, 131]] = off[[131, 130]]  # wave 2 of block 0: not consecutive
+        ln[200] = 40                       # a runt inside a coalesced wave
+        ln[255] = 48                       # a wave's last slot at caplen 48
+        ln[319] = 60
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, n, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), (variant, n)
+
+
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
