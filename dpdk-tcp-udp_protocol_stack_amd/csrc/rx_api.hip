@@ -175,6 +175,31 @@ static uint32_t build_udp_port(const ft_host &u, std::vector<uint32_t> *port) {
     return dip;
 }
 
+// UDP port window (rx_common.h): the host-order port range of the sockets
+// bound to udp_dip, when it spans <= RX_UDPW_MAX_PORTS ports and the compact
+// table exists; u16 flow ids, 0xFFFF = no socket on (udp_dip, port).  Empty
+// otherwise.  *lo = its first port.
+static void build_udpw(const std::vector<uint32_t> &port, bool compact, std::vector<uint16_t> *w,
+                       uint32_t *lo) {
+    w->clear();
+    *lo = 0;
+    if (!compact || port.empty()) return;
+    uint32_t mn = 65536, mx = 0;
+    for (uint32_t r = 0; r < 65536; ++r)
+        if ((port[r] & RX_PORT_NONE) != RX_PORT_NONE) {
+            const uint32_t h = ((r & 0xFFu) << 8) | (r >> 8);
+            mn = std::min(mn, h);
+            mx = std::max(mx, h);
+        }
+    if (mn > mx || mx - mn + 1 > RX_UDPW_MAX_PORTS) return;
+    w->assign(mx - mn + 1, 0xFFFFu);
+    for (uint32_t h = mn; h <= mx; ++h) {
+        const uint32_t f = port[((h & 0xFFu) << 8) | (h >> 8)] & RX_PORT_NONE;
+        if (f != RX_PORT_NONE) (*w)[h - mn] = (uint16_t)f; // < RX_UDPC_MAX_FLOWS
+    }
+    *lo = mn;
+}
+
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -190,6 +215,10 @@ struct rxg_ctx {
     std::vector<uint32_t> h_udp_port; // UDP direct port table (empty: not built)
     uint32_t udp_dip = 0;
     uint32_t *d_udp_port = nullptr;
+    std::vector<uint16_t> h_udpw; // UDP port window (empty: not built)
+    uint32_t udpw_lo = 0;
+    uint16_t *d_udpw = nullptr;
+    size_t d_udpw_cap = 0;
     uint32_t tune_tables = 0; // rxg_tune_tables flags
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
@@ -345,6 +374,7 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_ws);
     (void)hipFree(c->d_aux);
     (void)hipFree(c->d_udpc);
+    (void)hipFree(c->d_udpw);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
     for (rxg_ctx::slot &sl : c->slots) {
         (void)hipFree(sl.d_pkts);
@@ -384,6 +414,7 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
     c->h_udp_port.clear();
     if (!ue.empty() && !(c->tune_tables & RXG_TT_NO_UDP_PORT))
         c->udp_dip = build_udp_port(c->h_udp, &c->h_udp_port);
+    build_udpw(c->h_udp_port, !c->h_udpc.empty(), &c->h_udpw, &c->udpw_lo);
     c->h_listen.assign(65536, RXG_FLOW_NONE);
     for (uint32_t i = 0; i < nt; ++i)
         if (t[i].status == RXG_TCP_STATUS_LISTEN) c->h_listen[t[i].dport] = i;
@@ -423,6 +454,17 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
                          hipMemcpyHostToDevice));
         c->ft.udp_port = c->d_udp_port;
         c->ft.udp_dip = c->udp_dip;
+    }
+    c->ft.udpw = nullptr;
+    c->ft.udpw_lo = c->ft.udpw_n = 0;
+    if (!c->h_udpw.empty()) {
+        if ((rc = ensure_dev((void **)&c->d_udpw, &c->d_udpw_cap, c->h_udpw.size() * sizeof(uint16_t))))
+            return rc;
+        HIPCHK(hipMemcpy(c->d_udpw, c->h_udpw.data(), c->h_udpw.size() * sizeof(uint16_t),
+                         hipMemcpyHostToDevice));
+        c->ft.udpw = c->d_udpw;
+        c->ft.udpw_lo = c->udpw_lo;
+        c->ft.udpw_n = (uint32_t)c->h_udpw.size();
     }
     c->ft.udp = c->d_udp;
     c->ft.tcp = c->d_tcp;

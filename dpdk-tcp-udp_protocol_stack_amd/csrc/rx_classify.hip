@@ -557,7 +557,8 @@ __device__ __forceinline__ void lane_stage(lane_frame &L, const uint4 (&v)[4], b
 // 16-B verdict and the per-flow count slot (~0u = not counted).
 template <int ABL = 0, bool NTL = true, bool LDT = false>
 __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, const rx_ft_dev &ft,
-                                              uint32_t *count_idx, const uint2 *lt = nullptr) {
+                                              uint32_t *count_idx, const uint2 *lt = nullptr,
+                                              const uint16_t *lw = nullptr) {
     const int32_t cp = L.cap;
     if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
 #pragma unroll
@@ -640,13 +641,19 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
     if (ABL & 1) {
         flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
     } else if (LDT && probe && is_udp) { // compact UDP table in LDS
-        uint32_t i = rx_hash3(dip, dport, 17u) & ft.udpc_mask;
-        for (uint32_t pr = 0; pr < ft.udpc_probe; ++pr, i = (i + 1) & ft.udpc_mask) {
-            const uint2 sl = lt[i];
-            if (sl.y == 0xFFFFFFFFu) break;
-            if (sl.x == dip && (sl.y & 0xFFFFu) == dport) {
-                flow = sl.y >> 16;
-                break;
+        const uint32_t k = rx_bswap16(dport) - ft.udpw_lo;
+        if (dip == ft.udp_dip && k < ft.udpw_n) { // the port window decides (one LDS read)
+            const uint32_t e = lw[k];
+            flow = e == 0xFFFFu ? RXG_FLOW_NONE : e;
+        } else {
+            uint32_t i = rx_hash3(dip, dport, 17u) & ft.udpc_mask;
+            for (uint32_t pr = 0; pr < ft.udpc_probe; ++pr, i = (i + 1) & ft.udpc_mask) {
+                const uint2 sl = lt[i];
+                if (sl.y == 0xFFFFFFFFu) break;
+                if (sl.x == dip && (sl.y & 0xFFFFu) == dport) {
+                    flow = sl.y >> 16;
+                    break;
+                }
             }
         }
     } else if (probe) {
@@ -728,9 +735,9 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
                                              const rx_ft_dev &ft, uint4 *__restrict__ out,
                                              unsigned long long *__restrict__ counts,
                                              uint32_t *hist, uint32_t lds_bins,
-                                             const uint2 *lt = nullptr) {
+                                             const uint2 *lt = nullptr, const uint16_t *lw = nullptr) {
     uint32_t idx;
-    const uint4 v = lane_verdict<ABL, NTL, LDT>(L, next, ft, &idx, lt);
+    const uint4 v = lane_verdict<ABL, NTL, LDT>(L, next, ft, &idx, lt, lw);
     if (L.valid) {
         if (ABL & 4)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
@@ -756,12 +763,16 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     static_assert(!LDT || PIPE == 0 || PIPE >= 12, "LDS table: PIPE 0 / 12 / 14 / 15 only");
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
+    // the port window after the compact table, then (PIPE 12/14/15) the stage
+    uint16_t *lw = reinterpret_cast<uint16_t *>(lt + (LDT ? ft.udpc_mask + 1u : 0u));
+    const uint32_t lw_words = LDT ? ((ft.udpw_n + 7u) & ~7u) / 2u : 0u; // 16-B multiple
     if (n_dev) n = min(n, *n_dev); // index-list mode: the list length lives on the device
     const uint32_t tid = threadIdx.x;
     if constexpr (LDT) {
         const uint32_t q = (ft.udpc_mask + 1) / 2; // 16-B pieces
         for (uint32_t i = tid; i < q; i += 256)
             reinterpret_cast<uint4 *>(lt)[i] = reinterpret_cast<const uint4 *>(ft.udpc)[i];
+        for (uint32_t i = tid; i < ft.udpw_n; i += 256) lw[i] = ft.udpw[i];
     }
     if (lds_bins) {
         for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
@@ -805,13 +816,13 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             lane_frame L;
             lane_desc(L, p, n, pkts, off, len, unit_log2, idx);
             lane_load<NTL>(L);
-            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
+            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
         }
     } else if constexpr (PIPE == 12) {
         // as 0, but a wave whose 64 frames fill consecutive 64-B slots loads
         // them coalesced through its LDS stage (lane_load_staged)
         uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
-                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
                        (tid >> 6) * 256u;
         const uint32_t lane = tid & 63u;
         for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
@@ -827,7 +838,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_load_staged(L, pkts + f0, stage, lane);
             else
                 lane_load<NTL>(L);
-            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt);
+            lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
         }
     } else if constexpr (PIPE == 14) {
         // 12, software-pipelined: descriptors two trips ahead, frame bytes one
@@ -842,7 +853,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
         // register moves are needed (a move would wait for the load it
         // copies).
         uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
-                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
                        (tid >> 6) * 256u;
         const uint32_t lane = tid & 63u;
         uint64_t base = (uint64_t)blockIdx.x * 256;
@@ -857,7 +868,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(B, pkts, lane, vb);
                 lane_stage(A, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -865,7 +876,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(D, pkts, lane, va);
                 lane_stage(B, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -873,7 +884,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(A, pkts, lane, vb);
                 lane_stage(D, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -881,7 +892,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(B, pkts, lane, va);
                 lane_stage(A, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -889,7 +900,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(D, pkts, lane, vb);
                 lane_stage(B, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -897,7 +908,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(A, pkts, lane, va);
                 lane_stage(D, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -917,7 +928,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
         // waited for by its move, at the end of the trip that loaded it, where
         // only younger loads (the frame bytes issued after it) stay in flight.
         uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
-                                                 (LDT ? 2u * (ft.udpc_mask + 1u) : 0u)) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
                        (tid >> 6) * 256u;
         const uint32_t lane = tid & 63u;
         uint64_t base = (uint64_t)blockIdx.x * 256;
@@ -935,7 +946,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(L3, p + 3 * stride, n, pkts, off, len, unit_log2);
                 cn = lane_issue(L2, pkts, lane, VN);
                 lane_stage(L0, VC, cc, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(L0, nullptr, ft, out, counts, hist, lds_bins, lt);
+                lane_process<ABL, ST_NT, NTL, LDT>(L0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 L0 = L1;
@@ -1011,7 +1022,8 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
     if ((PIPE == 14 || PIPE == 15) && idx) return hipErrorInvalidValue; // no index-list mode
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
-                       (LDT ? (size_t)(ft.udpc_mask + 1) * 8u : 0u) + (PIPE == 12 || PIPE == 14 || PIPE == 15 ? 16384u : 0u);
+                       (LDT ? (size_t)(ft.udpc_mask + 1) * 8u + ((ft.udpw_n + 7u) & ~7u) * 2u : 0u) +
+                       (PIPE == 12 || PIPE == 14 || PIPE == 15 ? 16384u : 0u);
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
         reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
@@ -1531,6 +1543,335 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 }
 
 // ---------------------------------------------------------------------------
+// Stream-heads kernel (pipes 44/45): the stream kernel without its head phase.
+//   The block's span now covers every captured byte of its 256 frames (chunks
+//   [off, off + len) rounded out to 16 B), known from the descriptors alone, so
+//   the first tail tile is issued one HBM round trip after the descriptors
+//   instead of two (descriptor -> head -> span).  Each tile's 16-B chunks pass
+//   through an LDS copy of the tile (double-buffered) besides the chunk-sum
+//   scan; a frame's owner thread picks its four head chunks out of the tile
+//   they arrive in, parses the headers there, and from then on knows its
+//   checksum end e and reads the prefix sums at its tail boundaries (byte 64,
+//   e & ~15) and its last partial chunk from the tiles that hold them: both lie
+//   in the head's tile or a later one.  The frame heads are read once (with
+//   the stream, coalesced) instead of once per thread plus again inside the
+//   span.  The flow probe runs after the stream (stream kernel HO = 2).  A
+//   block whose span is far larger than its frames (scattered frames) loads
+//   heads and tails per thread instead.  TC = chunks per tile (16 KiB at
+//   1024); the LDS copy costs 2 x 16 B x TC.
+template <uint32_t TC, bool NTS>
+__global__ __launch_bounds__(256) void rx_classify_sh_kernel(
+    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
+    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    constexpr uint32_t LPT = TC / 256; // 16-B chunks per thread per tile
+    static_assert(LPT >= 1 && LPT <= 4 && TC % 256 == 0, "tile shape");
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    __shared__ __attribute__((aligned(16))) uint4 s_tile[2][TC];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TC];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16];
+    __shared__ unsigned long long s_lo, s_hi;
+    __shared__ uint32_t s_tail;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (tid == 0) {
+        s_lo = ~0ull;
+        s_hi = 0;
+        s_tail = 0;
+    }
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
+    const bool valid = p < n;
+    const uint64_t q = valid ? p : 0;
+    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
+    const uint8_t *fb = pkts + fpos;
+    const int32_t cp = valid ? (int32_t)len[q] : 0;
+    const uint64_t c0_abs = fpos >> 4, c1_abs = (fpos + (uint32_t)cp + 15u) >> 4;
+    __syncthreads(); // s_lo/s_hi/s_tail initialised
+    if (cp > 0) {
+        atomicMin(&s_lo, (unsigned long long)c0_abs);
+        atomicMax(&s_hi, (unsigned long long)c1_abs);
+        atomicAdd(&s_tail, (uint32_t)(c1_abs - c0_abs));
+    }
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    const uint32_t tsum = s_tail;
+    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + TC && hi - lo < (1ull << 26);
+
+    // ---- header decode (once the head's four chunks are in c) ---------------
+    uint4 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = make_uint4(0, 0, 0, 0);
+    uint32_t cl = RXG_CLS_NON_IP, nd = 14, tl = 0, proto = 0, sip = 0, dip = 0, sport = 0,
+             dport = 0, dgl = 0, hl = 0, acc = 0, stored = 0;
+    int32_t e = 0, ef = 0;
+    bool is_udp = false, is_tcp = false, l4 = false, do_sum = false, part = false, tail = false;
+    auto parse = [&]() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
+        const uint32_t et = c[0].w & 0xFFFFu;
+        tl = rx_bswap16(c[1].x & 0xFFFFu);
+        proto = c[1].y >> 24;
+        sip = (c[1].z >> 16) | (c[1].w << 16);
+        dip = (c[1].w >> 16) | (c[2].x << 16);
+        sport = c[2].x >> 16;
+        dport = c[2].y & 0xFFFFu;
+        dgl = rx_bswap16(c[2].y >> 16);
+        hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+        if (et == 0x0608u) {
+            cl = RXG_CLS_ARP;
+            nd = 42;
+        } else if (et != 0x0008u) {
+            cl = RXG_CLS_NON_IP;
+            nd = 14;
+        } else if (proto == 17u) {
+            cl = RXG_CLS_UDP;
+            nd = 42;
+        } else if (proto == 6u) {
+            cl = RXG_CLS_TCP;
+            nd = 54;
+        } else {
+            cl = RXG_CLS_IPV4_OTHER;
+            nd = 24;
+        }
+        is_udp = cl == RXG_CLS_UDP;
+        is_tcp = cl == RXG_CLS_TCP;
+        l4 = is_udp || is_tcp;
+        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+        do_sum = l4 && tl >= 20u;
+        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+        e = do_sum ? 34 + (int32_t)l4n : 0;
+        if (e > cp) e = cp;
+        ef = e & ~15; // full tail chunks: [64, ef)
+        part = ef < e && ef >= 64;
+        tail = ef > 64;
+        uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+        h1.x = 0;
+        h1.y = 0;
+        h1.z &= 0xFFFF0000u;
+        if (is_udp) h2.z &= 0xFFFF0000u;
+        if (is_tcp) h3.x &= 0x0000FFFFu;
+        acc = lane_chunk_sum(0u, h1, 16, e);
+        acc = lane_chunk_sum(acc, h2, 32, e);
+        acc = lane_chunk_sum(acc, h3, 48, e);
+        if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
+        stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+    };
+
+    // the flow probe's first reads (the port-table / listener entry and the
+    // hashed table's home slot), issued as soon as the head is parsed and
+    // consumed after the stream, so their latency hides behind it
+    const bool udp_tab = ft.udp_port != nullptr;
+    uint32_t pe = 0;
+    uint4 sl0 = make_uint4(0, 0, 0, 0);
+    auto probe_issue = [&]() {
+        const bool pr = valid && (is_udp || is_tcp);
+        const uint32_t *ptab = is_udp && udp_tab ? ft.udp_port : ft.listen;
+        pe = ptab[pr ? dport : 0u];
+        const bool h0 = pr && !(is_udp && udp_tab) && (is_udp ? ft.udp_probe : ft.tcp_probe) > 0;
+        const uint32_t ka = is_udp ? dip : sip, kb = is_udp ? dport : dip;
+        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+        const uint4 *sp = h0 ? (is_udp ? ft.udp : ft.tcp) +
+                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                             : reinterpret_cast<const uint4 *>(pkts);
+        sl0 = ld_slot(sp);
+    };
+    uint4 pc = make_uint4(0, 0, 0, 0); // the last partial chunk [ef, e)
+    uint32_t es = 0, ee = 0;          // prefix sums at the tail's first and end chunk
+    if (streamed) {
+        const uint32_t span = (uint32_t)(hi - lo);
+        const uint8_t *sb = pkts + (lo << 4);
+        const uint32_t hs = cp > 0 ? (uint32_t)(c0_abs - lo) : 0xFFFFFFFFu; // head chunk 0
+        const uint32_t nh = cp >= 64 ? 4u : ((uint32_t)cp + 15u) >> 4;     // head chunks present
+        uint32_t need = (1u << nh) - 1u; // head chunks still to arrive
+        bool parsed = false;
+        uint32_t ts = 0xFFFFFFFFu, te = 0xFFFFFFFFu; // tail chunks [ts, te); te = partial chunk
+        if (valid && need == 0) { // caplen 0: nothing to wait for
+            parse();
+            probe_issue();
+            parsed = true;
+        }
+        auto tile_load = [&](uint4 *v, uint32_t c0) {
+#pragma unroll
+            for (int j = 0; j < (int)LPT; ++j) {
+                const uint32_t k = c0 + j * 256 + tid;
+                v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
+            }
+        };
+        uint32_t carry = 0;
+        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
+            uint32_t sj[LPT], xj[LPT];
+#pragma unroll
+            for (int j = 0; j < (int)LPT; ++j) {
+                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
+                xj[j] = wave_incl_scan(sj[j]);
+                s_tile[buf][j * 256 + tid] = v[j];
+            }
+            if (lane == 63) {
+#pragma unroll
+                for (int j = 0; j < (int)LPT; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+            }
+            __syncthreads();
+            uint32_t wt[LPT * 4]; // block-uniform: kept in SGPRs
+#pragma unroll
+            for (int j = 0; j < (int)LPT; ++j) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
+                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
+                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
+                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
+                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
+            }
+            uint32_t base = carry;
+#pragma unroll
+            for (int j = 0; j < (int)LPT; ++j) {
+                uint32_t wb = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
+                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
+                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
+            }
+            carry = base;
+            __syncthreads();
+            // this thread's frame: head chunks that arrived in this tile, then
+            // (once parsed) its tail boundaries and partial chunk
+            if (need) {
+#pragma unroll
+                for (uint32_t h = 0; h < 4; ++h)
+                    if (((need >> h) & 1u) && hs + h - c0 < TC) {
+                        c[h] = s_tile[buf][hs + h - c0];
+                        need &= ~(1u << h);
+                    }
+                if (!need) {
+                    parse();
+                    probe_issue();
+                    parsed = true;
+                    ts = hs + 4u;
+                    te = hs + ((uint32_t)ef >> 4);
+                }
+            }
+            if (parsed) {
+                if (tail && ts - c0 < TC) es = s_pre[buf][ts - c0];
+                if (tail && te - c0 < TC) ee = s_pre[buf][te - c0];
+                if (part && te - c0 < TC) pc = s_tile[buf][te - c0];
+            }
+        };
+        // unrolled twice: the A/B tiles swap roles without register moves
+        uint4 va[LPT], vb[LPT];
+        tile_load(va, 0);
+        for (uint32_t c0 = 0; c0 < span; c0 += 2 * TC) {
+            tile_load(vb, c0 + TC);
+            tile(va, c0, 0);
+            tile_load(va, c0 + 2 * TC);
+            tile(vb, c0 + TC, 1);
+        }
+        if (tail && te == span) ee = carry; // a tail ending at the span's end
+        if (tail) acc += ee - es;
+    } else if (valid) { // scattered frames: this thread loads its own head and tail
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
+        parse();
+        probe_issue();
+        pc = ldg16<false>(fb + (part ? ef : 0));
+        for (int32_t s = 64; s < ef; s += 64) {
+            uint4 r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = ldg16<false>(fb + (s + 16 * u < ef ? s + 16 * u : 0));
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (s + 16 * u < ef) acc += chunk_sum(r[u]);
+        }
+    }
+    if (part) acc = lane_chunk_sum(acc, pc, ef, e);
+
+    // ---- flow probe and verdict (as the stream kernel) ------------------------
+    uint32_t flags = 0, poff = 0, plen = 0;
+    if (is_udp) {
+        poff = 42;
+        plen = dgl > 8u ? dgl - 8u : 0u;
+        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+    } else if (is_tcp) {
+        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+        poff = 34u + 4u * hl;
+        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+        plen = pl < 0 ? 0u : (uint32_t)pl;
+    }
+    const bool trunc = (int32_t)nd > cp;
+    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
+    uint32_t ck = 0;
+    if (do_sum) {
+        ck = (~fold16(acc)) & 0xFFFFu;
+        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+    }
+    const bool ok = l4 && stored == ck;
+    // UDP always; TCP only with a good checksum (the reference looks nothing
+    // up for a bad one)
+    const bool probe = valid && (is_udp || (is_tcp && ok));
+    const uint32_t ka = is_udp ? dip : sip;
+    const uint32_t kb = is_udp ? dport : dip;
+    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+    const bool udp_port = is_udp && udp_tab;
+    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+    uint32_t flow = RXG_FLOW_NONE;
+    bool hashed = probe && maxp > 0;
+    if (hashed && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
+    if (hashed) {
+        const uint4 *tb = is_udp ? ft.udp : ft.tcp;
+        const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
+        uint32_t pj = rx_hash3(ka, kb, kc) & mk;
+        for (uint32_t pr = 0; pr < maxp; ++pr, pj = (pj + 1) & mk) {
+            // the home slot came with the head (a UDP key on a flagged port:
+            // loaded now)
+            const uint4 sl = pr == 0 && !udp_port ? sl0 : ld_slot(tb + pj);
+            if (sl.w == RX_SLOT_EMPTY) break;
+            if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                flow = sl.w;
+                break;
+            }
+        }
+    }
+    if (is_tcp && probe && flow == RXG_FLOW_NONE) flow = pe; // listener (tcp_stream_search pass 2)
+    int32_t rc = RXG_RC_KNI;
+    if (is_udp)
+        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                   : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+    else if (is_tcp)
+        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+    if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+    if (valid) {
+        uint4 vd;
+        vd.x = flow;
+        vd.y = (poff & 0xFFFFu) | (plen << 16);
+        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+        stg16(&out[p], vd);
+        const uint32_t cidx =
+            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+        lane_count(cidx, counts, hist, lds_bins);
+        if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
+    }
+    if (lds_bins) {
+        __syncthreads();
+        for (uint32_t i = tid; i < lds_bins; i += 256) {
+            const uint32_t cnt = hist[i];
+            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
+        }
+    }
+}
+
+template <uint32_t TC, bool NTS = true>
+hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                     unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                     const uint32_t *, const uint32_t *) {
+    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rx_classify_sh_kernel<TC, NTS>), dim3((uint32_t)blocks), dim3(256),
+                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
+                       lds_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
 // memory-side request): the classify kernel writes one count index per frame
@@ -1875,6 +2216,9 @@ static const variant_entry k_variants[] = {
     // 42/43: pipes 38/39 on a resident grid (blocks loop over tiles)
     {0, 1, 1, 42, launch_stream<true, 0, 3, 1, true, true>},
     {0, 1, 1, 43, launch_stream<true, 0, 0, 1, true, true>},
+    // 44/45: stream-heads kernel (heads picked out of an LDS copy of the
+    // stream), 16-KiB / 8-KiB tiles
+    {0, 1, 1, 44, launch_sh<1024>}, {0, 1, 1, 45, launch_sh<512>},
 };
 
 } // namespace
@@ -1885,8 +2229,10 @@ static const variant_entry k_variants[] = {
 // choice only moves speed.
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
     if (len_hint == 0) len_hint = 1518;
-    if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b)
-        *g = 1, *p = 4, *fpg = 1, *pipe = 12;
+    if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b),
+        // software-pipelined one trip ahead at 3 blocks/CU (pipe 14: 0.2487-0.2506 vs 0.2641-0.2660
+        // ms for pipe 12, with and without counts; pipe 15, two trips ahead: 0.2607; r02i)
+        *g = 1, *p = 4, *fpg = 1, *pipe = 14;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel, flow probe after the
         // tail stream at 5 blocks/CU (HO = 3): 1-3% ahead of pipe 30 in every interleaved
         // sweep (r01g: 1.184 vs 1.194, 1.177 vs 1.211, 1.305 vs 1.319 ms); one barrier per

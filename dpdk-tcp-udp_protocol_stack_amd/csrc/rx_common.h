@@ -40,6 +40,12 @@ struct rx_ft_dev {
     // the host's own); see rx_udp_port_decide
     const uint32_t *udp_port;
     uint32_t udp_dip;
+    // UDP port window (null: not built), with the compact table only: u16
+    // flow ids (0xFFFF = none) of the sockets bound to udp_dip on host-order
+    // ports [udpw_lo, udpw_lo + udpw_n), copied into LDS beside the compact
+    // table so such keys are decided by one LDS read instead of a probe loop
+    const uint16_t *udpw;
+    uint32_t udpw_lo, udpw_n;
     // per-launch output, set by rx_classify_launch on its copy: on the slab
     // count path every kernel writes frame i's count index (UDP flow k -> k,
     // TCP flow k -> nu + k; all ones = not counted) to count_idx[i], which
@@ -76,6 +82,7 @@ RX_HD bool rx_udp_port_decide(uint32_t e, uint32_t dip, uint32_t udp_dip, uint32
     return true;
 }
 #define RX_UDPC_MAX_FLOWS 1024u // load <= 1/2: <= 2048 slots = 16 KiB of LDS
+#define RX_UDPW_MAX_PORTS 4096u // port window: <= 8 KiB of LDS
 #define RX_FT_LOAD_LOG2 2u      // exact-key tables: load <= 1/4 by default (rxg_tune_flow_load)
 
 // Host: CU count of the calling thread's current device and the resident

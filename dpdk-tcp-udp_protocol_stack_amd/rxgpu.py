@@ -63,7 +63,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
-                   (0, 0, 0, 42), (0, 0, 0, 43)]  # the same on a resident grid
+                   (0, 0, 0, 42), (0, 0, 0, 43),  # the same on a resident grid
+                   (0, 0, 0, 44), (0, 0, 0, 45)]  # stream-heads kernel, 16-/8-KiB tiles
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

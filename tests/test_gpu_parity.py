@@ -189,9 +189,60 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
+@pytest.mark.parametrize("variant", [(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
+                                     (1, 4, 1, 15), (0, 0, 0, 20)])
+@pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
+def test_udp_port_window(ctx, torch_dev, variant, tables):
+    """small UDP socket sets (the compact LDS table) with the LDS port window:
+    keys on the main address inside the window (bound, unbound, rebound:
+    newest wins), outside it, on another address sharing window ports, and on
+    an address with no socket; 64-B slotted frames (coalesced lane path) and
+    a few longer ones; verdicts and counts bit-exact against the oracle, with
+    the window (tables 0) and without the port tables (NO_UDP_PORT)"""
+    L, L2, L3 = "192.168.100.77", "10.9.9.9", "172.16.0.1"
+    socks = [(L, 30000 + 3 * k) for k in range(300)]        # window 30000..30897
+    socks += [(L2, 30000 + 21 * k) for k in range(20)]      # another address, shared ports
+    socks += [(L, 30000 + 30 * k) for k in range(10)]       # rebinds: newest wins
+    socks += [(L, 40000), (L2, 5555)]
+    udp = np.zeros(len(socks), R.UDP_SOCK_DTYPE)
+    for i, (ip, port) in enumerate(socks):
+        udp[i] = (R.ip_raw(ip), R.port_raw(port), 17)
+    tcb = np.zeros(0, R.TCB_DTYPE)
+    rng = np.random.default_rng(7)
+    frames = []
+    for i in range(5000):
+        r = rng.integers(0, 8)
+        if r < 4:
+            dst, port = L, 30000 + int(rng.integers(0, 900))
+        elif r == 4:
+            dst, port = L, int(rng.choice([40000, 29999, 30900, 50000]))
+        elif r == 5:
+            dst, port = L2, 30000 + 21 * int(rng.integers(0, 25))
+        elif r == 6:
+            dst, port = L2, int(rng.choice([5555, 30003, 20000]))
+        else:
+            dst, port = L3, 30000 + 3 * int(rng.integers(0, 300))
+        pay = b"x" * (14 if i % 97 else 300)
+        frames.append(F.udp_frame("10.0.0.1", 1000 + i % 50000, dst, port, pay))
+    buf, off, lens = F.pack_frames(frames, 6)
+    ctx.tune_tables(tables)
+    try:
+        ctx.flows_sync(udp, tcb)
+        want, wcnt = O.Tables(udp, tcb).classify(buf, off, lens, 6, counts=True)
+        ctx.tune(*variant)
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 6, 64, counts=True)
+    finally:
+        ctx.tune(0)
+        ctx.tune_tables(0)
+    assert got.tobytes() == want.tobytes(), (variant, tables, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), (variant, tables)
+    assert (want["rc"] == 0).sum() > 1000 and (want["rc"] == -3).sum() > 500
+
+
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
+                                     (0, 0, 0, 44), (0, 0, 0, 45),
                                      (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor

@@ -1,0 +1,18 @@
+#!/bin/bash
+# r02l: LDS port window (cfg2 lane pipes), stream-heads kernel with early
+# probe loads (cfg4/cfg5); SQ counters of the cfg2 default again
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+step() { local name=$1 t=$2; shift 2; echo "== $name: $*"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n 30 "$OUT/$name.log"; return $rc; }
+step pytest_gpu 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
+step sweep2 300 python bench.py --sweep cfg2 --sweep-counts --steps 20 --warmup 5 \
+    --sweep-variants '1,4,1,12;1,4,1,14,3;1,4,1,14,4;1,4,1,15,3' || exit $?
+step sweep45 400 python bench.py --sweep cfg4,cfg5 --sweep-counts --steps 10 --warmup 3 \
+    --sweep-variants '0,0,0,38;0,0,0,44;0,0,0,45' || exit $?
+export TMPDIR=/tmp
+step sq2 200 python tools/pmc_counters.py sq cfg2 "--no-tx --no-cfg1" \
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+    "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" || exit $?
+echo ALLDONE

@@ -1,0 +1,119 @@
+// membw_cfg2.hip — the cfg2 byte pattern with no per-frame work (diagnostics
+// only; not part of the product): 16M 64-B frames back to back (1 GiB), their
+// descriptors (u32 offset + u16 length: 96 MiB) and one 16-B store per frame
+// (256 MiB) — the ceiling the lane kernel's 1.44 GB per launch can reach.
+//   hipcc --offload-arch=gfx950 -O3 tools/membw_cfg2.hip -o tools/membw_cfg2 && tools/membw_cfg2
+// Variants: R = frames only; RD = frames + descriptors; RDW = + 16-B nt store
+// per frame; RDWp = the same with plain stores.  U = frames per thread per
+// trip (loads of all U in flight before any is consumed).  Grid = blocks/CU x
+// CUs (resident), grid-stride over 256-frame tiles.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CHK(x)                                                                                     \
+    do {                                                                                           \
+        hipError_t e = (x);                                                                        \
+        if (e != hipSuccess) {                                                                     \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);                        \
+            exit(1);                                                                               \
+        }                                                                                          \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE, int U> // MODE 0 = R, 1 = RD, 2 = RDW (nt store), 3 = RDW (plain store)
+__global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
+                                              const unsigned *__restrict__ off,
+                                              const unsigned short *__restrict__ len, size_t n,
+                                              u32x4 *__restrict__ out, unsigned *__restrict__ sink) {
+    const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t t0 = (size_t)blockIdx.x * 256 * U; t0 < n; t0 += stride) {
+        u32x4 v[U][4];
+        unsigned o[U], l[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t f = t0 + (size_t)u * 256 + threadIdx.x; // this lane's frame
+            const size_t fq = f < n ? f : 0;
+            const size_t w0 = t0 + (size_t)u * 256 + wv * 64; // the wave's first frame
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { // the wave's 4 KiB, coalesced
+                const size_t c = w0 * 4 + q * 64 + lane;
+                v[u][q] = __builtin_nontemporal_load(fr + (c < n * 4 ? c : 0));
+            }
+            if (MODE >= 1) {
+                o[u] = off[fq];
+                l[u] = len[fq];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t f = t0 + (size_t)u * 256 + threadIdx.x;
+            u32x4 r = v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+            if (MODE >= 1) r.x += o[u], r.y += l[u];
+            if (MODE >= 2 && f < n) {
+                if (MODE == 2)
+                    __builtin_nontemporal_store(r, out + f);
+                else
+                    out[f] = r;
+            } else {
+                acc += r.x ^ r.y ^ r.z ^ r.w;
+            }
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int MODE, int U>
+static void run(const char *name, const u32x4 *fr, const unsigned *off, const unsigned short *len,
+                size_t n, u32x4 *out, unsigned *sink, int cu, int bpc, double bytes) {
+    const int grid = cu * bpc;
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_cfg2<MODE, U>), dim3(grid), dim3(256), 0, 0, fr, off, len, n, out, sink);
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    const int reps = 50;
+    CHK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((k_cfg2<MODE, U>), dim3(grid), dim3(256), 0, 0, fr, off, len, n, out, sink);
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    printf("%-5s U=%d bpc=%d: %.4f ms  %.0f GB/s (of the bytes this variant moves)\n", name, U, bpc,
+           ms, bytes / ms / 1e6);
+}
+
+int main() {
+    const size_t n = 16ull << 20;
+    u32x4 *fr, *out;
+    unsigned *off, *sink;
+    unsigned short *len;
+    CHK(hipMalloc(&fr, n * 64));
+    CHK(hipMalloc(&out, n * 16));
+    CHK(hipMalloc(&off, n * 4));
+    CHK(hipMalloc(&len, n * 2));
+    CHK(hipMalloc(&sink, 4));
+    CHK(hipMemset(fr, 1, n * 64));
+    CHK(hipMemset(off, 0, n * 4));
+    CHK(hipMemset(len, 0, n * 2));
+    int dev = 0, cu = 0;
+    CHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev));
+    const double r = n * 64.0, d = n * 6.0, w = n * 16.0;
+    // warm the clocks
+    for (int i = 0; i < 200; ++i) hipLaunchKernelGGL((k_cfg2<2, 2>), dim3(cu * 4), dim3(256), 0, 0, fr, off, len, n, out, sink);
+    CHK(hipDeviceSynchronize());
+    for (int bpc : {2, 3, 4, 6, 8}) {
+        run<0, 1>("R", fr, off, len, n, out, sink, cu, bpc, r);
+        run<0, 2>("R", fr, off, len, n, out, sink, cu, bpc, r);
+        run<1, 2>("RD", fr, off, len, n, out, sink, cu, bpc, r + d);
+        run<2, 1>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+        run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+        run<2, 4>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+        run<3, 2>("RDWp", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+    }
+    printf("(cfg2 algorithmic bytes per launch: %.3f GB)\n", (r + d + w) / 1e9);
+    return 0;
+}
