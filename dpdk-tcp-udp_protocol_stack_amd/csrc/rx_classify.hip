@@ -1165,7 +1165,6 @@ static hipError_t launch_binned(const uint8_t *pkts, const uint32_t *off, const 
 //   is far larger than its tails (frames scattered over the buffer) falls back
 //   to per-thread tail loops: correct for any layout, fast for ordered ones
 //   (packed bursts, fixed slots).
-constexpr uint32_t ST_TILE = 1024; // chunks per block trip (16 KiB)
 
 // inclusive prefix sum over the 64 lanes of a wave
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -1176,6 +1175,40 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1,3
     x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2,3
     return x;
+}
+
+// four independent inclusive scans, step-interleaved: each DPP step of one
+// row reads a register the previous VALU op did not write, so the DPP
+// read-after-write wait states (s_nop) of a single scan disappear
+__device__ __forceinline__ void wave_incl_scan4(uint32_t (&x)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x111, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x112, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x114, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x118, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x142, 0xA, 0xF, false);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x143, 0xC, 0xF, false);
+}
+
+template <int N>
+__device__ __forceinline__ void wave_incl_scan_n(uint32_t (&x)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x111, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x112, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x114, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x118, 0xF, 0xF, true);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x142, 0xA, 0xF, false);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x143, 0xC, 0xF, false);
 }
 
 __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
@@ -1201,17 +1234,22 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false>
-__global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
+          bool DS = false, int LPT = 4>
+__global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][ST_TILE];
-    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16]; // [row j][wave w]
+    // LPT = 16-B chunks per thread per tail tile: TCH = 256 * LPT chunks per tile
+    constexpr uint32_t TCH = 256u * LPT;
+    static_assert(LPT == 4 || LPT == 8, "tile shape");
+    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
     __shared__ unsigned long long s_lo, s_hi;
     __shared__ uint32_t s_tail;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv); // wave-uniform: SALU selects
     if (tid == 0) {
         s_lo = ~0ull;
         s_hi = 0;
@@ -1246,6 +1284,41 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
         uint4 c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
+        // block span of the tail chunks (below); DS: from the descriptors alone,
+        // bytes [64, caplen) of every frame rounded out to 16 B (a superset of
+        // the checksummed tails), so the first tiles go out while the heads are
+        // still in flight instead of one HBM round trip after them
+        uint64_t lo = 0, hi = 0;
+        uint32_t tsum = 0, span = 0;
+        bool streamed = false;
+        const uint8_t *sb = fb;
+        auto tile_load = [&](uint4 *v, uint32_t c0) {
+#pragma unroll
+            for (int j = 0; j < LPT; ++j) {
+                const uint32_t k = c0 + j * 256 + tid;
+                v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
+            }
+        };
+        auto span_of = [&]() { // a span far larger than the tails means scattered frames
+            streamed = hi > lo && hi - lo <= 2ull * tsum + TCH && hi - lo < (1ull << 26);
+            span = streamed ? (uint32_t)(hi - lo) : 0u;
+            // (not streamed: loads of the thread's own frame head, never consumed)
+            sb = streamed ? pkts + (lo << 4) : fb;
+        };
+        uint4 va[LPT], vb[LPT];
+        if constexpr (DS) {
+            const uint64_t ds_cs = (fpos + 64) >> 4, ds_ce = (fpos + (uint32_t)cp + 15u) >> 4;
+            __syncthreads(); // s_lo/s_hi/s_tail initialised
+            if (cp > 64) {
+                atomicMin(&s_lo, (unsigned long long)ds_cs);
+                atomicMax(&s_hi, (unsigned long long)ds_ce);
+                atomicAdd(&s_tail, (uint32_t)(ds_ce - ds_cs));
+            }
+            __syncthreads();
+            lo = s_lo, hi = s_hi, tsum = s_tail;
+            span_of();
+            tile_load(va, 0);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
         const uint32_t et = c[0].w & 0xFFFFu;
@@ -1323,26 +1396,17 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
 
         // block span of the tail chunks; a span far larger than the tails means
         // scattered frames (per-thread fallback below)
-        __syncthreads(); // s_lo/s_hi/s_tail initialised
-        if (tail) {
-            atomicMin(&s_lo, (unsigned long long)cs_abs);
-            atomicMax(&s_hi, (unsigned long long)ce_abs);
-            atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
-        }
-        __syncthreads();
-        const uint64_t lo = s_lo, hi = s_hi;
-        const uint32_t tsum = s_tail;
-        const bool streamed = hi > lo && hi - lo <= 2ull * tsum + ST_TILE && hi - lo < (1ull << 26);
-        const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
-        // (not streamed: loads of the thread's own frame head, never consumed)
-        const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
-        auto tile_load = [&](uint4 *v, uint32_t c0) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = c0 + j * 256 + tid;
-                v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
+        if constexpr (!DS) {
+            __syncthreads(); // s_lo/s_hi/s_tail initialised
+            if (tail) {
+                atomicMin(&s_lo, (unsigned long long)cs_abs);
+                atomicMax(&s_hi, (unsigned long long)ce_abs);
+                atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
             }
-        };
+            __syncthreads();
+            lo = s_lo, hi = s_hi, tsum = s_tail;
+            span_of();
+        }
         if (part) acc = lane_chunk_sum(acc, pc, ef, e);
 
         // every verdict field that does not depend on the flow: payload offset and
@@ -1402,10 +1466,9 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                                            : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
             if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
         };
-        uint4 va[4], vb[4];
         if constexpr (HO == 0) probe_flow();
         // ---- tail phase -------------------------------------------------------
-        tile_load(va, 0);
+        if constexpr (!DS) tile_load(va, 0);
         if constexpr (HO == 1) probe_flow();
         if (streamed) {
             const uint32_t cs = tail ? (uint32_t)(cs_abs - lo) : 0xFFFFFFFFu;
@@ -1414,25 +1477,26 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             // one tile: chunk sums, exclusive prefix (wave scans + wave totals via
             // LDS), then each frame picks up its boundary values
             auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
-                uint32_t sj[4], xj[4];
+                uint32_t sj[LPT], xj[LPT];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < LPT; ++j) {
                     sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
-                    xj[j] = wave_incl_scan(sj[j]);
+                    xj[j] = sj[j];
                 }
+                wave_incl_scan_n<LPT>(xj);
                 if (lane == 63) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+                    for (int j = 0; j < LPT; ++j) s_wt[buf][j * 4 + wv] = xj[j];
                 }
                 __syncthreads();
                 if constexpr (B1) { // the previous tile's boundaries (buffer buf ^ 1)
-                    const uint32_t p0 = c0 - ST_TILE; // wraps for c0 = 0: no frame matches
-                    if (c0 != 0 && cs - p0 < ST_TILE) es = s_pre[buf ^ 1u][cs - p0];
-                    if (c0 != 0 && ce - p0 < ST_TILE) ee = s_pre[buf ^ 1u][ce - p0];
+                    const uint32_t p0 = c0 - TCH; // wraps for c0 = 0: no frame matches
+                    if (c0 != 0 && cs - p0 < TCH) es = s_pre[buf ^ 1u][cs - p0];
+                    if (c0 != 0 && ce - p0 < TCH) ee = s_pre[buf ^ 1u][ce - p0];
                 }
-                uint32_t wt[16]; // block-uniform: kept in SGPRs
+                uint32_t wt[4 * LPT]; // block-uniform: kept in SGPRs
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < LPT; ++j) {
                     const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
                     wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
                     wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
@@ -1441,35 +1505,35 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 }
                 uint32_t base = carry;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < LPT; ++j) {
                     uint32_t wb = 0;
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
+                    for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wvu ? wt[j * 4 + w] : 0u;
                     s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
                     base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
                 }
                 carry = base;
                 if constexpr (!B1) {
                     __syncthreads();
-                    if (cs - c0 < ST_TILE) es = s_pre[buf][cs - c0];
-                    if (ce - c0 < ST_TILE) ee = s_pre[buf][ce - c0];
+                    if (cs - c0 < TCH) es = s_pre[buf][cs - c0];
+                    if (ce - c0 < TCH) ee = s_pre[buf][ce - c0];
                 }
             };
             // unrolled twice: the A/B tiles swap roles without register moves (a
             // move would wait for the prefetch it copies); one exit per pair (a
             // trailing all-masked tile costs no bandwidth: its loads hit chunk 0)
             uint32_t c0 = 0;
-            for (; c0 < span; c0 += 2 * ST_TILE) {
-                tile_load(vb, c0 + ST_TILE);
+            for (; c0 < span; c0 += 2 * TCH) {
+                tile_load(vb, c0 + TCH);
                 tile(va, c0, 0);
-                tile_load(va, c0 + 2 * ST_TILE);
-                tile(vb, c0 + ST_TILE, 1);
+                tile_load(va, c0 + 2 * TCH);
+                tile(vb, c0 + TCH, 1);
             }
             if constexpr (B1) { // the last tile's boundaries (buffer 1)
                 __syncthreads();
-                const uint32_t p0 = c0 - ST_TILE;
-                if (cs - p0 < ST_TILE) es = s_pre[1][cs - p0];
-                if (ce - p0 < ST_TILE) ee = s_pre[1][ce - p0];
+                const uint32_t p0 = c0 - TCH;
+                if (cs - p0 < TCH) es = s_pre[1][cs - p0];
+                if (ce - p0 < TCH) ee = s_pre[1][ce - p0];
             }
             if (ce == span) ee = carry;
             if (tail) acc += ee - es;
@@ -1520,7 +1584,8 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
 
 // PERS: a resident grid (occupancy x CUs, or the g_bpc_cap) of blocks that
 // loop over the tiles, instead of one block per tile
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
+          bool DS = false, int LPT = 4>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -1529,14 +1594,14 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
     if constexpr (PERS) {
         int cu = 0, occ = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS>), 256,
+            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT>), 256,
             (size_t)lds_bins * 4u, &cu, &occ);
         if (e != hipSuccess) return e;
         if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
         blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
     }
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2219,6 +2284,15 @@ static const variant_entry k_variants[] = {
     // 44/45: stream-heads kernel (heads picked out of an LDS copy of the
     // stream), 16-KiB / 8-KiB tiles
     {0, 1, 1, 44, launch_sh<1024>}, {0, 1, 1, 45, launch_sh<512>},
+    // 46/47: pipes 38/39 with the span from the descriptors (DS: the first
+    // tiles issued while the heads are in flight)
+    {0, 1, 1, 46, launch_stream<true, 0, 3, 1, true, false, true>},
+    {0, 1, 1, 47, launch_stream<true, 0, 0, 1, true, false, true>},
+    // 48: pipe 38 at 6 blocks/CU (HO = 2 with B1)
+    {0, 1, 1, 48, launch_stream<true, 0, 2, 1, true>},
+    // 49/50: pipes 38/39 with 32-KiB tail tiles (8 chunks per thread per tile)
+    {0, 1, 1, 49, launch_stream<true, 0, 3, 1, true, false, false, 8>},
+    {0, 1, 1, 50, launch_stream<true, 0, 0, 1, true, false, false, 8>},
 };
 
 } // namespace

@@ -64,7 +64,10 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
                    (0, 0, 0, 42), (0, 0, 0, 43),  # the same on a resident grid
-                   (0, 0, 0, 44), (0, 0, 0, 45)]  # stream-heads kernel, 16-/8-KiB tiles
+                   (0, 0, 0, 44), (0, 0, 0, 45),  # stream-heads kernel, 16-/8-KiB tiles
+                   (0, 0, 0, 46), (0, 0, 0, 47),  # 38/39 with the span from the descriptors
+                   (0, 0, 0, 48),  # 38 at 6 blocks/CU
+                   (0, 0, 0, 49), (0, 0, 0, 50)]  # 38/39 with 32-KiB tail tiles
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

@@ -206,7 +206,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables):
     socks += [(L, 40000), (L2, 5555)]
     udp = np.zeros(len(socks), R.UDP_SOCK_DTYPE)
     for i, (ip, port) in enumerate(socks):
-        udp[i] = (R.ip_raw(ip), R.port_raw(port), 17)
+        udp[i] = (R.ip_raw(ip), R.port_raw(port), 17, 0)
     tcb = np.zeros(0, R.TCB_DTYPE)
     rng = np.random.default_rng(7)
     frames = []
@@ -242,7 +242,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables):
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
-                                     (0, 0, 0, 44), (0, 0, 0, 45),
+                                     (0, 0, 0, 44), (0, 0, 0, 45), (0, 0, 0, 46),
                                      (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor

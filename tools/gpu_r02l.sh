@@ -10,7 +10,7 @@ rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
 step sweep2 300 python bench.py --sweep cfg2 --sweep-counts --steps 20 --warmup 5 \
     --sweep-variants '1,4,1,12;1,4,1,14,3;1,4,1,14,4;1,4,1,15,3' || exit $?
 step sweep45 400 python bench.py --sweep cfg4,cfg5 --sweep-counts --steps 10 --warmup 3 \
-    --sweep-variants '0,0,0,38;0,0,0,44;0,0,0,45' || exit $?
+    --sweep-variants '0,0,0,38;0,0,0,46;0,0,0,47;0,0,0,39;0,0,0,44' || exit $?
 export TMPDIR=/tmp
 step sq2 200 python tools/pmc_counters.py sq cfg2 "--no-tx --no-cfg1" \
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
