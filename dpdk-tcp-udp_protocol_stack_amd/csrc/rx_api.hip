@@ -16,6 +16,7 @@
 
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
 void rx_set_bpc_cap(uint32_t cap);
+bool rx_variant_exists(uint32_t g, uint32_t pipe);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
@@ -489,9 +490,12 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
     if (!c) return RXG_EINVAL;
-    if (lanes_per_frame == 0 &&
-        (pipeline == 20 || (pipeline >= 30 && pipeline <= 49) || pipeline == 130)) {
-        c->tune_g = 0; // size-class binned path (20) / stream kernel (30..39, 130)
+    if (lanes_per_frame == 0 && pipeline != ~0u) {
+        // size-class binned path (20) / stream kernel variants: anything else
+        // would silently run the automatic choice (r02o measured "ablations"
+        // that were the default kernel), so it is refused
+        if (pipeline != 20 && !rx_variant_exists(0, pipeline)) return RXG_EINVAL;
+        c->tune_g = 0;
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;
         return RXG_OK;

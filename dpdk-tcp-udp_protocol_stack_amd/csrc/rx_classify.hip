@@ -1235,8 +1235,8 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4>
-__global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_classify_stream_kernel(
+          bool DS = false, int LPT = 4, bool PP = false>
+__global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
@@ -1262,7 +1262,34 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
     // no loop at all: with one, the compiler keeps the re-arm constants in a
     // scratch spill, written once per thread = 16 B of HBM writes per frame
     // (PMC r02g: 32 B/frame written instead of the 16-B verdict)
+    // PP (resident grid only): the next tile's frame heads and the descriptors
+    // of the tile after it are loaded while this tile's tail streams, so a
+    // tile starts with its heads in registers instead of two dependent HBM
+    // round trips (descriptor -> head) of block-serial latency
+    static_assert(!PP || (PERS && !DS), "PP: resident grid, span from the headers");
     const uint64_t ntiles = ((uint64_t)n + 255) / 256;
+    uint64_t cur_fpos = 0, d1_fpos = 0, d2_fpos = 0; // PP: descriptors of tiles t, t+1, t+2
+    int32_t cur_cp = 0, d1_cp = 0, d2_cp = 0;
+    uint4 cn[4]; // PP: the head of this thread's frame in the next tile
+    auto pp_desc = [&](uint64_t t, uint64_t &fp, int32_t &cpl) {
+        const uint64_t pd = t * 256 + tid;
+        const uint64_t qd = pd < n ? pd : 0;
+        const uint32_t o = off[qd];
+        const uint32_t l = len[qd];
+        fp = (uint64_t)o << unit_log2;
+        cpl = pd < n ? (int32_t)l : 0;
+    };
+    auto pp_head = [&](uint64_t fp, int32_t cpl) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cn[j] = ldg16<false>(pkts + fp + (16 * j < cpl ? 16 * j : 0));
+    };
+    if constexpr (PP) {
+        if (blockIdx.x < ntiles) {
+            pp_desc(blockIdx.x, cur_fpos, cur_cp);
+            pp_head(cur_fpos, cur_cp);
+            pp_desc(blockIdx.x + gridDim.x, d1_fpos, d1_cp);
+        }
+    }
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERS ? gridDim.x : ntiles) {
         if (PERS && tile != blockIdx.x) { // re-arm the span state: every read of the last tile's is done
             __syncthreads();
@@ -1276,14 +1303,16 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
         const uint64_t p = tile * 256 + tid;
         const bool valid = p < n;
         const uint64_t q = valid ? p : 0;
-        const uint64_t fpos = (uint64_t)off[q] << unit_log2;
+        const uint64_t fpos = PP ? cur_fpos : (uint64_t)off[q] << unit_log2;
         const uint8_t *fb = pkts + fpos;
-        const int32_t cp = valid ? (int32_t)len[q] : 0;
+        const int32_t cp = PP ? cur_cp : (valid ? (int32_t)len[q] : 0);
 
         // ---- head phase -------------------------------------------------------
         uint4 c[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
+        for (int j = 0; j < 4; ++j)
+            c[j] = (ABL & 4) ? make_uint4(0, 0, 0, 0)
+                             : (PP ? cn[j] : ldg16<false>(fb + (16 * j < cp ? 16 * j : 0)));
         // block span of the tail chunks (below); DS: from the descriptors alone,
         // bytes [64, caplen) of every frame rounded out to 16 B (a superset of
         // the checksummed tails), so the first tiles go out while the heads are
@@ -1304,6 +1333,10 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
             span = streamed ? (uint32_t)(hi - lo) : 0u;
             // (not streamed: loads of the thread's own frame head, never consumed)
             sb = streamed ? pkts + (lo << 4) : fb;
+            if constexpr ((ABL & 2) != 0) { // diagnostic: no tail stream at all
+                streamed = true;
+                span = 0;
+            }
         };
         uint4 va[LPT], vb[LPT];
         if constexpr (DS) {
@@ -1467,6 +1500,10 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
             if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
         };
         if constexpr (HO == 0) probe_flow();
+        if constexpr (PP) { // the next tile's heads, the descriptors after it
+            pp_head(d1_fpos, d1_cp);
+            pp_desc(tile + 2ull * gridDim.x, d2_fpos, d2_cp);
+        }
         // ---- tail phase -------------------------------------------------------
         if constexpr (!DS) tile_load(va, 0);
         if constexpr (HO == 1) probe_flow();
@@ -1572,6 +1609,10 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
             lane_count(cidx, counts, hist, lds_bins);
             if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
         }
+        if constexpr (PP) { // advance the descriptor queue (long since arrived)
+            cur_fpos = d1_fpos, cur_cp = d1_cp;
+            d1_fpos = d2_fpos, d1_cp = d2_cp;
+        }
     } // tiles
     if (lds_bins) {
         __syncthreads();
@@ -1585,7 +1626,7 @@ __global__ __launch_bounds__(256, LPT == 8 ? 4 : (HO == 3 ? 5 : 6)) void rx_clas
 // PERS: a resident grid (occupancy x CUs, or the g_bpc_cap) of blocks that
 // loop over the tiles, instead of one block per tile
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4>
+          bool DS = false, int LPT = 4, bool PP = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -1594,14 +1635,14 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
     if constexpr (PERS) {
         int cu = 0, occ = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT>), 256,
+            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP>), 256,
             (size_t)lds_bins * 4u, &cu, &occ);
         if (e != hipSuccess) return e;
         if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
         blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
     }
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2293,6 +2334,16 @@ static const variant_entry k_variants[] = {
     // 49/50: pipes 38/39 with 32-KiB tail tiles (8 chunks per thread per tile)
     {0, 1, 1, 49, launch_stream<true, 0, 3, 1, true, false, false, 8>},
     {0, 1, 1, 50, launch_stream<true, 0, 0, 1, true, false, false, 8>},
+    // diagnostic ablations of pipe 46 (wrong verdicts by construction): no
+    // flow probe (146), no tail stream (246), no head loads (446), neither
+    // heads nor stream (646)
+    // 52/53: pipes 42/43 (resident grid) with the next tile's heads prefetched (PP)
+    {0, 1, 1, 52, launch_stream<true, 0, 3, 1, true, true, false, 4, true>},
+    {0, 1, 1, 53, launch_stream<true, 0, 0, 1, true, true, false, 4, true>},
+    {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, false, true>},
+    {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, false, true>},
+    {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, false, true>},
+    {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, false, true>},
 };
 
 } // namespace
@@ -2321,6 +2372,13 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
 }
 
 void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
+
+// a compiled variant with this lanes-per-frame and pipeline id (rxg_tune)
+bool rx_variant_exists(uint32_t g, uint32_t pipe) {
+    for (const variant_entry &v : k_variants)
+        if (v.g == g && v.pipe == pipe) return true;
+    return false;
+}
 
 // workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
 // frame), then the count indices (room for 4 B per frame) and the count slabs

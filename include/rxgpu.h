@@ -205,10 +205,12 @@ int rxg_tx_cksum(rxg_ctx *ctx, uint8_t *pkts, uint64_t span_bytes, const uint32_
 
 /* Tuning hook: force the kernel variant (lanes per frame 1 or 4..64, passes
  * loaded up front, frames per lane group, pipeline mode; 0xFFFFFFFF = the
- * default pipeline); lanes_per_frame = 0 = automatic from len_hint, except
- * with pipeline 20 (size-class binned path) or 30..43 / 130 (stream kernel
- * variants, csrc/rx_classify.hip k_variants).  Unknown combinations make the
- * next burst fail with RXG_EHIP. */
+ * default pipeline); lanes_per_frame = 0 with pipeline 0xFFFFFFFF =
+ * automatic from len_hint; lanes_per_frame = 0 with any other pipeline =
+ * that frame-size-independent variant (20: size-class binned path; 30 and
+ * up: stream kernel variants, >= 100 diagnostic ablations; csrc/
+ * rx_classify.hip k_variants), RXG_EINVAL if it is not compiled in.  Unknown
+ * lanes_per_frame > 0 combinations make the next burst fail with RXG_EHIP. */
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline);
 

@@ -106,6 +106,19 @@ def test_flow_table_matches_list_scan(nu, nt, load_log2, tables):
             assert c.lookup_tcp(*a) == ora.lookup_tcp(*a)
 
 
+def test_tune_refuses_variants_not_compiled_in():
+    """a frame-size-independent pipeline that is not compiled in is refused at
+    rxg_tune (it used to run the automatic kernel silently); every listed
+    variant is accepted"""
+    with R.Context(R.HOST_ONLY) as c:
+        for bad in (21, 29, 51, 99, 131, 999):
+            with pytest.raises(R.RxgError):
+                c.tune(0, 0, 0, bad)
+        for v in R.KERNEL_VARIANTS:
+            c.tune(*v)
+        c.tune(0)
+
+
 def test_flow_load_rejects_out_of_range():
     with R.Context(R.HOST_ONLY) as c:
         with pytest.raises(R.RxgError):
