@@ -1211,6 +1211,30 @@ __device__ __forceinline__ void wave_incl_scan_n(uint32_t (&x)[N]) {
     for (int j = 0; j < N; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x143, 0xC, 0xF, false);
 }
 
+// One wave's share of the block span: the min of a and the max of b over the
+// lanes with `has`, and the sum of b - a, reduced across the wave first so
+// that one lane issues three LDS atomics.  (64 lanes of one wave atomically
+// updating the same three LDS words serialise: 192 conflicting LDS atomics
+// per wave, per 256-frame tile.)  Every lane of the wave must be active.
+__device__ __forceinline__ void span_add(bool has, uint64_t a, uint64_t b, unsigned long long *lo,
+                                         unsigned long long *hi, uint32_t *tail, uint32_t lane) {
+    unsigned long long mn = has ? a : ~0ull, mx = has ? b : 0ull;
+    uint32_t sm = has ? (uint32_t)(b - a) : 0u;
+    const bool any = __ballot(has) != 0ull;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long omn = __shfl_xor(mn, o), omx = __shfl_xor(mx, o);
+        mn = omn < mn ? omn : mn;
+        mx = omx > mx ? omx : mx;
+        sm += __shfl_xor(sm, o);
+    }
+    if (lane == 0 && any) {
+        atomicMin(lo, mn);
+        atomicMax(hi, mx);
+        atomicAdd(tail, sm);
+    }
+}
+
 __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
     return add_halves(add_halves(add_halves(add_halves(0u, v.x), v.y), v.z), v.w);
 }
@@ -1235,7 +1259,7 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4, bool PP = false>
+          bool DS = false, int LPT = 4, bool PP = false, bool HG = false>
 __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1248,8 +1272,12 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
     __shared__ unsigned long long s_lo, s_hi;
     __shared__ uint32_t s_tail;
+    // HG: heads gathered four lanes per head (head_gather_issue), transposed
+    // through a 4-KiB stage per wave
+    __shared__ __attribute__((aligned(16))) uint4 s_head[HG ? 4 : 1][HG ? 256 : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv); // wave-uniform: SALU selects
+    uint4 *hstage = &s_head[HG ? wv : 0][0];
     if (tid == 0) {
         s_lo = ~0ull;
         s_hi = 0;
@@ -1280,8 +1308,12 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
         cpl = pd < n ? (int32_t)l : 0;
     };
     auto pp_head = [&](uint64_t fp, int32_t cpl) {
+        if constexpr (HG) {
+            head_gather_issue(pkts, fp, cpl, lane, cn);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cn[j] = ldg16<false>(pkts + fp + (16 * j < cpl ? 16 * j : 0));
+            for (int j = 0; j < 4; ++j) cn[j] = ldg16<false>(pkts + fp + (16 * j < cpl ? 16 * j : 0));
+        }
     };
     if constexpr (PP) {
         if (blockIdx.x < ntiles) {
@@ -1309,10 +1341,15 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
 
         // ---- head phase -------------------------------------------------------
         uint4 c[4];
+        if constexpr (HG && !(ABL & 4)) {
+            if constexpr (!PP) head_gather_issue(pkts, fpos, cp, lane, cn);
+            head_gather_stage(hstage, lane, cn, c);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            c[j] = (ABL & 4) ? make_uint4(0, 0, 0, 0)
-                             : (PP ? cn[j] : ldg16<false>(fb + (16 * j < cp ? 16 * j : 0)));
+            for (int j = 0; j < 4; ++j)
+                c[j] = (ABL & 4) ? make_uint4(0, 0, 0, 0)
+                                 : (PP ? cn[j] : ldg16<false>(fb + (16 * j < cp ? 16 * j : 0)));
+        }
         // block span of the tail chunks (below); DS: from the descriptors alone,
         // bytes [64, caplen) of every frame rounded out to 16 B (a superset of
         // the checksummed tails), so the first tiles go out while the heads are
@@ -1342,11 +1379,7 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
         if constexpr (DS) {
             const uint64_t ds_cs = (fpos + 64) >> 4, ds_ce = (fpos + (uint32_t)cp + 15u) >> 4;
             __syncthreads(); // s_lo/s_hi/s_tail initialised
-            if (cp > 64) {
-                atomicMin(&s_lo, (unsigned long long)ds_cs);
-                atomicMax(&s_hi, (unsigned long long)ds_ce);
-                atomicAdd(&s_tail, (uint32_t)(ds_ce - ds_cs));
-            }
+            span_add(cp > 64, ds_cs, ds_ce, &s_lo, &s_hi, &s_tail, lane);
             __syncthreads();
             lo = s_lo, hi = s_hi, tsum = s_tail;
             span_of();
@@ -1431,11 +1464,7 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
         // scattered frames (per-thread fallback below)
         if constexpr (!DS) {
             __syncthreads(); // s_lo/s_hi/s_tail initialised
-            if (tail) {
-                atomicMin(&s_lo, (unsigned long long)cs_abs);
-                atomicMax(&s_hi, (unsigned long long)ce_abs);
-                atomicAdd(&s_tail, (uint32_t)(ce_abs - cs_abs));
-            }
+            span_add(tail, cs_abs, ce_abs, &s_lo, &s_hi, &s_tail, lane);
             __syncthreads();
             lo = s_lo, hi = s_hi, tsum = s_tail;
             span_of();
@@ -1626,7 +1655,7 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
 // PERS: a resident grid (occupancy x CUs, or the g_bpc_cap) of blocks that
 // loop over the tiles, instead of one block per tile
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4, bool PP = false>
+          bool DS = false, int LPT = 4, bool PP = false, bool HG = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -1635,14 +1664,354 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
     if constexpr (PERS) {
         int cu = 0, occ = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP>), 256,
+            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP, HG>), 256,
             (size_t)lds_bins * 4u, &cu, &occ);
         if (e != hipSuccess) return e;
         if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
         blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
     }
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP, HG>), dim3((uint32_t)blocks), dim3(256),
+                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
+                       lds_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Multi-frame stream kernel (pipes 56/57): the stream kernel's default shape
+// (pipe 54: heads gathered four lanes per head, one barrier per tail tile,
+// flow probe consumed after the stream) with F frames per thread, so a block
+// covers 256 F frames.  The ablations of r02p put a quarter of the IMIX burst
+// time in work that does not scale with bytes: the descriptor -> head -> span
+// latency chain and the barriers every block pays once (0.25 ms of 1.32 with
+// neither heads nor tails loaded).  With F frames per thread that chain is
+// paid once per 256 F frames.  Thread t owns frames t + 256 f (stores stay
+// coalesced per f).
+template <int F>
+__global__ __launch_bounds__(256, F == 1 ? 5 : 4) void rx_classify_stream2_kernel(
+    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
+    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    constexpr uint32_t TCH = 1024; // chunks per tail tile (16 KiB, 4 per thread)
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    // the head stages (16 KiB, head phase) and the prefix buffers (8 KiB, tail
+    // phase) share LDS: the span barrier separates the phases
+    __shared__ __attribute__((aligned(16))) uint4 s_buf[1024];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16];
+    __shared__ unsigned long long s_lo, s_hi;
+    __shared__ uint32_t s_tail;
+    uint32_t(*s_pre)[TCH] = reinterpret_cast<uint32_t(*)[TCH]>(s_buf);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
+    uint4 *hstage = s_buf + wv * 256u;
+    if (tid == 0) {
+        s_lo = ~0ull;
+        s_hi = 0;
+        s_tail = 0;
+    }
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+
+    const uint64_t p0 = (uint64_t)blockIdx.x * (256u * F);
+    uint64_t fpos[F];
+    int32_t cp[F];
+    bool valid[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        const uint64_t p = p0 + 256u * f + tid;
+        valid[f] = p < n;
+        const uint64_t q = valid[f] ? p : 0;
+        const uint32_t o = off[q];
+        const uint32_t l = len[q];
+        fpos[f] = (uint64_t)o << unit_log2;
+        cp[f] = valid[f] ? (int32_t)l : 0;
+    }
+    uint4 hv[F][4];
+#pragma unroll
+    for (int f = 0; f < F; ++f) head_gather_issue(pkts, fpos[f], cp[f], lane, hv[f]);
+
+    // per-frame state carried across the tail stream
+    uint32_t acc[F], cs[F], ce[F], es[F], ee[F], stored[F], vy[F], info[F], ka[F], kb[F], kc[F],
+        pe[F];
+    int32_t e[F], ef[F];
+    uint4 sl0[F], pc[F];
+    uint64_t cs_abs[F], ce_abs[F];
+    // info: cl | is_udp << 4 | is_tcp << 5 | do_sum << 6 | part << 7 | tail << 8 |
+    // hashed-home-slot << 9 | trunc << 10 | trunc_ok << 11 | flags << 16 | proto << 24
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        uint4 c[4];
+        head_gather_stage(hstage, lane, hv[f], c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp[f]);
+        const uint32_t et = c[0].w & 0xFFFFu;
+        const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
+        const uint32_t proto = c[1].y >> 24;
+        const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
+        const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
+        const uint32_t sport = c[2].x >> 16;
+        const uint32_t dport = c[2].y & 0xFFFFu;
+        const uint32_t dgl = rx_bswap16(c[2].y >> 16);
+        const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+        uint32_t cl, nd;
+        if (et == 0x0608u) {
+            cl = RXG_CLS_ARP;
+            nd = 42;
+        } else if (et != 0x0008u) {
+            cl = RXG_CLS_NON_IP;
+            nd = 14;
+        } else if (proto == 17u) {
+            cl = RXG_CLS_UDP;
+            nd = 42;
+        } else if (proto == 6u) {
+            cl = RXG_CLS_TCP;
+            nd = 54;
+        } else {
+            cl = RXG_CLS_IPV4_OTHER;
+            nd = 24;
+        }
+        const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+        const bool l4 = is_udp || is_tcp;
+        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+        const bool do_sum = l4 && tl >= 20u;
+        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+        e[f] = do_sum ? 34 + (int32_t)l4n : 0;
+        if (e[f] > cp[f]) e[f] = cp[f];
+        ef[f] = e[f] & ~15; // full tail chunks: [64, ef)
+        const bool part = ef[f] < e[f] && ef[f] >= 64;
+        const bool tail = ef[f] > 64;
+        cs_abs[f] = (fpos[f] + 64) >> 4;
+        ce_abs[f] = (fpos[f] + (uint32_t)ef[f]) >> 4;
+        const uint8_t *fb = pkts + fpos[f];
+        pc[f] = ldg16<false>(fb + (part ? ef[f] : 0));
+        // flow probe keys and its first reads (consumed after the stream)
+        const bool probe = valid[f] && l4;
+        ka[f] = is_udp ? dip : sip;
+        kb[f] = is_udp ? dport : dip;
+        kc[f] = is_udp ? 17u : (sport | (dport << 16));
+        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        const bool udp_port = is_udp && ft.udp_port != nullptr;
+        const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+        pe[f] = ptab[l4 ? dport : 0u];
+        const bool hash0 = probe && maxp > 0 && !udp_port;
+        const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
+                                       (rx_hash3(ka[f], kb[f], kc[f]) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                                 : reinterpret_cast<const uint4 *>(fb);
+        sl0[f] = ld_slot(sp0);
+        uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+        h1.x = 0;
+        h1.y = 0;
+        h1.z &= 0xFFFF0000u;
+        if (is_udp) h2.z &= 0xFFFF0000u;
+        if (is_tcp) h3.x &= 0x0000FFFFu;
+        uint32_t a = lane_chunk_sum(0u, h1, 16, e[f]);
+        a = lane_chunk_sum(a, h2, 32, e[f]);
+        a = lane_chunk_sum(a, h3, 48, e[f]);
+        if (do_sum) a += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
+        acc[f] = a;
+        stored[f] = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+        uint32_t flags = 0, poff = 0, plen = 0;
+        if (is_udp) {
+            poff = 42;
+            plen = dgl > 8u ? dgl - 8u : 0u;
+            if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        } else if (is_tcp) {
+            const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+            poff = 34u + 4u * hl;
+            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+            plen = pl < 0 ? 0u : (uint32_t)pl;
+        }
+        const bool trunc = (int32_t)nd > cp[f];
+        const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp[f]);
+        vy[f] = (poff & 0xFFFFu) | (plen << 16);
+        info[f] = cl | (is_udp ? 1u << 4 : 0u) | (is_tcp ? 1u << 5 : 0u) | (do_sum ? 1u << 6 : 0u) |
+                  (part ? 1u << 7 : 0u) | (tail ? 1u << 8 : 0u) | (hash0 ? 1u << 9 : 0u) |
+                  (trunc ? 1u << 10 : 0u) | (trunc_ok ? 1u << 11 : 0u) | (flags << 16) | (proto << 24);
+        es[f] = ee[f] = 0;
+    }
+
+    // block span of the tail chunks (the stages above are dead past this barrier)
+    __syncthreads(); // s_lo/s_hi/s_tail initialised; every head staged
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+        span_add((info[f] >> 8) & 1u, cs_abs[f], ce_abs[f], &s_lo, &s_hi, &s_tail, lane);
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    const uint32_t tsum = s_tail;
+    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + TCH && hi - lo < (1ull << 26);
+    if (streamed) {
+        const uint32_t span = (uint32_t)(hi - lo);
+        const uint8_t *sb = pkts + (lo << 4);
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const bool tail = (info[f] >> 8) & 1u;
+            cs[f] = tail ? (uint32_t)(cs_abs[f] - lo) : 0xFFFFFFFFu;
+            ce[f] = tail ? (uint32_t)(ce_abs[f] - lo) : 0xFFFFFFFFu;
+        }
+        auto tile_load = [&](uint4 *v, uint32_t c0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = c0 + j * 256 + tid;
+                v[j] = ldg16<true>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
+            }
+        };
+        uint32_t carry = 0;
+        // one tile: chunk sums, exclusive prefix (interleaved wave scans + wave
+        // totals through LDS); a tile's boundaries are read after the next
+        // tile's barrier (double-buffered s_pre / s_wt: one barrier per tile)
+        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
+            uint32_t sj[4], xj[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
+                xj[j] = sj[j];
+            }
+            wave_incl_scan_n<4>(xj);
+            if (lane == 63) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+            }
+            __syncthreads();
+            const uint32_t q0 = c0 - TCH; // wraps for c0 = 0: no frame matches
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                if (c0 != 0 && cs[f] - q0 < TCH) es[f] = s_pre[buf ^ 1u][cs[f] - q0];
+                if (c0 != 0 && ce[f] - q0 < TCH) ee[f] = s_pre[buf ^ 1u][ce[f] - q0];
+            }
+            uint32_t wt[16]; // block-uniform: kept in SGPRs
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
+                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
+                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
+                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
+                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
+            }
+            uint32_t base = carry;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t wb = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wvu ? wt[j * 4 + w] : 0u;
+                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
+                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
+            }
+            carry = base;
+        };
+        uint4 va[4], vb[4];
+        tile_load(va, 0);
+        uint32_t c0 = 0;
+        for (; c0 < span; c0 += 2 * TCH) {
+            tile_load(vb, c0 + TCH);
+            tile(va, c0, 0);
+            tile_load(va, c0 + 2 * TCH);
+            tile(vb, c0 + TCH, 1);
+        }
+        __syncthreads(); // the last tile's boundaries (buffer 1)
+        const uint32_t q0 = c0 - TCH;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            if (cs[f] - q0 < TCH) es[f] = s_pre[1][cs[f] - q0];
+            if (ce[f] - q0 < TCH) ee[f] = s_pre[1][ce[f] - q0];
+            if (ce[f] == span) ee[f] = carry;
+            if ((info[f] >> 8) & 1u) acc[f] += ee[f] - es[f];
+        }
+    } else { // scattered frames: each thread sums its own tails
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const uint8_t *fb = pkts + fpos[f];
+            if ((info[f] >> 8) & 1u)
+                for (int32_t s = 64; s < ef[f]; s += 64) {
+                    uint4 r[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        r[u] = ldg16<false>(fb + (s + 16 * u < ef[f] ? s + 16 * u : 0));
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (s + 16 * u < ef[f]) acc[f] += chunk_sum(r[u]);
+                }
+        }
+    }
+
+    // ---- verdicts -----------------------------------------------------------
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        const uint32_t in = info[f];
+        const uint32_t cl = in & 0xFu, proto = in >> 24;
+        const bool is_udp = (in >> 4) & 1u, is_tcp = (in >> 5) & 1u, do_sum = (in >> 6) & 1u;
+        const bool part = (in >> 7) & 1u, hash0 = (in >> 9) & 1u;
+        const bool trunc = (in >> 10) & 1u, trunc_ok = (in >> 11) & 1u;
+        uint32_t flags = (in >> 16) & 0xFFu;
+        const bool l4 = is_udp || is_tcp;
+        uint32_t a = acc[f];
+        if (part) a = lane_chunk_sum(a, pc[f], ef[f], e[f]);
+        uint32_t ck = 0;
+        if (do_sum) {
+            ck = (~fold16(a)) & 0xFFFFu;
+            if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+        }
+        const bool ok = l4 && stored[f] == ck;
+        // UDP always, TCP only with a good checksum (the reference looks
+        // nothing up for a bad one)
+        const bool probe = valid[f] && (is_udp || (is_tcp && ok));
+        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+        const bool udp_port = is_udp && ft.udp_port != nullptr;
+        uint32_t flow = RXG_FLOW_NONE;
+        bool hashed = probe && maxp > 0;
+        if (hashed && udp_port) hashed = !rx_udp_port_decide(pe[f], ka[f], ft.udp_dip, &flow);
+        if (hashed) {
+            const uint4 *tb = is_udp ? ft.udp : ft.tcp;
+            const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
+            uint32_t pj = rx_hash3(ka[f], kb[f], kc[f]) & mk;
+            for (uint32_t pr = 0; pr < maxp; ++pr, pj = (pj + 1) & mk) {
+                // the home slot came with the head (a UDP key on a flagged port:
+                // loaded now)
+                const uint4 sl = pr == 0 && hash0 ? sl0[f] : ld_slot(tb + pj);
+                if (sl.w == RX_SLOT_EMPTY) break;
+                if (sl.x == ka[f] && sl.y == kb[f] && sl.z == kc[f]) {
+                    flow = sl.w;
+                    break;
+                }
+            }
+        }
+        if (is_tcp && probe && flow == RXG_FLOW_NONE) flow = pe[f]; // listener
+        int32_t rc = RXG_RC_KNI;
+        if (is_udp)
+            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                       : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        else if (is_tcp)
+            rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+        if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+        if (valid[f]) {
+            const uint64_t p = p0 + 256u * f + tid;
+            uint4 vd;
+            vd.x = flow;
+            vd.y = vy[f];
+            vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+            vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
+            stg16(&out[p], vd);
+            const uint32_t cidx =
+                rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+            lane_count(cidx, counts, hist, lds_bins);
+            if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
+        }
+    }
+    if (lds_bins) {
+        __syncthreads();
+        for (uint32_t i = tid; i < lds_bins; i += 256) {
+            const uint32_t cnt = hist[i];
+            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
+        }
+    }
+}
+
+template <int F>
+hipError_t launch_stream2(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                          const uint32_t *, const uint32_t *) {
+    const uint64_t blocks = ((uint64_t)n + 256u * F - 1) / (256u * F);
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rx_classify_stream2_kernel<F>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -1694,11 +2063,7 @@ __global__ __launch_bounds__(256) void rx_classify_sh_kernel(
     const int32_t cp = valid ? (int32_t)len[q] : 0;
     const uint64_t c0_abs = fpos >> 4, c1_abs = (fpos + (uint32_t)cp + 15u) >> 4;
     __syncthreads(); // s_lo/s_hi/s_tail initialised
-    if (cp > 0) {
-        atomicMin(&s_lo, (unsigned long long)c0_abs);
-        atomicMax(&s_hi, (unsigned long long)c1_abs);
-        atomicAdd(&s_tail, (uint32_t)(c1_abs - c0_abs));
-    }
+    span_add(cp > 0, c0_abs, c1_abs, &s_lo, &s_hi, &s_tail, lane);
     __syncthreads();
     const uint64_t lo = s_lo, hi = s_hi;
     const uint32_t tsum = s_tail;
@@ -2277,7 +2642,7 @@ static const variant_entry k_variants[] = {
     // 12 (first entry): 5 with coalesced LDS-staged head loads; 13: 12 without the LDS UDP table
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6},
     // 14: 12 software-pipelined (descriptors two trips, frame bytes one trip ahead)
-    {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 3},
+    {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 2},
     // 15: 14 with the frame bytes two trips ahead
     {1, 4, 1, 15, launch_lane_udpc<15, 0, true, false>, 3},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
@@ -2340,6 +2705,11 @@ static const variant_entry k_variants[] = {
     // 52/53: pipes 42/43 (resident grid) with the next tile's heads prefetched (PP)
     {0, 1, 1, 52, launch_stream<true, 0, 3, 1, true, true, false, 4, true>},
     {0, 1, 1, 53, launch_stream<true, 0, 0, 1, true, true, false, 4, true>},
+    // 54: pipe 38 with the heads gathered four lanes per head (HG); 55: 52 with HG
+    {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, false, 4, false, true>},
+    {0, 1, 1, 55, launch_stream<true, 0, 3, 1, true, true, false, 4, true, true>},
+    // 56/57: the multi-frame stream kernel, 1 / 2 frames per thread
+    {0, 1, 1, 56, launch_stream2<1>}, {0, 1, 1, 57, launch_stream2<2>},
     {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, false, true>},
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, false, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, false, true>},
@@ -2355,14 +2725,17 @@ static const variant_entry k_variants[] = {
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b),
-        // software-pipelined one trip ahead at 3 blocks/CU (pipe 14: 0.2487-0.2506 vs 0.2641-0.2660
-        // ms for pipe 12, with and without counts; pipe 15, two trips ahead: 0.2607; r02i)
+        // software-pipelined one trip ahead (pipe 14: 0.2487-0.2506 vs 0.2641-0.2660 ms for
+        // pipe 12 at 3 blocks/CU, r02i); with the LDS port window the two tie within 1%
+        // and pipe 14 is best at 2 blocks/CU (0.2328-0.2343 vs 0.2346-0.2352 for pipe 12 at
+        // 4-6, r02m, r02o)
         *g = 1, *p = 4, *fpg = 1, *pipe = 14;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel, flow probe after the
         // tail stream at 5 blocks/CU (HO = 3): 1-3% ahead of pipe 30 in every interleaved
-        // sweep (r01g: 1.184 vs 1.194, 1.177 vs 1.211, 1.305 vs 1.319 ms); one barrier per
-        // tail tile (B1) takes another 0.7% (r01g: 1.177 vs 1.185 vs 1.194 ms for pipe 30)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 38;
+        // sweep (r01g); one barrier per tail tile (B1) takes another 0.7% (r01g); heads
+        // gathered four lanes per head (HG, pipe 54): 1.2668 vs 1.3204 ms (no counts) and
+        // 1.3347 vs 1.3824 (counts), r02s
+        *g = 0, *p = 0, *fpg = 0, *pipe = 54;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), the

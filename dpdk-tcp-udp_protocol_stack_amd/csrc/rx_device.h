@@ -115,6 +115,41 @@ __device__ __forceinline__ void stage64_load(const uint8_t *b, uint4 *st, uint32
     __builtin_amdgcn_wave_barrier();
 }
 
+// Frame heads at arbitrary positions, gathered four lanes per head: lane l
+// loads chunk (l & 3) of the head of the wave's frame 16q + (l >> 2), q = 0..3
+// (its position and caplen fetched from the owning lane with ds_bpermute), so
+// one load instruction touches 16 heads instead of 64 (one 16-B piece per
+// lane, 64 distinct 64-B segments).  Chunks at or past a frame's caplen load
+// its chunk 0 (valid memory) and are masked by the consumer.
+__device__ __forceinline__ void head_gather_issue(const uint8_t *pkts, uint64_t fpos, int32_t cp,
+                                                  uint32_t lane, uint4 (&v)[4]) {
+    const int lo = (int)(uint32_t)fpos, hi = (int)(uint32_t)(fpos >> 32);
+    const uint32_t k = lane & 3u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int src = (int)((16u * q + (lane >> 2)) << 2);
+        const uint64_t f = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, hi) << 32) |
+                           (uint32_t)__builtin_amdgcn_ds_bpermute(src, lo);
+        const int32_t fc = __builtin_amdgcn_ds_bpermute(src, cp);
+        v[q] = ldg16<false>(pkts + f + (16 * (int32_t)k < fc ? 16u * k : 0u));
+    }
+}
+
+// head_gather_issue's chunks into each lane's own four (the stage64_load
+// layout through the wave's 4-KiB LDS stage st)
+__device__ __forceinline__ void head_gather_stage(uint4 *st, uint32_t lane, const uint4 (&v)[4],
+                                                  uint4 (&c)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t kk = q * 64u + lane, f = kk >> 2;
+        st[f * 4u + (((kk & 3u) + (f >> 2)) & 3u)] = v[q];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = st[lane * 4u + ((k + (lane >> 2)) & 3u)];
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
     s = (s >> 16) + (s & 0xFFFFu);
     s = (s >> 16) + (s & 0xFFFFu);

@@ -68,7 +68,9 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 46), (0, 0, 0, 47),  # 38/39 with the span from the descriptors
                    (0, 0, 0, 48),  # 38 at 6 blocks/CU
                    (0, 0, 0, 49), (0, 0, 0, 50),  # 38/39 with 32-KiB tail tiles
-                   (0, 0, 0, 52), (0, 0, 0, 53)]  # 42/43 with the next tile's heads prefetched
+                   (0, 0, 0, 52), (0, 0, 0, 53),  # 42/43 with the next tile's heads prefetched
+                   (0, 0, 0, 54), (0, 0, 0, 55),  # 38/52 with heads gathered 4 lanes per head
+                   (0, 0, 0, 56), (0, 0, 0, 57)]  # multi-frame stream kernel, 1 / 2 frames/thread
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

@@ -243,6 +243,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables):
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
                                      (0, 0, 0, 44), (0, 0, 0, 45), (0, 0, 0, 46), (0, 0, 0, 52),
+                                     (0, 0, 0, 54), (0, 0, 0, 55), (0, 0, 0, 56), (0, 0, 0, 57),
                                      (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor
