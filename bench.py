@@ -356,12 +356,17 @@ def cpu_rate(tb, pk, off, ln, ul, budget_s, threads=1):
     t0 = time.perf_counter()
     tb.classify(pk, off[:k], ln[:k], ul)
     per = (time.perf_counter() - t0) / k
-    target = max(k, int(budget_s / max(per, 1e-9)))
+    target = max(1, int(budget_s / max(per, 1e-9)))  # frames per thread
     if threads <= 1:
         shards = [np.arange(len(off))]
     else:
-        first, perm = R.rss_split(pk, off, ln, ul, threads)
-        shards = [perm[first[s]:first[s + 1]] for s in range(threads)]
+        # RSS shards (at most RXG_MAX_SHARDS = 64 queues), each cut into
+        # contiguous pieces when there are more threads than queues
+        nq = min(threads, 64)
+        first, perm = R.rss_split(pk, off, ln, ul, nq)
+        per = -(-threads // nq)
+        shards = [piece for s in range(nq)
+                  for piece in np.array_split(perm[first[s]:first[s + 1]], per)]
         shards = [s for s in shards if len(s)]
 
     def work(ix):
@@ -398,7 +403,11 @@ def cpu_baseline(name, budget_s, cores):
         # every logical CPU the host reports (nproc threads), whatever the
         # cgroup quota allows this process: the quota, not the thread count,
         # then bounds the rate (reported beside it)
-        rp, dp, ep = cpu_rate(tb, pk, off, ln, ul, budget_s / 8, cores["nproc"])
+        # (per-thread work scaled so the leg's total CPU time stays ~budget_s / 8
+        # of the box's share: nproc threads time-share the quota)
+        rp, dp, ep = cpu_rate(tb, pk, off, ln, ul,
+                              budget_s / 8 * cores["threads"] / max(cores["nproc"], 1),
+                              cores["nproc"])
         res[opt] = dict(one_core=dict(mpps=round(r1 / 1e6, 4), frames=d1, seconds=round(e1, 2)),
                         all_cores=dict(mpps=round(rn / 1e6, 4), frames=dn, seconds=round(en, 2),
                                        threads=cores["threads"]),
