@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0 || PIPE >= 12, "LDS table: PIPE 0 / 12 / 14 / 15 only");
+    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14, "LDS table: PIPE 0 / 12 / 14 only");
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     // the port window after the compact table, then (PIPE 12/14/15) the stage
@@ -920,46 +920,6 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 asm volatile("" ::"v"(B.cap), "v"(B.fb));
             }
         }
-    } else if constexpr (PIPE == 15) {
-        // 14 with the frame bytes two trips ahead (three 4-KiB sets per wave in
-        // flight, for lower occupancy: 3 blocks/CU) and the descriptors three
-        // trips ahead.  The frame-byte sets rotate (unrolled x3, no moves); the
-        // descriptors shift down a queue by value each trip: the newest one is
-        // waited for by its move, at the end of the trip that loaded it, where
-        // only younger loads (the frame bytes issued after it) stay in flight.
-        uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
-                                                 (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
-                       (tid >> 6) * 256u;
-        const uint32_t lane = tid & 63u;
-        uint64_t base = (uint64_t)blockIdx.x * 256;
-        if (base < n) {
-            lane_frame L0, L1, L2, L3; // trips t .. t+3
-            uint4 va[4], vb[4], vc[4];
-            lane_desc_nb(L0, p, n, pkts, off, len, unit_log2);
-            lane_desc_nb(L1, p + stride, n, pkts, off, len, unit_log2);
-            lane_desc_nb(L2, p + 2 * stride, n, pkts, off, len, unit_log2);
-            bool c0 = lane_issue(L0, pkts, lane, va);
-            bool c1 = lane_issue(L1, pkts, lane, vb);
-            bool c2 = false;
-            // one trip: descriptors of t+3, bytes of t+2 into VN, trip t from VC
-            auto trip = [&](uint4 (&VC)[4], bool cc, uint4 (&VN)[4], bool &cn) -> bool {
-                lane_desc_nb(L3, p + 3 * stride, n, pkts, off, len, unit_log2);
-                cn = lane_issue(L2, pkts, lane, VN);
-                lane_stage(L0, VC, cc, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(L0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
-                base += stride;
-                p += stride;
-                L0 = L1;
-                L1 = L2;
-                L2 = L3;
-                return base < n;
-            };
-            for (;;) {
-                if (!trip(va, c0, vc, c2)) break; // bytes of t+2 -> vc
-                if (!trip(vb, c1, va, c0)) break; // t+3 -> va
-                if (!trip(vc, c2, vb, c1)) break; // t+4 -> vb
-            }
-        }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
         uint64_t base = (uint64_t)blockIdx.x * 256;
@@ -1020,10 +980,10 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
-    if ((PIPE == 14 || PIPE == 15) && idx) return hipErrorInvalidValue; // no index-list mode
+    if (PIPE == 14 && idx) return hipErrorInvalidValue; // no index-list mode
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
                        (LDT ? (size_t)(ft.udpc_mask + 1) * 8u + ((ft.udpw_n + 7u) & ~7u) * 2u : 0u) +
-                       (PIPE == 12 || PIPE == 14 || PIPE == 15 ? 16384u : 0u);
+                       (PIPE == 12 || PIPE == 14 ? 16384u : 0u);
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
         reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
@@ -1177,24 +1137,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-// four independent inclusive scans, step-interleaved: each DPP step of one
+// N independent inclusive scans, step-interleaved: each DPP step of one
 // row reads a register the previous VALU op did not write, so the DPP
 // read-after-write wait states (s_nop) of a single scan disappear
-__device__ __forceinline__ void wave_incl_scan4(uint32_t (&x)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x111, 0xF, 0xF, true);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x112, 0xF, 0xF, true);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x114, 0xF, 0xF, true);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x118, 0xF, 0xF, true);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x142, 0xA, 0xF, false);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] += __builtin_amdgcn_update_dpp(0u, x[j], 0x143, 0xC, 0xF, false);
-}
-
 template <int N>
 __device__ __forceinline__ void wave_incl_scan_n(uint32_t (&x)[N]) {
 #pragma unroll
@@ -1258,16 +1203,15 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4, bool PP = false, bool HG = false>
-__global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void rx_classify_stream_kernel(
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
+          bool HG = false>
+__global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    // LPT = 16-B chunks per thread per tail tile: TCH = 256 * LPT chunks per tile
-    constexpr uint32_t TCH = 256u * LPT;
-    static_assert(LPT == 4 || LPT == 8, "tile shape");
+    constexpr uint32_t LPT = 4;          // 16-B chunks per thread per tail tile
+    constexpr uint32_t TCH = 256u * LPT; // chunks per tail tile (16 KiB)
     __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
     __shared__ unsigned long long s_lo, s_hi;
@@ -1285,70 +1229,30 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
     }
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
 
-    // one 256-frame tile per trip: one trip per block on a full grid, a
-    // block-strided loop on a resident (persistent) grid.  The full grid has
-    // no loop at all: with one, the compiler keeps the re-arm constants in a
-    // scratch spill, written once per thread = 16 B of HBM writes per frame
-    // (PMC r02g: 32 B/frame written instead of the 16-B verdict)
-    // PP (resident grid only): the next tile's frame heads and the descriptors
-    // of the tile after it are loaded while this tile's tail streams, so a
-    // tile starts with its heads in registers instead of two dependent HBM
-    // round trips (descriptor -> head) of block-serial latency
-    static_assert(!PP || (PERS && !DS), "PP: resident grid, span from the headers");
-    const uint64_t ntiles = ((uint64_t)n + 255) / 256;
-    uint64_t cur_fpos = 0, d1_fpos = 0, d2_fpos = 0; // PP: descriptors of tiles t, t+1, t+2
-    int32_t cur_cp = 0, d1_cp = 0, d2_cp = 0;
-    uint4 cn[4]; // PP: the head of this thread's frame in the next tile
-    auto pp_desc = [&](uint64_t t, uint64_t &fp, int32_t &cpl) {
-        const uint64_t pd = t * 256 + tid;
-        const uint64_t qd = pd < n ? pd : 0;
-        const uint32_t o = off[qd];
-        const uint32_t l = len[qd];
-        fp = (uint64_t)o << unit_log2;
-        cpl = pd < n ? (int32_t)l : 0;
-    };
-    auto pp_head = [&](uint64_t fp, int32_t cpl) {
-        if constexpr (HG) {
-            head_gather_issue(pkts, fp, cpl, lane, cn);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cn[j] = ldg16<false>(pkts + fp + (16 * j < cpl ? 16 * j : 0));
-        }
-    };
-    if constexpr (PP) {
-        if (blockIdx.x < ntiles) {
-            pp_desc(blockIdx.x, cur_fpos, cur_cp);
-            pp_head(cur_fpos, cur_cp);
-            pp_desc(blockIdx.x + gridDim.x, d1_fpos, d1_cp);
-        }
-    }
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERS ? gridDim.x : ntiles) {
-        if (PERS && tile != blockIdx.x) { // re-arm the span state: every read of the last tile's is done
-            __syncthreads();
-            if (tid == 0) {
-                s_lo = ~0ull;
-                s_hi = 0;
-                s_tail = 0;
-            }
-        }
-
+    // one 256-frame tile per block.  (A resident grid looping over tiles, with
+    // or without the next tile's heads prefetched, measured slower: r02e,
+    // r02q.  With a tile loop here the compiler kept the span re-arm constants
+    // in a scratch spill written once per thread, 16 B of HBM writes per
+    // frame: PMC r02g.)
+    {
+        const uint64_t tile = blockIdx.x;
         const uint64_t p = tile * 256 + tid;
         const bool valid = p < n;
         const uint64_t q = valid ? p : 0;
-        const uint64_t fpos = PP ? cur_fpos : (uint64_t)off[q] << unit_log2;
+        const uint64_t fpos = (uint64_t)off[q] << unit_log2;
         const uint8_t *fb = pkts + fpos;
-        const int32_t cp = PP ? cur_cp : (valid ? (int32_t)len[q] : 0);
+        const int32_t cp = valid ? (int32_t)len[q] : 0;
 
         // ---- head phase -------------------------------------------------------
         uint4 c[4];
         if constexpr (HG && !(ABL & 4)) {
-            if constexpr (!PP) head_gather_issue(pkts, fpos, cp, lane, cn);
-            head_gather_stage(hstage, lane, cn, c);
+            uint4 hv[4];
+            head_gather_issue(pkts, fpos, cp, lane, hv);
+            head_gather_stage(hstage, lane, hv, c);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                c[j] = (ABL & 4) ? make_uint4(0, 0, 0, 0)
-                                 : (PP ? cn[j] : ldg16<false>(fb + (16 * j < cp ? 16 * j : 0)));
+                c[j] = (ABL & 4) ? make_uint4(0, 0, 0, 0) : ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
         }
         // block span of the tail chunks (below); DS: from the descriptors alone,
         // bytes [64, caplen) of every frame rounded out to 16 B (a superset of
@@ -1529,10 +1433,6 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
             if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
         };
         if constexpr (HO == 0) probe_flow();
-        if constexpr (PP) { // the next tile's heads, the descriptors after it
-            pp_head(d1_fpos, d1_cp);
-            pp_desc(tile + 2ull * gridDim.x, d2_fpos, d2_cp);
-        }
         // ---- tail phase -------------------------------------------------------
         if constexpr (!DS) tile_load(va, 0);
         if constexpr (HO == 1) probe_flow();
@@ -1638,11 +1538,7 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
             lane_count(cidx, counts, hist, lds_bins);
             if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
         }
-        if constexpr (PP) { // advance the descriptor queue (long since arrived)
-            cur_fpos = d1_fpos, cur_cp = d1_cp;
-            d1_fpos = d2_fpos, d1_cp = d2_cp;
-        }
-    } // tiles
+    } // tile
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -1652,695 +1548,20 @@ __global__ __launch_bounds__(256, (LPT == 8 || PP) ? 4 : (HO == 3 ? 5 : 6)) void
     }
 }
 
-// PERS: a resident grid (occupancy x CUs, or the g_bpc_cap) of blocks that
-// loop over the tiles, instead of one block per tile
-template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool PERS = false,
-          bool DS = false, int LPT = 4, bool PP = false, bool HG = false>
+template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
+          bool HG = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
-    uint64_t blocks = ((uint64_t)n + 255) / 256;
-    if constexpr (PERS) {
-        int cu = 0, occ = 0;
-        hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP, HG>), 256,
-            (size_t)lds_bins * 4u, &cu, &occ);
-        if (e != hipSuccess) return e;
-        if (g_bpc_cap && (uint32_t)occ > g_bpc_cap) occ = (int)g_bpc_cap;
-        blocks = std::min<uint64_t>(blocks, (uint64_t)cu * occ);
-    }
-    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, PERS, DS, LPT, PP, HG>), dim3((uint32_t)blocks), dim3(256),
-                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
-                       lds_bins);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Multi-frame stream kernel (pipes 56/57): the stream kernel's default shape
-// (pipe 54: heads gathered four lanes per head, one barrier per tail tile,
-// flow probe consumed after the stream) with F frames per thread, so a block
-// covers 256 F frames.  The ablations of r02p put a quarter of the IMIX burst
-// time in work that does not scale with bytes: the descriptor -> head -> span
-// latency chain and the barriers every block pays once (0.25 ms of 1.32 with
-// neither heads nor tails loaded).  With F frames per thread that chain is
-// paid once per 256 F frames.  Thread t owns frames t + 256 f (stores stay
-// coalesced per f).
-template <int F>
-__global__ __launch_bounds__(256, F == 1 ? 5 : 4) void rx_classify_stream2_kernel(
-    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
-    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
-    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
-    constexpr uint32_t TCH = 1024; // chunks per tail tile (16 KiB, 4 per thread)
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    // the head stages (16 KiB, head phase) and the prefix buffers (8 KiB, tail
-    // phase) share LDS: the span barrier separates the phases
-    __shared__ __attribute__((aligned(16))) uint4 s_buf[1024];
-    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16];
-    __shared__ unsigned long long s_lo, s_hi;
-    __shared__ uint32_t s_tail;
-    uint32_t(*s_pre)[TCH] = reinterpret_cast<uint32_t(*)[TCH]>(s_buf);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
-    uint4 *hstage = s_buf + wv * 256u;
-    if (tid == 0) {
-        s_lo = ~0ull;
-        s_hi = 0;
-        s_tail = 0;
-    }
-    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
-
-    const uint64_t p0 = (uint64_t)blockIdx.x * (256u * F);
-    uint64_t fpos[F];
-    int32_t cp[F];
-    bool valid[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-        const uint64_t p = p0 + 256u * f + tid;
-        valid[f] = p < n;
-        const uint64_t q = valid[f] ? p : 0;
-        const uint32_t o = off[q];
-        const uint32_t l = len[q];
-        fpos[f] = (uint64_t)o << unit_log2;
-        cp[f] = valid[f] ? (int32_t)l : 0;
-    }
-    uint4 hv[F][4];
-#pragma unroll
-    for (int f = 0; f < F; ++f) head_gather_issue(pkts, fpos[f], cp[f], lane, hv[f]);
-
-    // per-frame state carried across the tail stream
-    uint32_t acc[F], cs[F], ce[F], es[F], ee[F], stored[F], vy[F], info[F], ka[F], kb[F], kc[F],
-        pe[F];
-    int32_t e[F], ef[F];
-    uint4 sl0[F], pc[F];
-    uint64_t cs_abs[F], ce_abs[F];
-    // info: cl | is_udp << 4 | is_tcp << 5 | do_sum << 6 | part << 7 | tail << 8 |
-    // hashed-home-slot << 9 | trunc << 10 | trunc_ok << 11 | flags << 16 | proto << 24
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-        uint4 c[4];
-        head_gather_stage(hstage, lane, hv[f], c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp[f]);
-        const uint32_t et = c[0].w & 0xFFFFu;
-        const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
-        const uint32_t proto = c[1].y >> 24;
-        const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
-        const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
-        const uint32_t sport = c[2].x >> 16;
-        const uint32_t dport = c[2].y & 0xFFFFu;
-        const uint32_t dgl = rx_bswap16(c[2].y >> 16);
-        const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
-        uint32_t cl, nd;
-        if (et == 0x0608u) {
-            cl = RXG_CLS_ARP;
-            nd = 42;
-        } else if (et != 0x0008u) {
-            cl = RXG_CLS_NON_IP;
-            nd = 14;
-        } else if (proto == 17u) {
-            cl = RXG_CLS_UDP;
-            nd = 42;
-        } else if (proto == 6u) {
-            cl = RXG_CLS_TCP;
-            nd = 54;
-        } else {
-            cl = RXG_CLS_IPV4_OTHER;
-            nd = 24;
-        }
-        const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
-        const bool l4 = is_udp || is_tcp;
-        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-        const bool do_sum = l4 && tl >= 20u;
-        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-        e[f] = do_sum ? 34 + (int32_t)l4n : 0;
-        if (e[f] > cp[f]) e[f] = cp[f];
-        ef[f] = e[f] & ~15; // full tail chunks: [64, ef)
-        const bool part = ef[f] < e[f] && ef[f] >= 64;
-        const bool tail = ef[f] > 64;
-        cs_abs[f] = (fpos[f] + 64) >> 4;
-        ce_abs[f] = (fpos[f] + (uint32_t)ef[f]) >> 4;
-        const uint8_t *fb = pkts + fpos[f];
-        pc[f] = ldg16<false>(fb + (part ? ef[f] : 0));
-        // flow probe keys and its first reads (consumed after the stream)
-        const bool probe = valid[f] && l4;
-        ka[f] = is_udp ? dip : sip;
-        kb[f] = is_udp ? dport : dip;
-        kc[f] = is_udp ? 17u : (sport | (dport << 16));
-        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-        const bool udp_port = is_udp && ft.udp_port != nullptr;
-        const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
-        pe[f] = ptab[l4 ? dport : 0u];
-        const bool hash0 = probe && maxp > 0 && !udp_port;
-        const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
-                                       (rx_hash3(ka[f], kb[f], kc[f]) & (is_udp ? ft.udp_mask : ft.tcp_mask))
-                                 : reinterpret_cast<const uint4 *>(fb);
-        sl0[f] = ld_slot(sp0);
-        uint4 h1 = c[1], h2 = c[2], h3 = c[3];
-        h1.x = 0;
-        h1.y = 0;
-        h1.z &= 0xFFFF0000u;
-        if (is_udp) h2.z &= 0xFFFF0000u;
-        if (is_tcp) h3.x &= 0x0000FFFFu;
-        uint32_t a = lane_chunk_sum(0u, h1, 16, e[f]);
-        a = lane_chunk_sum(a, h2, 32, e[f]);
-        a = lane_chunk_sum(a, h3, 48, e[f]);
-        if (do_sum) a += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
-        acc[f] = a;
-        stored[f] = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
-        uint32_t flags = 0, poff = 0, plen = 0;
-        if (is_udp) {
-            poff = 42;
-            plen = dgl > 8u ? dgl - 8u : 0u;
-            if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-        } else if (is_tcp) {
-            const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-            poff = 34u + 4u * hl;
-            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-            plen = pl < 0 ? 0u : (uint32_t)pl;
-        }
-        const bool trunc = (int32_t)nd > cp[f];
-        const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp[f]);
-        vy[f] = (poff & 0xFFFFu) | (plen << 16);
-        info[f] = cl | (is_udp ? 1u << 4 : 0u) | (is_tcp ? 1u << 5 : 0u) | (do_sum ? 1u << 6 : 0u) |
-                  (part ? 1u << 7 : 0u) | (tail ? 1u << 8 : 0u) | (hash0 ? 1u << 9 : 0u) |
-                  (trunc ? 1u << 10 : 0u) | (trunc_ok ? 1u << 11 : 0u) | (flags << 16) | (proto << 24);
-        es[f] = ee[f] = 0;
-    }
-
-    // block span of the tail chunks (the stages above are dead past this barrier)
-    __syncthreads(); // s_lo/s_hi/s_tail initialised; every head staged
-#pragma unroll
-    for (int f = 0; f < F; ++f)
-        span_add((info[f] >> 8) & 1u, cs_abs[f], ce_abs[f], &s_lo, &s_hi, &s_tail, lane);
-    __syncthreads();
-    const uint64_t lo = s_lo, hi = s_hi;
-    const uint32_t tsum = s_tail;
-    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + TCH && hi - lo < (1ull << 26);
-    if (streamed) {
-        const uint32_t span = (uint32_t)(hi - lo);
-        const uint8_t *sb = pkts + (lo << 4);
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            const bool tail = (info[f] >> 8) & 1u;
-            cs[f] = tail ? (uint32_t)(cs_abs[f] - lo) : 0xFFFFFFFFu;
-            ce[f] = tail ? (uint32_t)(ce_abs[f] - lo) : 0xFFFFFFFFu;
-        }
-        auto tile_load = [&](uint4 *v, uint32_t c0) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = c0 + j * 256 + tid;
-                v[j] = ldg16<true>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
-            }
-        };
-        uint32_t carry = 0;
-        // one tile: chunk sums, exclusive prefix (interleaved wave scans + wave
-        // totals through LDS); a tile's boundaries are read after the next
-        // tile's barrier (double-buffered s_pre / s_wt: one barrier per tile)
-        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
-            uint32_t sj[4], xj[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
-                xj[j] = sj[j];
-            }
-            wave_incl_scan_n<4>(xj);
-            if (lane == 63) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) s_wt[buf][j * 4 + wv] = xj[j];
-            }
-            __syncthreads();
-            const uint32_t q0 = c0 - TCH; // wraps for c0 = 0: no frame matches
-#pragma unroll
-            for (int f = 0; f < F; ++f) {
-                if (c0 != 0 && cs[f] - q0 < TCH) es[f] = s_pre[buf ^ 1u][cs[f] - q0];
-                if (c0 != 0 && ce[f] - q0 < TCH) ee[f] = s_pre[buf ^ 1u][ce[f] - q0];
-            }
-            uint32_t wt[16]; // block-uniform: kept in SGPRs
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
-                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
-                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
-                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
-                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
-            }
-            uint32_t base = carry;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t wb = 0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wvu ? wt[j * 4 + w] : 0u;
-                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
-                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
-            }
-            carry = base;
-        };
-        uint4 va[4], vb[4];
-        tile_load(va, 0);
-        uint32_t c0 = 0;
-        for (; c0 < span; c0 += 2 * TCH) {
-            tile_load(vb, c0 + TCH);
-            tile(va, c0, 0);
-            tile_load(va, c0 + 2 * TCH);
-            tile(vb, c0 + TCH, 1);
-        }
-        __syncthreads(); // the last tile's boundaries (buffer 1)
-        const uint32_t q0 = c0 - TCH;
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            if (cs[f] - q0 < TCH) es[f] = s_pre[1][cs[f] - q0];
-            if (ce[f] - q0 < TCH) ee[f] = s_pre[1][ce[f] - q0];
-            if (ce[f] == span) ee[f] = carry;
-            if ((info[f] >> 8) & 1u) acc[f] += ee[f] - es[f];
-        }
-    } else { // scattered frames: each thread sums its own tails
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            const uint8_t *fb = pkts + fpos[f];
-            if ((info[f] >> 8) & 1u)
-                for (int32_t s = 64; s < ef[f]; s += 64) {
-                    uint4 r[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        r[u] = ldg16<false>(fb + (s + 16 * u < ef[f] ? s + 16 * u : 0));
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (s + 16 * u < ef[f]) acc[f] += chunk_sum(r[u]);
-                }
-        }
-    }
-
-    // ---- verdicts -----------------------------------------------------------
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-        const uint32_t in = info[f];
-        const uint32_t cl = in & 0xFu, proto = in >> 24;
-        const bool is_udp = (in >> 4) & 1u, is_tcp = (in >> 5) & 1u, do_sum = (in >> 6) & 1u;
-        const bool part = (in >> 7) & 1u, hash0 = (in >> 9) & 1u;
-        const bool trunc = (in >> 10) & 1u, trunc_ok = (in >> 11) & 1u;
-        uint32_t flags = (in >> 16) & 0xFFu;
-        const bool l4 = is_udp || is_tcp;
-        uint32_t a = acc[f];
-        if (part) a = lane_chunk_sum(a, pc[f], ef[f], e[f]);
-        uint32_t ck = 0;
-        if (do_sum) {
-            ck = (~fold16(a)) & 0xFFFFu;
-            if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-        }
-        const bool ok = l4 && stored[f] == ck;
-        // UDP always, TCP only with a good checksum (the reference looks
-        // nothing up for a bad one)
-        const bool probe = valid[f] && (is_udp || (is_tcp && ok));
-        const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-        const bool udp_port = is_udp && ft.udp_port != nullptr;
-        uint32_t flow = RXG_FLOW_NONE;
-        bool hashed = probe && maxp > 0;
-        if (hashed && udp_port) hashed = !rx_udp_port_decide(pe[f], ka[f], ft.udp_dip, &flow);
-        if (hashed) {
-            const uint4 *tb = is_udp ? ft.udp : ft.tcp;
-            const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
-            uint32_t pj = rx_hash3(ka[f], kb[f], kc[f]) & mk;
-            for (uint32_t pr = 0; pr < maxp; ++pr, pj = (pj + 1) & mk) {
-                // the home slot came with the head (a UDP key on a flagged port:
-                // loaded now)
-                const uint4 sl = pr == 0 && hash0 ? sl0[f] : ld_slot(tb + pj);
-                if (sl.w == RX_SLOT_EMPTY) break;
-                if (sl.x == ka[f] && sl.y == kb[f] && sl.z == kc[f]) {
-                    flow = sl.w;
-                    break;
-                }
-            }
-        }
-        if (is_tcp && probe && flow == RXG_FLOW_NONE) flow = pe[f]; // listener
-        int32_t rc = RXG_RC_KNI;
-        if (is_udp)
-            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                       : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-        else if (is_tcp)
-            rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-        if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
-        if (valid[f]) {
-            const uint64_t p = p0 + 256u * f + tid;
-            uint4 vd;
-            vd.x = flow;
-            vd.y = vy[f];
-            vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-            vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
-            stg16(&out[p], vd);
-            const uint32_t cidx =
-                rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
-            lane_count(cidx, counts, hist, lds_bins);
-            if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
-        }
-    }
-    if (lds_bins) {
-        __syncthreads();
-        for (uint32_t i = tid; i < lds_bins; i += 256) {
-            const uint32_t cnt = hist[i];
-            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
-        }
-    }
-}
-
-template <int F>
-hipError_t launch_stream2(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
-                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
-                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
-                          const uint32_t *, const uint32_t *) {
-    const uint64_t blocks = ((uint64_t)n + 256u * F - 1) / (256u * F);
-    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream2_kernel<F>), dim3((uint32_t)blocks), dim3(256),
-                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
-                       lds_bins);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Stream-heads kernel (pipes 44/45): the stream kernel without its head phase.
-//   The block's span now covers every captured byte of its 256 frames (chunks
-//   [off, off + len) rounded out to 16 B), known from the descriptors alone, so
-//   the first tail tile is issued one HBM round trip after the descriptors
-//   instead of two (descriptor -> head -> span).  Each tile's 16-B chunks pass
-//   through an LDS copy of the tile (double-buffered) besides the chunk-sum
-//   scan; a frame's owner thread picks its four head chunks out of the tile
-//   they arrive in, parses the headers there, and from then on knows its
-//   checksum end e and reads the prefix sums at its tail boundaries (byte 64,
-//   e & ~15) and its last partial chunk from the tiles that hold them: both lie
-//   in the head's tile or a later one.  The frame heads are read once (with
-//   the stream, coalesced) instead of once per thread plus again inside the
-//   span.  The flow probe runs after the stream (stream kernel HO = 2).  A
-//   block whose span is far larger than its frames (scattered frames) loads
-//   heads and tails per thread instead.  TC = chunks per tile (16 KiB at
-//   1024); the LDS copy costs 2 x 16 B x TC.
-template <uint32_t TC, bool NTS>
-__global__ __launch_bounds__(256) void rx_classify_sh_kernel(
-    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
-    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
-    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
-    constexpr uint32_t LPT = TC / 256; // 16-B chunks per thread per tile
-    static_assert(LPT >= 1 && LPT <= 4 && TC % 256 == 0, "tile shape");
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    __shared__ __attribute__((aligned(16))) uint4 s_tile[2][TC];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TC];
-    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][16];
-    __shared__ unsigned long long s_lo, s_hi;
-    __shared__ uint32_t s_tail;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    if (tid == 0) {
-        s_lo = ~0ull;
-        s_hi = 0;
-        s_tail = 0;
-    }
-    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
-
-    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
-    const bool valid = p < n;
-    const uint64_t q = valid ? p : 0;
-    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
-    const uint8_t *fb = pkts + fpos;
-    const int32_t cp = valid ? (int32_t)len[q] : 0;
-    const uint64_t c0_abs = fpos >> 4, c1_abs = (fpos + (uint32_t)cp + 15u) >> 4;
-    __syncthreads(); // s_lo/s_hi/s_tail initialised
-    span_add(cp > 0, c0_abs, c1_abs, &s_lo, &s_hi, &s_tail, lane);
-    __syncthreads();
-    const uint64_t lo = s_lo, hi = s_hi;
-    const uint32_t tsum = s_tail;
-    const bool streamed = hi > lo && hi - lo <= 2ull * tsum + TC && hi - lo < (1ull << 26);
-
-    // ---- header decode (once the head's four chunks are in c) ---------------
-    uint4 c[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = make_uint4(0, 0, 0, 0);
-    uint32_t cl = RXG_CLS_NON_IP, nd = 14, tl = 0, proto = 0, sip = 0, dip = 0, sport = 0,
-             dport = 0, dgl = 0, hl = 0, acc = 0, stored = 0;
-    int32_t e = 0, ef = 0;
-    bool is_udp = false, is_tcp = false, l4 = false, do_sum = false, part = false, tail = false;
-    auto parse = [&]() {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
-        const uint32_t et = c[0].w & 0xFFFFu;
-        tl = rx_bswap16(c[1].x & 0xFFFFu);
-        proto = c[1].y >> 24;
-        sip = (c[1].z >> 16) | (c[1].w << 16);
-        dip = (c[1].w >> 16) | (c[2].x << 16);
-        sport = c[2].x >> 16;
-        dport = c[2].y & 0xFFFFu;
-        dgl = rx_bswap16(c[2].y >> 16);
-        hl = ((c[2].w >> 16) & 0xFFu) >> 4;
-        if (et == 0x0608u) {
-            cl = RXG_CLS_ARP;
-            nd = 42;
-        } else if (et != 0x0008u) {
-            cl = RXG_CLS_NON_IP;
-            nd = 14;
-        } else if (proto == 17u) {
-            cl = RXG_CLS_UDP;
-            nd = 42;
-        } else if (proto == 6u) {
-            cl = RXG_CLS_TCP;
-            nd = 54;
-        } else {
-            cl = RXG_CLS_IPV4_OTHER;
-            nd = 24;
-        }
-        is_udp = cl == RXG_CLS_UDP;
-        is_tcp = cl == RXG_CLS_TCP;
-        l4 = is_udp || is_tcp;
-        const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-        do_sum = l4 && tl >= 20u;
-        if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-        e = do_sum ? 34 + (int32_t)l4n : 0;
-        if (e > cp) e = cp;
-        ef = e & ~15; // full tail chunks: [64, ef)
-        part = ef < e && ef >= 64;
-        tail = ef > 64;
-        uint4 h1 = c[1], h2 = c[2], h3 = c[3];
-        h1.x = 0;
-        h1.y = 0;
-        h1.z &= 0xFFFF0000u;
-        if (is_udp) h2.z &= 0xFFFF0000u;
-        if (is_tcp) h3.x &= 0x0000FFFFu;
-        acc = lane_chunk_sum(0u, h1, 16, e);
-        acc = lane_chunk_sum(acc, h2, 32, e);
-        acc = lane_chunk_sum(acc, h3, 48, e);
-        if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
-        stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
-    };
-
-    // the flow probe's first reads (the port-table / listener entry and the
-    // hashed table's home slot), issued as soon as the head is parsed and
-    // consumed after the stream, so their latency hides behind it
-    const bool udp_tab = ft.udp_port != nullptr;
-    uint32_t pe = 0;
-    uint4 sl0 = make_uint4(0, 0, 0, 0);
-    auto probe_issue = [&]() {
-        const bool pr = valid && (is_udp || is_tcp);
-        const uint32_t *ptab = is_udp && udp_tab ? ft.udp_port : ft.listen;
-        pe = ptab[pr ? dport : 0u];
-        const bool h0 = pr && !(is_udp && udp_tab) && (is_udp ? ft.udp_probe : ft.tcp_probe) > 0;
-        const uint32_t ka = is_udp ? dip : sip, kb = is_udp ? dport : dip;
-        const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-        const uint4 *sp = h0 ? (is_udp ? ft.udp : ft.tcp) +
-                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
-                             : reinterpret_cast<const uint4 *>(pkts);
-        sl0 = ld_slot(sp);
-    };
-    uint4 pc = make_uint4(0, 0, 0, 0); // the last partial chunk [ef, e)
-    uint32_t es = 0, ee = 0;          // prefix sums at the tail's first and end chunk
-    if (streamed) {
-        const uint32_t span = (uint32_t)(hi - lo);
-        const uint8_t *sb = pkts + (lo << 4);
-        const uint32_t hs = cp > 0 ? (uint32_t)(c0_abs - lo) : 0xFFFFFFFFu; // head chunk 0
-        const uint32_t nh = cp >= 64 ? 4u : ((uint32_t)cp + 15u) >> 4;     // head chunks present
-        uint32_t need = (1u << nh) - 1u; // head chunks still to arrive
-        bool parsed = false;
-        uint32_t ts = 0xFFFFFFFFu, te = 0xFFFFFFFFu; // tail chunks [ts, te); te = partial chunk
-        if (valid && need == 0) { // caplen 0: nothing to wait for
-            parse();
-            probe_issue();
-            parsed = true;
-        }
-        auto tile_load = [&](uint4 *v, uint32_t c0) {
-#pragma unroll
-            for (int j = 0; j < (int)LPT; ++j) {
-                const uint32_t k = c0 + j * 256 + tid;
-                v[j] = ldg16<NTS>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
-            }
-        };
-        uint32_t carry = 0;
-        auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
-            uint32_t sj[LPT], xj[LPT];
-#pragma unroll
-            for (int j = 0; j < (int)LPT; ++j) {
-                sj[j] = c0 + j * 256 + tid < span ? chunk_sum(v[j]) : 0u;
-                xj[j] = wave_incl_scan(sj[j]);
-                s_tile[buf][j * 256 + tid] = v[j];
-            }
-            if (lane == 63) {
-#pragma unroll
-                for (int j = 0; j < (int)LPT; ++j) s_wt[buf][j * 4 + wv] = xj[j];
-            }
-            __syncthreads();
-            uint32_t wt[LPT * 4]; // block-uniform: kept in SGPRs
-#pragma unroll
-            for (int j = 0; j < (int)LPT; ++j) {
-                const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
-                wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
-                wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
-                wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
-                wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
-            }
-            uint32_t base = carry;
-#pragma unroll
-            for (int j = 0; j < (int)LPT; ++j) {
-                uint32_t wb = 0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wv ? wt[j * 4 + w] : 0u;
-                s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
-                base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
-            }
-            carry = base;
-            __syncthreads();
-            // this thread's frame: head chunks that arrived in this tile, then
-            // (once parsed) its tail boundaries and partial chunk
-            if (need) {
-#pragma unroll
-                for (uint32_t h = 0; h < 4; ++h)
-                    if (((need >> h) & 1u) && hs + h - c0 < TC) {
-                        c[h] = s_tile[buf][hs + h - c0];
-                        need &= ~(1u << h);
-                    }
-                if (!need) {
-                    parse();
-                    probe_issue();
-                    parsed = true;
-                    ts = hs + 4u;
-                    te = hs + ((uint32_t)ef >> 4);
-                }
-            }
-            if (parsed) {
-                if (tail && ts - c0 < TC) es = s_pre[buf][ts - c0];
-                if (tail && te - c0 < TC) ee = s_pre[buf][te - c0];
-                if (part && te - c0 < TC) pc = s_tile[buf][te - c0];
-            }
-        };
-        // unrolled twice: the A/B tiles swap roles without register moves
-        uint4 va[LPT], vb[LPT];
-        tile_load(va, 0);
-        for (uint32_t c0 = 0; c0 < span; c0 += 2 * TC) {
-            tile_load(vb, c0 + TC);
-            tile(va, c0, 0);
-            tile_load(va, c0 + 2 * TC);
-            tile(vb, c0 + TC, 1);
-        }
-        if (tail && te == span) ee = carry; // a tail ending at the span's end
-        if (tail) acc += ee - es;
-    } else if (valid) { // scattered frames: this thread loads its own head and tail
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = ldg16<false>(fb + (16 * j < cp ? 16 * j : 0));
-        parse();
-        probe_issue();
-        pc = ldg16<false>(fb + (part ? ef : 0));
-        for (int32_t s = 64; s < ef; s += 64) {
-            uint4 r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[u] = ldg16<false>(fb + (s + 16 * u < ef ? s + 16 * u : 0));
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (s + 16 * u < ef) acc += chunk_sum(r[u]);
-        }
-    }
-    if (part) acc = lane_chunk_sum(acc, pc, ef, e);
-
-    // ---- flow probe and verdict (as the stream kernel) ------------------------
-    uint32_t flags = 0, poff = 0, plen = 0;
-    if (is_udp) {
-        poff = 42;
-        plen = dgl > 8u ? dgl - 8u : 0u;
-        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-    } else if (is_tcp) {
-        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-        poff = 34u + 4u * hl;
-        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
-        plen = pl < 0 ? 0u : (uint32_t)pl;
-    }
-    const bool trunc = (int32_t)nd > cp;
-    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
-    uint32_t ck = 0;
-    if (do_sum) {
-        ck = (~fold16(acc)) & 0xFFFFu;
-        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-    }
-    const bool ok = l4 && stored == ck;
-    // UDP always; TCP only with a good checksum (the reference looks nothing
-    // up for a bad one)
-    const bool probe = valid && (is_udp || (is_tcp && ok));
-    const uint32_t ka = is_udp ? dip : sip;
-    const uint32_t kb = is_udp ? dport : dip;
-    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-    const bool udp_port = is_udp && udp_tab;
-    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-    uint32_t flow = RXG_FLOW_NONE;
-    bool hashed = probe && maxp > 0;
-    if (hashed && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
-    if (hashed) {
-        const uint4 *tb = is_udp ? ft.udp : ft.tcp;
-        const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
-        uint32_t pj = rx_hash3(ka, kb, kc) & mk;
-        for (uint32_t pr = 0; pr < maxp; ++pr, pj = (pj + 1) & mk) {
-            // the home slot came with the head (a UDP key on a flagged port:
-            // loaded now)
-            const uint4 sl = pr == 0 && !udp_port ? sl0 : ld_slot(tb + pj);
-            if (sl.w == RX_SLOT_EMPTY) break;
-            if (sl.x == ka && sl.y == kb && sl.z == kc) {
-                flow = sl.w;
-                break;
-            }
-        }
-    }
-    if (is_tcp && probe && flow == RXG_FLOW_NONE) flow = pe; // listener (tcp_stream_search pass 2)
-    int32_t rc = RXG_RC_KNI;
-    if (is_udp)
-        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
-                                   : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
-    else if (is_tcp)
-        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
-    if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
-    if (valid) {
-        uint4 vd;
-        vd.x = flow;
-        vd.y = (poff & 0xFFFFu) | (plen << 16);
-        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-        stg16(&out[p], vd);
-        const uint32_t cidx =
-            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
-        lane_count(cidx, counts, hist, lds_bins);
-        if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
-    }
-    if (lds_bins) {
-        __syncthreads();
-        for (uint32_t i = tid; i < lds_bins; i += 256) {
-            const uint32_t cnt = hist[i];
-            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
-        }
-    }
-}
-
-template <uint32_t TC, bool NTS = true>
-hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
-                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
-                     unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
-                     const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_sh_kernel<TC, NTS>), dim3((uint32_t)blocks), dim3(256),
-                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
-                       lds_bins);
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG>), dim3((uint32_t)blocks),
+                       dim3(256), (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out,
+                       counts, lds_bins);
     return hipGetLastError();
 }
+
 
 // ---------------------------------------------------------------------------
 // Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
@@ -2643,8 +1864,6 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6},
     // 14: 12 software-pipelined (descriptors two trips, frame bytes one trip ahead)
     {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 2},
-    // 15: 14 with the frame bytes two trips ahead
-    {1, 4, 1, 15, launch_lane_udpc<15, 0, true, false>, 3},
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},
@@ -2684,36 +1903,18 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
     // 38/39: pipes 34/30 with one barrier per tail tile (B1)
     {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>}, {0, 1, 1, 39, launch_stream<true, 0, 0, 1, true>},
-    // 42/43: pipes 38/39 on a resident grid (blocks loop over tiles)
-    {0, 1, 1, 42, launch_stream<true, 0, 3, 1, true, true>},
-    {0, 1, 1, 43, launch_stream<true, 0, 0, 1, true, true>},
-    // 44/45: stream-heads kernel (heads picked out of an LDS copy of the
-    // stream), 16-KiB / 8-KiB tiles
-    {0, 1, 1, 44, launch_sh<1024>}, {0, 1, 1, 45, launch_sh<512>},
-    // 46/47: pipes 38/39 with the span from the descriptors (DS: the first
-    // tiles issued while the heads are in flight)
-    {0, 1, 1, 46, launch_stream<true, 0, 3, 1, true, false, true>},
-    {0, 1, 1, 47, launch_stream<true, 0, 0, 1, true, false, true>},
-    // 48: pipe 38 at 6 blocks/CU (HO = 2 with B1)
-    {0, 1, 1, 48, launch_stream<true, 0, 2, 1, true>},
-    // 49/50: pipes 38/39 with 32-KiB tail tiles (8 chunks per thread per tile)
-    {0, 1, 1, 49, launch_stream<true, 0, 3, 1, true, false, false, 8>},
-    {0, 1, 1, 50, launch_stream<true, 0, 0, 1, true, false, false, 8>},
+    // 46: pipe 38 with the span from the descriptors (DS: the first tiles
+    // issued while the heads are in flight); the base of the ablations below
+    {0, 1, 1, 46, launch_stream<true, 0, 3, 1, true, true>},
     // diagnostic ablations of pipe 46 (wrong verdicts by construction): no
     // flow probe (146), no tail stream (246), no head loads (446), neither
     // heads nor stream (646)
-    // 52/53: pipes 42/43 (resident grid) with the next tile's heads prefetched (PP)
-    {0, 1, 1, 52, launch_stream<true, 0, 3, 1, true, true, false, 4, true>},
-    {0, 1, 1, 53, launch_stream<true, 0, 0, 1, true, true, false, 4, true>},
-    // 54: pipe 38 with the heads gathered four lanes per head (HG); 55: 52 with HG
-    {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, false, 4, false, true>},
-    {0, 1, 1, 55, launch_stream<true, 0, 3, 1, true, true, false, 4, true, true>},
-    // 56/57: the multi-frame stream kernel, 1 / 2 frames per thread
-    {0, 1, 1, 56, launch_stream2<1>}, {0, 1, 1, 57, launch_stream2<2>},
-    {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, false, true>},
-    {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, false, true>},
-    {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, false, true>},
-    {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, false, true>},
+    // 54: pipe 38 with the heads gathered four lanes per head (HG)
+    {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>},
+    {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, true>},
+    {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
+    {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
+    {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, true>},
 };
 
 } // namespace

@@ -47,7 +47,7 @@ HOST_ONLY = -1
 # rx_classify.hip (verdict-exact ones; the >= 100 pipeline ids are ablations)
 KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4, 1, 4),
                    (1, 4, 1, 5), (1, 4, 1, 6), (1, 4, 1, 7), (1, 4, 1, 8), (1, 4, 1, 9), (1, 4, 1, 10),
-                   (1, 4, 1, 11), (1, 4, 1, 12), (1, 4, 1, 13), (1, 4, 1, 14), (1, 4, 1, 15),
+                   (1, 4, 1, 11), (1, 4, 1, 12), (1, 4, 1, 13), (1, 4, 1, 14),
                    (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 1, 3), (4, 1, 2, 2), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
                    (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
@@ -63,14 +63,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
-                   (0, 0, 0, 42), (0, 0, 0, 43),  # the same on a resident grid
-                   (0, 0, 0, 44), (0, 0, 0, 45),  # stream-heads kernel, 16-/8-KiB tiles
-                   (0, 0, 0, 46), (0, 0, 0, 47),  # 38/39 with the span from the descriptors
-                   (0, 0, 0, 48),  # 38 at 6 blocks/CU
-                   (0, 0, 0, 49), (0, 0, 0, 50),  # 38/39 with 32-KiB tail tiles
-                   (0, 0, 0, 52), (0, 0, 0, 53),  # 42/43 with the next tile's heads prefetched
-                   (0, 0, 0, 54), (0, 0, 0, 55),  # 38/52 with heads gathered 4 lanes per head
-                   (0, 0, 0, 56), (0, 0, 0, 57)]  # multi-frame stream kernel, 1 / 2 frames/thread
+                   (0, 0, 0, 46),  # 38 with the span from the descriptors
+                   (0, 0, 0, 54)]  # 38 with heads gathered four lanes per head
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
