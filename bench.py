@@ -371,9 +371,13 @@ def cpu_rate(tb, pk, off, ln, ul, budget_s, threads=1):
 
     def work(ix):
         o, l = np.ascontiguousarray(off[ix]), np.ascontiguousarray(ln[ix])
+        # at least 16 frames of the thread's shard: a lookup's cost depends on
+        # where its flow sits in the list, so one or two frames per thread (1M
+        # tcbs, nproc threads) are not a sample
+        want = max(target, min(len(ix), 16))
         done = 0
-        while done < target:
-            m = min(len(ix), target - done)
+        while done < want:
+            m = min(len(ix), want - done)
             tb.classify(pk, o[:m], l[:m], ul)
             done += m
         return done
