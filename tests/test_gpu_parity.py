@@ -192,18 +192,21 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
 @pytest.mark.parametrize("variant", [(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
                                      (0, 0, 0, 20)])
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
-def test_udp_port_window(ctx, torch_dev, variant, tables):
+@pytest.mark.parametrize("far", [False, True])
+def test_udp_port_window(ctx, torch_dev, variant, tables, far):
     """small UDP socket sets (the compact LDS table) with the LDS port window:
     keys on the main address inside the window (bound, unbound, rebound:
     newest wins), outside it, on another address sharing window ports, and on
     an address with no socket; 64-B slotted frames (coalesced lane path) and
     a few longer ones; verdicts and counts bit-exact against the oracle, with
-    the window (tables 0) and without the port tables (NO_UDP_PORT)"""
+    the window (tables 0; far = a main-address socket 10000 ports away, so
+    the ports span more than the window's 4096 and none is built) and
+    without the port tables (NO_UDP_PORT)"""
     L, L2, L3 = "192.168.100.77", "10.9.9.9", "172.16.0.1"
-    socks = [(L, 30000 + 3 * k) for k in range(300)]        # window 30000..30897
+    socks = [(L, 30000 + 3 * k) for k in range(300)]        # window 30000..33000
     socks += [(L2, 30000 + 21 * k) for k in range(20)]      # another address, shared ports
     socks += [(L, 30000 + 30 * k) for k in range(10)]       # rebinds: newest wins
-    socks += [(L, 40000), (L2, 5555)]
+    socks += [(L, 40000 if far else 33000), (L2, 5555)]
     udp = np.zeros(len(socks), R.UDP_SOCK_DTYPE)
     for i, (ip, port) in enumerate(socks):
         udp[i] = (R.ip_raw(ip), R.port_raw(port), 17, 0)
@@ -215,7 +218,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables):
         if r < 4:
             dst, port = L, 30000 + int(rng.integers(0, 900))
         elif r == 4:
-            dst, port = L, int(rng.choice([40000, 29999, 30900, 50000]))
+            dst, port = L, int(rng.choice([40000, 33000, 29999, 30900, 33001, 50000]))
         elif r == 5:
             dst, port = L2, 30000 + 21 * int(rng.integers(0, 25))
         elif r == 6:
