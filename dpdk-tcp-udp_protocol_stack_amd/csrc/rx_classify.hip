@@ -1,6 +1,21 @@
 // rx_classify.hip — K1: fused parse + L4 checksum + flow classify (gfx950).
 //
-// Work decomposition
+// Three kernel shapes, picked per typical frame length by rx_pick_variant
+// (bottom of this file); every shape is correct for any layout and length:
+//   lane kernel   (rx_classify_lane_kernel)   one frame per lane: 64-B frames
+//                 (heads staged through LDS by coalesced 1-KiB wave loads,
+//                 software-pipelined one trip ahead, UDP table and port
+//                 window in LDS);
+//   group kernel  (rx_classify_kernel)        G lanes per frame: 1500-B frames
+//                 (described below);
+//   stream kernel (rx_classify_stream_kernel) heads per thread, tails streamed
+//                 by the block as one contiguous span with prefix sums: mixed
+//                 sizes (IMIX) and jumbo frames.
+// The variant table (k_variants) also holds tuning shapes and diagnostic
+// ablations (pipe >= 100, wrong verdicts by construction), reachable only
+// through rxg_tune.
+//
+// Group kernel work decomposition
 //   A frame is owned by a lane GROUP of G lanes (G = 4..64, power of two).
 //   Lane k of the group reads the 16-B chunks k, k+G, k+2G, ... of the frame;
 //   one "pass" of the group covers 16*G contiguous frame bytes, so a wave
