@@ -376,10 +376,11 @@ def test_fuzzed_frames_match_oracle(ctx, torch_dev):
         frames.append(bytes(f))
         caps.append(len(f) if rng.random() < 0.8 else int(rng.integers(0, len(f) + 1)))
     buf, off, lens = F.pack_frames(frames, 4, caplens=caps)
-    want = O.Tables(fl["udp"], fl["tcb"]).classify(buf, off, lens, 4)
-    for hint in (64, 600, 9000):
-        got = _dev_classify(torch_dev, ctx, buf, off, lens, 4, hint)
+    want, wcnt = O.Tables(fl["udp"], fl["tcb"]).classify(buf, off, lens, 4, counts=True)
+    for hint in (64, 600, 1500, 9000):  # every default kernel shape
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 4, hint, counts=True)
         assert got.tobytes() == want.tobytes(), (hint, _mismatch_report(got, want))
+        assert np.array_equal(cnt, wcnt), hint
 
 
 def test_process_mbufs(ctx):
