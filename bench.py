@@ -42,6 +42,9 @@ import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
 COUNTS = True
+# above 8192 flows the per-flow counts are two passes after the classify kernel;
+# on a second stream (rxg_classify_dev_cs) they overlap the next step's classify
+COUNT_STREAM = True
 TX = True
 RAMP_MS = 200.0
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
@@ -83,7 +86,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     alg_bytes = frame_bytes + 22 * n  # frame + off(4) + len(2) read + verdict(16) written
     # N > 1: step k's counts go to step_counts[k & 1]; the all-reduce runs on
     # the collective stream cs while step k+1's kernel runs, then adds into counts
-    cs = torch.cuda.Stream(dev) if world > 1 else None
+    cs = torch.cuda.Stream(dev) if (world > 1 or COUNT_STREAM) else None
+    csh = cs.cuda_stream if (cs is not None and COUNT_STREAM) else None
     step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)] if world > 1 else None
     k_ev = [torch.cuda.Event(), torch.cuda.Event()]
     done_ev = [torch.cuda.Event(), torch.cuda.Event()]
@@ -101,7 +105,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         if ev is not None:
             ev[0].record(stream)
         ctx.classify_dev(pk, off, ln, n, ul, w["len_hint"], out, tgt if COUNTS else None,
-                         stream=sh)
+                         stream=sh, count_stream=csh)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -135,6 +139,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     ev[0].record(stream)
     for k in range(steps):
         step()
+    if cs is not None:
+        stream.wait_stream(cs)  # the last step's counts (and all-reduce) are inside the window
     ev[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -170,7 +176,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         kernel_ms_avg=kavg,
         alg_bytes_per_launch=alg_bytes, frame_bytes=frame_bytes,
         rc0_frac=n_ok / max(n, 1), counts_ok=(expect is None or counted == expect),
-        setup_s=round(t_setup, 2),
+        setup_s=round(t_setup, 2), count_stream=bool(COUNTS and csh is not None),
     )
     achieved = alg_bytes / (kavg * 1e-3) / 1e9  # this rank's kernel (HIP events)
     res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
@@ -693,6 +699,9 @@ def main():
                          "timed steps (0 = none)")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--no-count-stream", action="store_true",
+                    help="per-flow counts on the classify stream (rxg_classify_dev), not "
+                         "overlapped with the next step (A/B)")
     ap.add_argument("--no-tx", action="store_true", help="skip timing the TX checksum kernel")
     ap.add_argument("--collective", default="rxg", choices=["rxg", "torch"],
                     help="N > 1 count all-reduce: rxg = RCCL through librxgpu's C ABI "
@@ -741,8 +750,9 @@ def main():
     ctx = R.Context(local)
     if a.flow_load:
         ctx.tune_flow_load(a.flow_load)
-    global COUNTS, TX, RAMP_MS
+    global COUNTS, TX, RAMP_MS, COUNT_STREAM
     RAMP_MS = a.ramp_ms
+    COUNT_STREAM = not a.no_count_stream
     COUNTS = not a.no_counts
     TX = not a.no_tx
     if a.variant:

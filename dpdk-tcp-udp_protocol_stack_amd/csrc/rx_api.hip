@@ -20,9 +20,11 @@ bool rx_variant_exists(uint32_t g, uint32_t pipe);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
-                              unsigned long long *counts, hipStream_t s, uint32_t *ws);
+                              unsigned long long *counts, hipStream_t s, uint32_t *ws,
+                              uint32_t phase, uint32_t buf, uint32_t nbuf);
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
-                            bool counts);
+                            bool counts, uint32_t nbuf);
+bool rx_count_uses_slabs(const rx_ft_dev &ft, bool counts);
 hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                            uint32_t unit_log2, uint32_t len_hint, uint32_t variant,
                            uint32_t bpc_cap, hipStream_t s);
@@ -226,13 +228,23 @@ struct rxg_ctx {
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
     uint32_t tune_tx = RXG_TX_AUTO, tune_tx_bpc = 0; // rxg_tune_tx
     uint32_t ft_load_log2 = RX_FT_LOAD_LOG2;           // rxg_tune_flow_load
-    uint32_t *d_ws = nullptr; // launch workspace (binned lists, count slabs), grown on demand
+    // launch workspace, grown on demand: [binned lists][count indices x 2][count
+    // slabs].  Three regions are tracked, each by the event of its last use and
+    // that use's stream: index buffer 0 (with the lists), index buffer 1, the
+    // slabs.  A launch that uses a region on another stream than its last use
+    // waits for that event first, so bursts on different streams never share a
+    // region in flight, and rxg_classify_dev_cs can classify burst k+1 into one
+    // index buffer while burst k is counted from the other on the count stream.
+    uint32_t *d_ws = nullptr;
     size_t d_ws_cap = 0;
-    // bursts on different streams share d_ws: a launch that uses it on another
-    // stream than the last one waits for that one's event first
-    hipEvent_t ws_ev = nullptr;
-    hipStream_t ws_stream = nullptr;
-    bool ws_used = false;
+    struct ws_use {
+        hipEvent_t ev = nullptr;
+        hipStream_t st = nullptr;
+        bool used = false;
+    } wu[3];
+    size_t ws_layout = 0; // region offsets depend on the burst shape; a change waits on all
+    uint32_t ws_flip = 0; // index buffer of the next split-stream burst
+    hipEvent_t ev_k1 = nullptr; // split-stream burst: classify done (count stream waits on it)
     void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
     size_t d_aux_cap = 0;
     // context-owned per-flow counts (host-buffer path)
@@ -324,7 +336,11 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
         if ((rc = rx_set_hip_error(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))))
             break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_listen, 65536 * sizeof(uint32_t))))) break;
-        if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming))))
+        for (rxg_ctx::ws_use &u : c->wu)
+            if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming))))
+                break;
+        if (rc) break;
+        if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming))))
             break;
         c->max_pkts = max_pkts;
         c->max_bytes = (max_bytes + 15) & ~15ull;
@@ -376,7 +392,9 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_aux);
     (void)hipFree(c->d_udpc);
     (void)hipFree(c->d_udpw);
-    if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
+    for (rxg_ctx::ws_use &u : c->wu)
+        if (u.ev) (void)hipEventDestroy(u.ev);
+    if (c->ev_k1) (void)hipEventDestroy(c->ev_k1);
     for (rxg_ctx::slot &sl : c->slots) {
         (void)hipFree(sl.d_pkts);
         (void)hipFree(sl.d_off);
@@ -559,9 +577,82 @@ uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport
     return rx_rss_hash(sip, dip, sport, dport);
 }
 
-int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
-                     const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t len_hint,
-                     rxg_verdict *d_out, uint64_t *d_counts, void *stream) {
+// workspace regions (rxg_ctx::wu)
+enum { WS_BUF0 = 0, WS_BUF1 = 1, WS_SLAB = 2 };
+
+static hipError_t ws_wait(rxg_ctx *c, int r, hipStream_t s) {
+    const rxg_ctx::ws_use &u = c->wu[r];
+    return (u.used && u.st != s) ? hipStreamWaitEvent(s, u.ev, 0) : hipSuccess;
+}
+
+static hipError_t ws_mark(rxg_ctx *c, int r, hipStream_t s) {
+    rxg_ctx::ws_use &u = c->wu[r];
+    hipError_t e = hipEventRecord(u.ev, s);
+    if (e == hipSuccess) u.st = s, u.used = true;
+    return e;
+}
+
+// size the workspace for a burst before its launches (growth drains every use
+// of the old one) and, when the burst shape moves the regions, order stream s
+// after every earlier use
+static int ws_prepare(rxg_ctx *c, size_t ws, size_t layout, hipStream_t s) {
+    if (ws > c->d_ws_cap) {
+        for (rxg_ctx::ws_use &u : c->wu)
+            if (u.used) HIPCHK(hipEventSynchronize(u.ev));
+        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
+        if (rc) return rc;
+    } else if (layout != c->ws_layout) {
+        for (int r = 0; r < 3; ++r) HIPCHK(ws_wait(c, r, s));
+    }
+    c->ws_layout = layout;
+    return RXG_OK;
+}
+
+// one burst on the workspace: classify + count on s (count_stream null or s),
+// or classify on s and the slab count on count_stream (double-buffered indices)
+static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                       const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
+                       uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
+                       unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
+    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr, 2);
+    const bool split = cs && cs != s && pipe != 20 && rx_count_uses_slabs(c->ft, d_counts != nullptr);
+    rx_set_bpc_cap(c->tune_bpc);
+    if (!ws) {
+        HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
+        return RXG_OK;
+    }
+    const size_t layout = ws ^ ((size_t)n << 40) ^ ((size_t)(pipe == 20) << 39);
+    int rc = ws_prepare(c, ws, layout, s);
+    if (rc) return rc;
+    if (!split) {
+        HIPCHK(ws_wait(c, WS_BUF0, s));
+        HIPCHK(ws_wait(c, WS_SLAB, s));
+        HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
+        HIPCHK(ws_mark(c, WS_BUF0, s));
+        HIPCHK(ws_mark(c, WS_SLAB, s));
+        return RXG_OK;
+    }
+    const uint32_t b = c->ws_flip;
+    c->ws_flip ^= 1u;
+    HIPCHK(ws_wait(c, b, s)); // the count that last read this index buffer
+    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+                              d_out, d_counts, s, c->d_ws, RX_PH_CLASSIFY, b, 2));
+    HIPCHK(hipEventRecord(c->ev_k1, s));
+    HIPCHK(hipStreamWaitEvent(cs, c->ev_k1, 0));
+    HIPCHK(ws_wait(c, WS_SLAB, cs));
+    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+                              d_out, d_counts, cs, c->d_ws, RX_PH_COUNT, b, 2));
+    HIPCHK(ws_mark(c, b, cs)); // covers the classify too (cs waited on it)
+    HIPCHK(ws_mark(c, WS_SLAB, cs));
+    return RXG_OK;
+}
+
+static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                             const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                             uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
+                             hipStream_t s, hipStream_t cs) {
     if (!c) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
     if (n == 0) return RXG_OK;
@@ -570,26 +661,24 @@ int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     HIPCHK(hipSetDevice(c->device));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
-    // workspace (binned lists, count slabs): grown on demand, so size it once
-    // per burst shape before any graph capture
-    const hipStream_t s = (hipStream_t)stream;
-    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr);
-    if (ws) {
-        if (ws > c->d_ws_cap && c->ws_used) HIPCHK(hipEventSynchronize(c->ws_ev)); // in use
-        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
-        if (rc) return rc;
-        if (c->ws_used && c->ws_stream != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
-    }
-    rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
-                              reinterpret_cast<uint4 *>(d_out),
-                              reinterpret_cast<unsigned long long *>(d_counts), s, c->d_ws));
-    if (ws) {
-        HIPCHK(hipEventRecord(c->ws_ev, s));
-        c->ws_stream = s;
-        c->ws_used = true;
-    }
-    return RXG_OK;
+    return classify_ws(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe,
+                       reinterpret_cast<uint4 *>(d_out),
+                       reinterpret_cast<unsigned long long *>(d_counts), s, cs);
+}
+
+int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                     const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t len_hint,
+                     rxg_verdict *d_out, uint64_t *d_counts, void *stream) {
+    return classify_dev_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, len_hint, d_out,
+                             d_counts, (hipStream_t)stream, nullptr);
+}
+
+int rxg_classify_dev_cs(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts, void *stream,
+                        void *count_stream) {
+    return classify_dev_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, len_hint, d_out,
+                             d_counts, (hipStream_t)stream, (hipStream_t)count_stream);
 }
 
 // Frames of a host burst into a slot: exactly `span` bytes cross PCIe (the
@@ -619,25 +708,9 @@ static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint6
     if (reused) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant((uint32_t)(span / n), &g, &p, &fpg, &pipe);
-    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, c->d_counts != nullptr);
-    if (ws) {
-        if (ws > c->d_ws_cap) { // grows only between bursts: drain the kernels using it
-            HIPCHK(hipStreamSynchronize(c->stream));
-            if (c->ws_used) HIPCHK(hipEventSynchronize(c->ws_ev));
-            int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
-            if (rc) return rc;
-        }
-        if (c->ws_used && c->ws_stream != c->stream)
-            HIPCHK(hipStreamWaitEvent(c->stream, c->ws_ev, 0));
-    }
-    rx_set_bpc_cap(c->tune_bpc);
-    HIPCHK(rx_classify_launch(sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, g, p, fpg, pipe,
-                              c->ft, sl.d_out, c->d_counts, c->stream, c->d_ws));
-    if (ws) {
-        HIPCHK(hipEventRecord(c->ws_ev, c->stream));
-        c->ws_stream = c->stream;
-        c->ws_used = true;
-    }
+    int rc = classify_ws(c, sl.d_pkts, sl.d_off, sl.d_len, n, off_unit_log2, g, p, fpg, pipe,
+                         sl.d_out, c->d_counts, c->stream, nullptr);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(sl.ev_k, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_d2h, sl.ev_k, 0));
     HIPCHK(hipMemcpyAsync(out, sl.d_out, n * 16ull, hipMemcpyDeviceToHost, c->s_d2h));

@@ -1579,6 +1579,334 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 
 
 // ---------------------------------------------------------------------------
+// Stream kernel with the frame heads taken out of the block stream (SH, pipe
+// 60).  The block span covers every captured byte of its 256 frames, known
+// from the descriptors alone, so the first tile's loads go out one descriptor
+// round trip after the block starts, with no head loads before them.  Each
+// frame's owner marks its head chunks (the first 4 of its 16-B chunks) in an
+// LDS map of the span (u8 per chunk: the owner, 0..254; 0xFF = none) and
+// publishes its first chunk; the lane that streams a marked chunk writes it to
+// the owner's 64-B LDS head slot at k = chunk - first.  (Thread 255 of a block
+// has no map value: it always reads its head from HBM.)  A frame's
+// tail sum is the prefix difference at two chunk boundaries known from the
+// descriptors: [64, caplen & ~15).  After the stream the owner parses its head
+// from LDS, probes the flow table and writes the verdict.  Exact, with
+// fallbacks that are rare in real bursts:
+//  - the L4 sum ends before the capture (14 + total_length < caplen, e.g.
+//    Ethernet padding): the owner re-sums [64, end) from HBM;
+//  - frames sharing head chunks (overlapping descriptors): the losers of the
+//    map write read their heads from HBM (checked after the map barrier), as
+//    does thread 255;
+//  - a span of scattered frames or one larger than the map (SH_MAPC chunks):
+//    per-thread head loads and tail loops.
+// LDS 31.9 KiB per block (map 7.25, heads 16, prefixes 8): 5 blocks per CU.
+constexpr uint32_t SH_MAPC = 7424; // span chunks the head map covers (116 KiB)
+
+// ABL (diagnostic builds, pipe 160): 1 = no flow-table probe (flow id from
+// the port: wrong verdicts by construction)
+template <int ABL = 0>
+__global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
+    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
+    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    constexpr uint32_t LPT = 4;          // 16-B chunks per thread per tile
+    constexpr uint32_t TCH = 256u * LPT; // chunks per tile (16 KiB)
+    __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[SH_MAPC];
+    __shared__ __attribute__((aligned(16))) uint4 s_hd[256 * 4];
+    __shared__ uint16_t s_rel[256]; // each frame's first chunk in the span
+    __shared__ unsigned long long s_lo, s_hi;
+    __shared__ uint32_t s_tail;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
+    if (tid == 0) {
+        s_lo = ~0ull;
+        s_hi = 0;
+        s_tail = 0;
+    }
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+    {
+        uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
+        for (uint32_t i = tid; i < SH_MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
+    const bool valid = p < n;
+    const uint64_t q = valid ? p : 0;
+    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
+    const uint8_t *fb = pkts + fpos;
+    const int32_t cp = valid ? (int32_t)len[q] : 0;
+    const uint64_t fc = fpos >> 4;                       // first chunk (absolute)
+    const uint32_t nch = ((uint32_t)cp + 15u) >> 4;      // chunks of the capture
+    const int32_t cf = cp & ~15;                         // full chunks: [0, cf)
+    // the partial last chunk past the head (descriptor-derived), used after the stream
+    const uint4 pcv = ldg16<false>(fb + (cf < cp && cf >= 64 ? cf : 0));
+    __syncthreads(); // s_lo/s_hi/s_tail and the map initialised
+    span_add(cp > 0, fc, fc + nch, &s_lo, &s_hi, &s_tail, lane);
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    const uint32_t tsum = s_tail;
+    const bool streamed = hi > lo && hi - lo <= SH_MAPC && hi - lo <= 2ull * tsum + TCH;
+    const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
+    const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
+    auto tile_load = [&](uint4 *v, uint32_t c0) {
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const uint32_t k = c0 + j * 256 + tid;
+            v[j] = ldg16<true>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
+        }
+    };
+    uint4 va[LPT], vb[LPT];
+    tile_load(va, 0);
+    const uint32_t rel = (streamed && cp > 0) ? (uint32_t)(fc - lo) : 0u;
+    const uint32_t nh = nch < 4u ? nch : 4u;
+    const bool mapped = streamed && tid < 255u;
+    if (mapped) {
+        for (uint32_t k = 0; k < nh; ++k) s_map[rel + k] = (uint8_t)tid;
+        s_rel[tid] = (uint16_t)rel;
+    }
+    __syncthreads(); // map complete
+    bool direct = !mapped && cp > 0;
+    if (mapped)
+        for (uint32_t k = 0; k < nh; ++k)
+            if (s_map[rel + k] != (uint8_t)tid) direct = true; // shared head chunk
+    uint4 hd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hd[k] = make_uint4(0, 0, 0, 0);
+    if (__ballot(direct) != 0ull) { // rare (wave-uniform branch)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hd[k] = ldg16<false>(direct && 16 * k < cp ? fb + 16 * k : pkts);
+    }
+
+    // ---- stream: tile prefixes, head capture, boundary pickup ---------------
+    const bool tailf = cf > 64; // full chunks past the head: [4, cf / 16)
+    const uint32_t cs = tailf ? rel + 4u : 0xFFFFFFFFu;
+    const uint32_t ce = tailf ? rel + ((uint32_t)cf >> 4) : 0xFFFFFFFFu;
+    uint32_t es = 0, ee = 0, carry = 0;
+    auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
+        uint32_t sj[LPT], xj[LPT];
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const uint32_t k = c0 + j * 256 + tid;
+            sj[j] = k < span ? chunk_sum(v[j]) : 0u;
+            xj[j] = sj[j];
+            if (k < span) {
+                const uint32_t m = s_map[k];
+                if (m != 0xFFu) s_hd[m * 4u + (k - s_rel[m])] = v[j];
+            }
+        }
+        wave_incl_scan_n<LPT>(xj);
+        if (lane == 63) {
+#pragma unroll
+            for (int j = 0; j < LPT; ++j) s_wt[buf][j * 4 + wv] = xj[j];
+        }
+        __syncthreads();
+        { // the previous tile's boundaries (buffer buf ^ 1)
+            const uint32_t p0 = c0 - TCH; // wraps for c0 = 0: no frame matches
+            if (c0 != 0 && cs - p0 < TCH) es = s_pre[buf ^ 1u][cs - p0];
+            if (c0 != 0 && ce - p0 < TCH) ee = s_pre[buf ^ 1u][ce - p0];
+        }
+        uint32_t wt[4 * LPT]; // block-uniform: kept in SGPRs
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const uint4 r = *reinterpret_cast<const uint4 *>(&s_wt[buf][j * 4]);
+            wt[j * 4 + 0] = __builtin_amdgcn_readfirstlane(r.x);
+            wt[j * 4 + 1] = __builtin_amdgcn_readfirstlane(r.y);
+            wt[j * 4 + 2] = __builtin_amdgcn_readfirstlane(r.z);
+            wt[j * 4 + 3] = __builtin_amdgcn_readfirstlane(r.w);
+        }
+        uint32_t base = carry;
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            uint32_t wb = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) wb += (uint32_t)w < wvu ? wt[j * 4 + w] : 0u;
+            s_pre[buf][j * 256 + tid] = base + wb + xj[j] - sj[j];
+            base += wt[j * 4] + wt[j * 4 + 1] + wt[j * 4 + 2] + wt[j * 4 + 3];
+        }
+        carry = base;
+    };
+    uint32_t c0 = 0;
+    for (; c0 < span; c0 += 2 * TCH) {
+        tile_load(vb, c0 + TCH);
+        tile(va, c0, 0);
+        tile_load(va, c0 + 2 * TCH);
+        tile(vb, c0 + TCH, 1);
+    }
+    __syncthreads(); // the last tile's prefixes and every head slot written
+    if (streamed) {
+        const uint32_t p0 = c0 - TCH;
+        if (cs - p0 < TCH) es = s_pre[1][cs - p0];
+        if (ce - p0 < TCH) ee = s_pre[1][ce - p0];
+        if (ce == span) ee = carry;
+    }
+
+    // ---- head: parse ----------------------------------------------------------
+    uint4 c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = direct ? hd[k] : s_hd[tid * 4u + k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
+    const uint32_t et = c[0].w & 0xFFFFu;
+    const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
+    const uint32_t proto = c[1].y >> 24;
+    const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
+    const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
+    const uint32_t sport = c[2].x >> 16;
+    const uint32_t dport = c[2].y & 0xFFFFu;
+    const uint32_t dgl = rx_bswap16(c[2].y >> 16);
+    const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+    uint32_t cl, nd;
+    if (et == 0x0608u) {
+        cl = RXG_CLS_ARP;
+        nd = 42;
+    } else if (et != 0x0008u) {
+        cl = RXG_CLS_NON_IP;
+        nd = 14;
+    } else if (proto == 17u) {
+        cl = RXG_CLS_UDP;
+        nd = 42;
+    } else if (proto == 6u) {
+        cl = RXG_CLS_TCP;
+        nd = 54;
+    } else {
+        cl = RXG_CLS_IPV4_OTHER;
+        nd = 24;
+    }
+    const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
+    const bool l4 = is_udp || is_tcp;
+    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+    const bool do_sum = l4 && tl >= 20u;
+    if (l4 && 34u + l4n > nd) nd = 34u + l4n;
+    int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
+    if (e > cp) e = cp;
+
+    // ---- flow probe loads (consumed below, after the sums) --------------------
+    const bool probe = valid && l4;
+    const uint32_t ka = is_udp ? dip : sip;
+    const uint32_t kb = is_udp ? dport : dip;
+    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
+    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
+    const bool probe0 = probe && maxp > 0 && !(ABL & 1);
+    const bool udp_port = is_udp && ft.udp_port != nullptr;
+    const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+    const uint32_t pe = (ABL & 1) ? RXG_FLOW_NONE : ptab[l4 ? dport : 0u];
+    const bool hash0 = probe0 && !udp_port;
+    const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
+                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                             : reinterpret_cast<const uint4 *>(fb);
+    const uint4 sl0 = ld_slot(sp0);
+
+    // ---- checksum -----------------------------------------------------------------
+    uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+    h1.x = 0;
+    h1.y = 0;
+    h1.z &= 0xFFFF0000u;
+    if (is_udp) h2.z &= 0xFFFF0000u;
+    if (is_tcp) h3.x &= 0x0000FFFFu;
+    uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
+    acc = lane_chunk_sum(acc, h2, 32, e);
+    acc = lane_chunk_sum(acc, h3, 48, e);
+    if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
+    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+    // the sum ends where the capture does (the common case): tail from the
+    // stream prefixes, the partial chunk from pcv; otherwise re-sum from HBM
+    const bool fast = streamed && e == cp;
+    if (do_sum && e > 64) {
+        if (fast) {
+            if (tailf) acc += ee - es;
+            if (cf < cp && cf >= 64) acc = lane_chunk_sum(acc, pcv, cf, e);
+        } else {
+            for (int32_t s = 64; s < e; s += 16) acc = lane_chunk_sum(acc, ldg16<false>(fb + s), s, e);
+        }
+    }
+
+    // ---- verdict --------------------------------------------------------------------
+    uint32_t flags = 0, poff = 0, plen = 0;
+    if (is_udp) {
+        poff = 42;
+        plen = dgl > 8u ? dgl - 8u : 0u;
+        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+    } else if (is_tcp) {
+        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
+        poff = 34u + 4u * hl;
+        if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+        plen = pl < 0 ? 0u : (uint32_t)pl;
+    }
+    const bool trunc = (int32_t)nd > cp;
+    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
+    uint32_t flow = RXG_FLOW_NONE;
+    int32_t rc = RXG_RC_KNI;
+    bool hashed = probe0;
+    if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
+    if (hashed) {
+        const uint4 *tb = is_udp ? ft.udp : ft.tcp;
+        const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
+        uint32_t pj = rx_hash3(ka, kb, kc) & mk;
+        uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
+        for (uint32_t pr = 0;;) {
+            if (sl.w == RX_SLOT_EMPTY) break;
+            if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                flow = sl.w;
+                break;
+            }
+            if (++pr >= maxp) break;
+            pj = (pj + 1) & mk;
+            sl = ld_slot(tb + pj);
+        }
+    }
+    if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
+    if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
+    if (is_udp)
+        rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                   : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+    if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+    uint32_t ck = 0;
+    if (do_sum) {
+        ck = (~fold16(acc)) & 0xFFFFu;
+        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
+    }
+    const bool ok = l4 && stored == ck;
+    if (is_tcp) {
+        if (!ok) flow = RXG_FLOW_NONE;
+        rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+    }
+    if (valid) {
+        uint4 vd;
+        vd.x = flow;
+        vd.y = (poff & 0xFFFFu) | (plen << 16);
+        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+        stg16(&out[p], vd);
+        const uint32_t cidx =
+            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+        lane_count(cidx, counts, hist, lds_bins);
+        if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
+    }
+    if (lds_bins) {
+        __syncthreads();
+        for (uint32_t i = tid; i < lds_bins; i += 256) {
+            const uint32_t cnt = hist[i];
+            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
+        }
+    }
+}
+
+template <int ABL = 0>
+hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
+                     unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
+                     const uint32_t *, const uint32_t *) {
+    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rx_classify_sh_kernel<ABL>, dim3((uint32_t)blocks), dim3(256),
+                       (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
+                       lds_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
 // memory-side request): the classify kernel writes one count index per frame
@@ -1930,6 +2258,8 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
     {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, true>},
+    // 60: heads taken out of the block stream (SH kernel)
+    {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
 };
 
 } // namespace
@@ -1970,51 +2300,72 @@ bool rx_variant_exists(uint32_t g, uint32_t pipe) {
 }
 
 // workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
-// frame), then the count indices (room for 4 B per frame) and the count slabs
+// frame), then nbuf count-index buffers (room for 4 B per frame each: two when
+// the counts of one burst run on a second stream while the next burst is
+// classified, rxg_classify_dev_cs) and the count slabs
+static size_t ws_lists_bytes(uint32_t n, uint32_t g, uint32_t pipe) {
+    return (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
+}
+static size_t ws_cidx_bytes(uint32_t n) { return ((size_t)n * 4 + 255) & ~(size_t)255; }
+
+bool rx_count_uses_slabs(const rx_ft_dev &ft, bool counts) { return use_slab(ft, counts); }
+
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
-                            bool counts) {
-    size_t b = (g == 0 && pipe == 20) ? 16 + 8ull * n : 0;
+                            bool counts, uint32_t nbuf) {
+    size_t b = ws_lists_bytes(n, g, pipe);
     if (use_slab(ft, counts)) {
         uint32_t nslabs, per;
         slab_geometry(n, slab_ranges(ft), &nslabs, &per);
-        b = ((b + 255) & ~(size_t)255) + (((size_t)n * 4 + 255) & ~(size_t)255) +
-            (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
+        b += ws_cidx_bytes(n) * std::max(nbuf, 1u) +
+             (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
     }
     return b;
 }
 
+// phase: RX_PH_ALL = classify then (slab path) count, both on s; RX_PH_CLASSIFY
+// = the classify kernel only, writing count indices into index buffer `buf`;
+// RX_PH_COUNT = the slab + reduce passes over index buffer `buf` only (the
+// caller orders it after the RX_PH_CLASSIFY launch that filled the buffer).
+// Without the slab path (few flows, or no counts) RX_PH_COUNT does nothing and
+// the other two count inside the classify kernel.
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft_in, uint4 *out,
-                              unsigned long long *counts, hipStream_t s, uint32_t *ws) {
+                              unsigned long long *counts, hipStream_t s, uint32_t *ws,
+                              uint32_t phase, uint32_t buf, uint32_t nbuf) {
     if (n == 0) return hipSuccess;
     const uint32_t nflows = ft_in.nu + ft_in.nt;
     const bool slab = use_slab(ft_in, counts != nullptr);
     if (slab && !ws) return hipErrorInvalidValue;
-    unsigned long long *kcounts = slab ? nullptr : counts; // slab: counted after classify
-    const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
-    // workspace: [binned lists][count indices][slabs]
-    const size_t lists = (g == 0 && pipe == 20) ? ((16 + 8ull * n + 255) & ~(size_t)255) : 0;
-    uint8_t *cidx = slab ? reinterpret_cast<uint8_t *>(ws) + lists : nullptr;
+    if (buf >= std::max(nbuf, 1u)) return hipErrorInvalidValue;
+    // workspace: [binned lists][count indices x nbuf][slabs]
+    const size_t lists = ws_lists_bytes(n, g, pipe);
+    uint8_t *cidx = slab ? reinterpret_cast<uint8_t *>(ws) + lists + ws_cidx_bytes(n) * buf : nullptr;
     rx_ft_dev ft = ft_in;
     ft.count_idx = cidx;
     ft.cidx16 = slab && cidx16(ft_in) && !ft_in.count_4b;
-    hipError_t e = hipErrorInvalidValue;
-    if (g == 0 && pipe == 20) { // size-class binned (workspace: 16 B + 8 B per frame)
-        e = launch_binned(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, ws);
-    } else {
-        for (const variant_entry &v : k_variants)
-            if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
-                (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
-                const uint32_t user_cap = g_bpc_cap;
-                if (!user_cap) g_bpc_cap = v.bpc;
-                e = v.fn(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, nullptr,
-                         nullptr);
-                g_bpc_cap = user_cap;
-                break;
-            }
+    if (phase != RX_PH_COUNT) {
+        unsigned long long *kcounts = slab ? nullptr : counts; // slab: counted after classify
+        const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
+        hipError_t e = hipErrorInvalidValue;
+        if (g == 0 && pipe == 20) { // size-class binned (workspace: 16 B + 8 B per frame)
+            e = launch_binned(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, ws);
+        } else {
+            for (const variant_entry &v : k_variants)
+                if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
+                    (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
+                    const uint32_t user_cap = g_bpc_cap;
+                    if (!user_cap) g_bpc_cap = v.bpc;
+                    e = v.fn(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, nullptr,
+                             nullptr);
+                    g_bpc_cap = user_cap;
+                    break;
+                }
+        }
+        if (e != hipSuccess) return e;
     }
-    if (e != hipSuccess || !slab) return e;
-    uint32_t *slabs = reinterpret_cast<uint32_t *>(cidx + (((size_t)n * 4 + 255) & ~(size_t)255));
+    if (!slab || phase == RX_PH_CLASSIFY) return hipSuccess;
+    uint32_t *slabs = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists +
+                                                   ws_cidx_bytes(n) * std::max(nbuf, 1u));
     return launch_count_slab(cidx, out, n, ft, counts, slabs, s);
 }

@@ -58,6 +58,9 @@ struct rx_ft_dev {
     uint32_t count_4b;
 };
 
+// rx_classify_launch phases (host side)
+enum { RX_PH_ALL = 0, RX_PH_CLASSIFY = 1, RX_PH_COUNT = 2 };
+
 // frame p's count index (idx = ~0u: not counted) on the slab count path
 RX_HD void rx_put_count_idx(const rx_ft_dev &ft, uint64_t p, uint32_t idx) {
     if (ft.cidx16)

@@ -64,7 +64,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
                    (0, 0, 0, 46),  # 38 with the span from the descriptors
-                   (0, 0, 0, 54)]  # 38 with heads gathered four lanes per head
+                   (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
+                   (0, 0, 0, 60)]  # heads taken out of the block stream
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -114,6 +115,8 @@ _strerror = _sig("rxg_strerror", C.c_char_p, _i32)
 _last_hip = _sig("rxg_last_hip_error", C.c_char_p)
 _flows_sync = _sig("rxg_flows_sync", _i32, _vp, _vp, _u32, _vp, _u32)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
+_classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
+                        _vp, _vp)
 _classify = _sig("rxg_classify", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp)
 _classify_span = _sig("rxg_classify_span", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32, _vp)
 _process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
@@ -159,7 +162,7 @@ MAX_SHARDS = 64
 GROUP_ID_BYTES = 128
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
-            "rxg_classify_dev", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
+            "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
@@ -301,12 +304,19 @@ class Context:
         _check(_wait(self._h, ticket), "rxg_wait")
 
     def classify_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
-                     d_out, d_counts=None, stream=None):
-        """Device tensors in/out (torch tensors or raw ints), asynchronous on `stream`."""
+                     d_out, d_counts=None, stream=None, count_stream=None):
+        """Device tensors in/out (torch tensors or raw ints), asynchronous on
+        `stream`; with count_stream (a raw hipStream_t), d_counts is completed
+        on that stream instead (rxg_classify_dev_cs)"""
         def p(x):
             return x if (x is None or isinstance(x, int)) else x.data_ptr()
-        _check(_classify_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, len_hint,
-                             p(d_out), p(d_counts), stream), "rxg_classify_dev")
+        if count_stream is None:
+            _check(_classify_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2,
+                                 len_hint, p(d_out), p(d_counts), stream), "rxg_classify_dev")
+        else:
+            _check(_classify_dev_cs(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2,
+                                    len_hint, p(d_out), p(d_counts), stream, count_stream),
+                   "rxg_classify_dev_cs")
 
     def tx_cksum(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
                  off_unit_log2: int) -> np.ndarray:

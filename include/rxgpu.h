@@ -159,6 +159,21 @@ int rxg_classify_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
                      uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
                      void *stream);
 
+/* rxg_classify_dev with the per-flow counts on a second stream: the verdicts
+ * are written on `stream` as above; d_counts is complete once `count_stream`
+ * (ordered after this burst's classify) has reached this point, not `stream`.
+ * Above 8192 flows the counts are two passes after the classify kernel
+ * (DESIGN.md §4); on count_stream they overlap the NEXT burst's classify on
+ * `stream` (the context double-buffers its count indices), which is how a
+ * burst loop hides them.  The caller orders readers of d_counts (a copy, the
+ * RCCL all-reduce) after count_stream.  count_stream NULL or == stream: same
+ * as rxg_classify_dev.  Replaces no reference call: the reference keeps no
+ * per-flow counters; this is the statistic the multi-GPU path all-reduces. */
+int rxg_classify_dev_cs(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
+                        void *stream, void *count_stream);
+
 /* Host-buffer burst (PCIe-inclusive): copies frames + descriptors to the
  * device, classifies, copies verdicts back, accumulates the context's own
  * per-flow counts.  Synchronous. */

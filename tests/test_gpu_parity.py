@@ -245,7 +245,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
-                                     (0, 0, 0, 46), (0, 0, 0, 54),
+                                     (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 60),
                                      (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor
@@ -285,7 +285,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
-                                     (4, 1, 2, 0)])
+                                     (0, 0, 0, 60), (4, 1, 2, 0)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
     frames shuffled inside each 256-frame block (streamed, unordered
@@ -349,6 +349,49 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
         got = d_out.cpu().numpy().view(R.VERDICT_DTYPE)
         assert got.tobytes() == want.tobytes(), _mismatch_report(got, want)
     assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 2 * wcnt)
+
+
+@pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 54)])
+@pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix"])
+def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
+    """the SH stream kernel's exact fallbacks, against the oracle: frames whose
+    L4 sum ends before the capture (random bytes after the IP datagram, as
+    Ethernet padding), descriptors sharing or overlapping head chunks
+    (duplicates, and starts 16 B into another frame), and blocks whose span
+    exceeds the head map (jumbo frames among IMIX ones)"""
+    rng = np.random.default_rng({"padded": 1, "overlap": 2, "jumbo_mix": 3}[case])
+    cfg = rxdist.gen_cfg("cfg4", n_udp=400, n_tcp=400)
+    udp, tcb = R.gen_flows(cfg)
+    pk, off, ln = R.gen_host(cfg, 77, 3000, 6)
+    frames = [pk[int(o) << 6:(int(o) << 6) + int(l)].tobytes() for o, l in zip(off, ln)]
+    if case == "padded":
+        frames = [f + bytes(rng.integers(0, 256, int(rng.integers(1, 40)), np.uint8))
+                  if rng.random() < 0.3 else f for f in frames]
+    elif case == "jumbo_mix":
+        jcfg = rxdist.gen_cfg("cfg5", n_tcp=400)
+        jpk, joff, jln = R.gen_host(jcfg, 5, 40, 6)
+        jumbo = [jpk[int(o) << 6:(int(o) << 6) + int(l)].tobytes() for o, l in zip(joff, jln)]
+        for k, j in enumerate(jumbo):  # 40 jumbo frames over the first blocks
+            frames.insert(37 * k + 5, j)
+        tcb = np.concatenate([tcb, R.gen_flows(jcfg)[1]])
+    buf, off, lens = F.pack_frames(frames, 4)
+    if case == "overlap":
+        off, lens = off.copy(), lens.copy()
+        for i in range(1, len(off), 7):
+            if rng.random() < 0.5:  # the previous frame again
+                off[i], lens[i] = off[i - 1], lens[i - 1]
+            else:  # 16 B into the previous frame, to its end
+                off[i] = off[i - 1] + 1
+                lens[i] = max(int(lens[i - 1]) - 16, 0)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(buf, off, lens, 4, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 354, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, case, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), (variant, case)
 
 
 def test_fuzzed_frames_match_oracle(ctx, torch_dev):

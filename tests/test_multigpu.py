@@ -202,3 +202,45 @@ def test_one_context_two_streams_share_workspace(torch_dev):
     for o, c in ((o1, c1), (o2, c2)):
         assert o.cpu().numpy().view(R.VERDICT_DTYPE).tobytes() == want.tobytes()
         assert np.array_equal(c.cpu().numpy().view(np.uint64), 4 * wcnt)
+
+
+@pytest.mark.parametrize("nu,nt,n", [(6000, 6000, 40000), (40000, 30000, 12000)])
+def test_counts_on_a_second_stream(torch_dev, nu, nt, n):
+    """rxg_classify_dev_cs: verdicts on the classify stream, the slab count on a
+    count stream, overlapping the next burst's classify (two index buffers in
+    the context).  Two different bursts alternate, a plain rxg_classify_dev
+    burst and a burst of another size (the workspace regions move) are mixed
+    in: every verdict is bit-exact and the counts add up to the histograms"""
+    torch, dev = torch_dev
+    cfg = rxdist.gen_cfg("cfg4", n_udp=nu, n_tcp=nt, other_per10k=300)
+    udp, tcb = R.gen_flows(cfg)
+    tb = O.Tables(udp, tcb)
+    bursts = []
+    for first, m in ((17, n), (5 * n, n), (9 * n, n // 2 + 3)):
+        pk, off, ln = R.gen_host(cfg, first, m, 6)
+        want, wcnt = tb.classify(pk, off, ln, 6, counts=True)
+        bursts.append((_to_dev(torch, dev, pk, off, ln), m, want, wcnt))
+    s, cs = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    order = [0, 1, 0, 1, 1, 2, 0, 2, 1, 0]  # burst index per step
+    plain = {3, 7}                           # these steps use rxg_classify_dev on s
+    with R.Context(0) as ctx:
+        ctx.flows_sync(udp, tcb)
+        cnt = torch.zeros(ctx.num_flows, dtype=torch.int64, device=dev)
+        outs = []
+        for k, b in enumerate(order):
+            (d_pk, d_off, d_ln), m, _, _ = bursts[b]
+            o = torch.empty(m * 16, dtype=torch.uint8, device=dev)
+            if k in plain:
+                s.wait_stream(cs)  # the caller orders its own count target
+                ctx.classify_dev(d_pk, d_off, d_ln, m, 6, 354, o, cnt, stream=s.cuda_stream)
+                cs.wait_stream(s)
+            else:
+                ctx.classify_dev(d_pk, d_off, d_ln, m, 6, 354, o, cnt, stream=s.cuda_stream,
+                                 count_stream=cs.cuda_stream)
+            outs.append(o)
+        torch.cuda.synchronize(dev)
+    want_cnt = sum(bursts[b][3].astype(np.uint64) for b in order)
+    for k, b in enumerate(order):
+        got = outs[k].cpu().numpy().view(R.VERDICT_DTYPE)
+        assert got.tobytes() == bursts[b][2].tobytes(), k
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), want_cnt)
