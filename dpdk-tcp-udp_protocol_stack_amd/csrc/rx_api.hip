@@ -99,9 +99,10 @@ struct ft_host {
         const uint64_t n = entries.size();
         uint64_t ns = 16;
         while (ns < (n << load_log2)) ns <<= 1;
-        // one slot past the end mirrors slot 0, so a two-slot probe window at
-        // any index reads in bounds (the stream kernel's first probe)
-        slots.assign(ns + 1, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
+        // RX_FT_MIRROR slots past the end mirror slots 0.., so a probe window of
+        // up to RX_FT_MIRROR + 1 slots at any index reads in bounds (the stream
+        // kernels' first probe)
+        slots.assign(ns + RX_FT_MIRROR, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
         mask = (uint32_t)(ns - 1);
         probe = 1;
         for (const uint4 &e : entries) {
@@ -119,7 +120,7 @@ struct ft_host {
                 break;
             }
         }
-        slots[ns] = slots[0];
+        for (uint32_t k = 0; k < RX_FT_MIRROR; ++k) slots[ns + k] = slots[k];
     }
 
     uint32_t lookup(uint32_t a, uint32_t b, uint32_t c) const {
@@ -144,7 +145,8 @@ static void build_udpc(const ft_host &u, uint32_t nu, std::vector<uint2> *out, u
     while (ns < 2 * nu) ns <<= 1;
     out->assign(ns, make_uint2(0, 0xFFFFFFFFu));
     const uint32_t mask = ns - 1;
-    for (const uint4 &sl : u.slots) {
+    for (uint32_t j = 0; j <= u.mask; ++j) { // (past the mask: mirrors)
+        const uint4 &sl = u.slots[j];
         if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> flow
         uint32_t i = rx_hash3(sl.x, sl.y, sl.z) & mask;
         uint32_t d = 0;
@@ -160,13 +162,13 @@ static void build_udpc(const ft_host &u, uint32_t nu, std::vector<uint2> *out, u
 // those other addresses probe the hashed table, which holds every key.
 static uint32_t build_udp_port(const ft_host &u, std::vector<uint32_t> *port) {
     std::unordered_map<uint32_t, uint32_t> dips; // dip -> sockets bound to it
-    for (uint32_t i = 0; i + 1 < u.slots.size(); ++i)
+    for (uint32_t i = 0; i <= u.mask; ++i)
         if (u.slots[i].w != RX_SLOT_EMPTY) ++dips[u.slots[i].x];
     uint32_t dip = 0, best = 0;
     for (const auto &d : dips)
         if (d.second > best || (d.second == best && d.first < dip)) best = d.second, dip = d.first;
     port->assign(65536, RX_PORT_NONE);
-    for (uint32_t i = 0; i + 1 < u.slots.size(); ++i) { // (the last slot mirrors slot 0)
+    for (uint32_t i = 0; i <= u.mask; ++i) { // (past the mask: mirrors)
         const uint4 &sl = u.slots[i];
         if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> newest flow
         uint32_t &e = (*port)[sl.y & 0xFFFFu];

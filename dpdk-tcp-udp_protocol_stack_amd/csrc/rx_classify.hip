@@ -1363,9 +1363,10 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
         const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
                                        (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
                                  : reinterpret_cast<const uint4 *>(fb);
-        const uint4 sl0 = ld_slot(sp0);
-        uint4 sl1 = sl0;
-        if constexpr (PW == 2) sl1 = ld_slot(sp0 + (hash0 ? 1 : 0));
+        static_assert(PW == 1 || PW == 2 || PW == 4, "probe window");
+        uint4 sw[PW];
+#pragma unroll
+        for (int w = 0; w < PW; ++w) sw[w] = ld_slot(sp0 + (hash0 ? w : 0));
 
         uint4 h1 = c[1], h2 = c[2], h3 = c[3];
         h1.x = 0;
@@ -1422,8 +1423,28 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
                 const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
                 uint32_t pj = rx_hash3(ka, kb, kc) & mk;
-                uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
-                for (uint32_t pr = 0;;) {
+                uint32_t pr = 0;
+                bool done = false;
+                if (hash0) { // the window loaded with the head
+#pragma unroll
+                    for (int w = 0; w < PW; ++w) {
+                        if (!done) {
+                            const uint4 sl = sw[w];
+                            if (sl.w == RX_SLOT_EMPTY) {
+                                done = true;
+                            } else if (sl.x == ka && sl.y == kb && sl.z == kc) {
+                                flow = sl.w;
+                                done = true;
+                            } else if (++pr >= mp) {
+                                done = true;
+                            } else {
+                                pj = (pj + 1) & mk;
+                            }
+                        }
+                    }
+                }
+                while (!done) { // past the window, or a UDP key on a shared port
+                    const uint4 sl = ld_slot(tb + pj);
                     if (sl.w == RX_SLOT_EMPTY) break;
                     if (sl.x == ka && sl.y == kb && sl.z == kc) {
                         flow = sl.w;
@@ -1431,13 +1452,6 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                     }
                     if (++pr >= mp) break;
                     pj = (pj + 1) & mk;
-                    if constexpr (PW == 2) {
-                        if (pr == 1 && hash0) {
-                            sl = sl1;
-                            continue;
-                        }
-                    }
-                    sl = ld_slot(tb + pj);
                 }
             }
             if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
@@ -1584,10 +1598,11 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 // from the descriptors alone, so the first tile's loads go out one descriptor
 // round trip after the block starts, with no head loads before them.  Each
 // frame's owner marks its head chunks (the first 4 of its 16-B chunks) in an
-// LDS map of the span (u8 per chunk: the owner, 0..254; 0xFF = none) and
-// publishes its first chunk; the lane that streams a marked chunk writes it to
-// the owner's 64-B LDS head slot at k = chunk - first.  (Thread 255 of a block
-// has no map value: it always reads its head from HBM.)  A frame's
+// LDS map of the span (u8 per chunk: the owner; 0xFF is also "none") and
+// publishes its first chunk; the lane that streams a chunk writes it to the
+// owner's 64-B LDS head slot at k = chunk - first when k < 4 (an unmarked
+// chunk reads as thread 255's, whose k is then out of range or past its
+// capture, masked).  A frame's
 // tail sum is the prefix difference at two chunk boundaries known from the
 // descriptors: [64, caplen & ~15).  After the stream the owner parses its head
 // from LDS, probes the flow table and writes the verdict.  Exact, with
@@ -1595,16 +1610,68 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 //  - the L4 sum ends before the capture (14 + total_length < caplen, e.g.
 //    Ethernet padding): the owner re-sums [64, end) from HBM;
 //  - frames sharing head chunks (overlapping descriptors): the losers of the
-//    map write read their heads from HBM (checked after the map barrier), as
-//    does thread 255;
+//    map write read their heads from HBM after the stream (checked after the
+//    map barrier);
 //  - a span of scattered frames or one larger than the map (SH_MAPC chunks):
 //    per-thread head loads and tail loops.
 // LDS 31.9 KiB per block (map 7.25, heads 16, prefixes 8): 5 blocks per CU.
 constexpr uint32_t SH_MAPC = 7424; // span chunks the head map covers (116 KiB)
 
-// ABL (diagnostic builds, pipe 160): 1 = no flow-table probe (flow id from
-// the port: wrong verdicts by construction)
-template <int ABL = 0>
+// header fields of a frame head (the first 64 B, bytes past caplen zeroed)
+struct sh_head {
+    uint32_t cl, nd, tl, proto, l4n, dgl, hl, ka, kb, kc, stored;
+    bool is_udp, is_tcp, l4, do_sum;
+    int32_t e; // end of the checksummed bytes
+};
+
+__device__ __forceinline__ sh_head sh_parse(const uint4 (&c)[4], int32_t cp) {
+    sh_head h;
+    const uint32_t et = c[0].w & 0xFFFFu;
+    h.tl = rx_bswap16(c[1].x & 0xFFFFu);
+    h.proto = c[1].y >> 24;
+    const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
+    const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
+    const uint32_t sport = c[2].x >> 16;
+    const uint32_t dport = c[2].y & 0xFFFFu;
+    h.dgl = rx_bswap16(c[2].y >> 16);
+    h.hl = ((c[2].w >> 16) & 0xFFu) >> 4;
+    if (et == 0x0608u) {
+        h.cl = RXG_CLS_ARP;
+        h.nd = 42;
+    } else if (et != 0x0008u) {
+        h.cl = RXG_CLS_NON_IP;
+        h.nd = 14;
+    } else if (h.proto == 17u) {
+        h.cl = RXG_CLS_UDP;
+        h.nd = 42;
+    } else if (h.proto == 6u) {
+        h.cl = RXG_CLS_TCP;
+        h.nd = 54;
+    } else {
+        h.cl = RXG_CLS_IPV4_OTHER;
+        h.nd = 24;
+    }
+    h.is_udp = h.cl == RXG_CLS_UDP;
+    h.is_tcp = h.cl == RXG_CLS_TCP;
+    h.l4 = h.is_udp || h.is_tcp;
+    h.l4n = h.tl >= 20u ? h.tl - 20u : 0u;
+    h.do_sum = h.l4 && h.tl >= 20u;
+    if (h.l4 && 34u + h.l4n > h.nd) h.nd = 34u + h.l4n;
+    h.e = h.do_sum ? 34 + (int32_t)h.l4n : 0;
+    if (h.e > cp) h.e = cp;
+    h.ka = h.is_udp ? dip : sip;
+    h.kb = h.is_udp ? dport : dip;
+    h.kc = h.is_udp ? 17u : (sport | (dport << 16));
+    h.stored = h.is_udp ? (c[2].z & 0xFFFFu) : (h.is_tcp ? (c[3].x >> 16) : 0u);
+    return h;
+}
+
+// ABL (diagnostic builds, pipe 160): 1 = no flow-table probe (flow id from the
+// port: wrong verdicts by construction).  PW: slots of the first probe window
+// (1, 2 or 4 consecutive slots of the hashed table loaded together; the table
+// mirrors its first slots past its end), so a displaced key costs no dependent
+// second round trip at the end of the block (pipes 60 / 63 / 64).
+template <int ABL = 0, int PW = 1>
 __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1621,12 +1688,12 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     __shared__ uint32_t s_tail;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
     if (tid == 0) {
         s_lo = ~0ull;
         s_hi = 0;
         s_tail = 0;
     }
-    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
     {
         uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
         for (uint32_t i = tid; i < SH_MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -1635,11 +1702,11 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     const bool valid = p < n;
     const uint64_t q = valid ? p : 0;
     const uint64_t fpos = (uint64_t)off[q] << unit_log2;
-    const uint8_t *fb = pkts + fpos;
     const int32_t cp = valid ? (int32_t)len[q] : 0;
-    const uint64_t fc = fpos >> 4;                       // first chunk (absolute)
-    const uint32_t nch = ((uint32_t)cp + 15u) >> 4;      // chunks of the capture
-    const int32_t cf = cp & ~15;                         // full chunks: [0, cf)
+    const uint8_t *fb = pkts + fpos;
+    const uint64_t fc = fpos >> 4;                  // first chunk (absolute)
+    const uint32_t nch = ((uint32_t)cp + 15u) >> 4; // chunks of the capture
+    const int32_t cf = cp & ~15;                    // full chunks: [0, cf)
     // the partial last chunk past the head (descriptor-derived), used after the stream
     const uint4 pcv = ldg16<false>(fb + (cf < cp && cf >= 64 ? cf : 0));
     __syncthreads(); // s_lo/s_hi/s_tail and the map initialised
@@ -1661,39 +1728,58 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     tile_load(va, 0);
     const uint32_t rel = (streamed && cp > 0) ? (uint32_t)(fc - lo) : 0u;
     const uint32_t nh = nch < 4u ? nch : 4u;
-    const bool mapped = streamed && tid < 255u;
-    if (mapped) {
+    if (streamed) {
         for (uint32_t k = 0; k < nh; ++k) s_map[rel + k] = (uint8_t)tid;
         s_rel[tid] = (uint16_t)rel;
     }
     __syncthreads(); // map complete
-    bool direct = !mapped && cp > 0;
-    if (mapped)
+    bool direct = !streamed && cp > 0;
+    if (streamed)
         for (uint32_t k = 0; k < nh; ++k)
             if (s_map[rel + k] != (uint8_t)tid) direct = true; // shared head chunk
-    uint4 hd[4];
+
+    // ---- flow probe loads: the port entry (UDP: the direct port table; TCP:
+    // the listener) and the hashed table's home slot, issued once per frame
+    static_assert(PW == 1 || PW == 2 || PW == 4, "probe window");
+    static_assert(PW - 1 <= RX_FT_MIRROR, "window past the mirrored slots");
+    uint32_t pe = RXG_FLOW_NONE;
+    uint4 sw[PW];
+    auto issue_probe = [&](const uint4 (&c)[4]) {
+        const sh_head h = sh_parse(c, cp);
+        const bool probe0 =
+            valid && h.l4 && (h.is_udp ? ft.udp_probe : ft.tcp_probe) > 0 && !(ABL & 1);
+        const bool udp_port = h.is_udp && ft.udp_port != nullptr;
+        const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+        const uint32_t dport = h.is_udp ? h.kb : (h.kc >> 16);
+        const bool hash0 = probe0 && !udp_port;
+        const uint4 *sp0 =
+            hash0 ? (h.is_udp ? ft.udp : ft.tcp) +
+                        (rx_hash3(h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask))
+                  : reinterpret_cast<const uint4 *>(pkts);
+        pe = (ABL & 1) ? RXG_FLOW_NONE : ptab[h.l4 ? dport : 0u];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) hd[k] = make_uint4(0, 0, 0, 0);
-    if (__ballot(direct) != 0ull) { // rare (wave-uniform branch)
+        for (int w = 0; w < PW; ++w) sw[w] = ld_slot(sp0 + (hash0 ? w : 0));
+    };
+    auto head_of = [&](uint4 (&c)[4]) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) hd[k] = ldg16<false>(direct && 16 * k < cp ? fb + 16 * k : pkts);
-    }
+        for (int k = 0; k < 4; ++k) c[k] = chunk_below(s_hd[tid * 4u + k], 16 * k, cp);
+    };
 
     // ---- stream: tile prefixes, head capture, boundary pickup ---------------
     const bool tailf = cf > 64; // full chunks past the head: [4, cf / 16)
     const uint32_t cs = tailf ? rel + 4u : 0xFFFFFFFFu;
     const uint32_t ce = tailf ? rel + ((uint32_t)cf >> 4) : 0xFFFFFFFFu;
     uint32_t es = 0, ee = 0, carry = 0;
-    auto tile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
+    auto stile = [&](const uint4 *v, uint32_t c0, uint32_t buf) {
         uint32_t sj[LPT], xj[LPT];
 #pragma unroll
         for (int j = 0; j < LPT; ++j) {
             const uint32_t k = c0 + j * 256 + tid;
             sj[j] = k < span ? chunk_sum(v[j]) : 0u;
             xj[j] = sj[j];
-            if (k < span) {
-                const uint32_t m = s_map[k];
-                if (m != 0xFFu) s_hd[m * 4u + (k - s_rel[m])] = v[j];
+            if (k < span) { // (0xFF is thread 255 or no head: the k range tells)
+                const uint32_t m = s_map[k], hk = k - s_rel[m];
+                if (hk < 4u) s_hd[m * 4u + hk] = v[j];
             }
         }
         wave_incl_scan_n<LPT>(xj);
@@ -1730,9 +1816,9 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     uint32_t c0 = 0;
     for (; c0 < span; c0 += 2 * TCH) {
         tile_load(vb, c0 + TCH);
-        tile(va, c0, 0);
+        stile(va, c0, 0);
         tile_load(va, c0 + 2 * TCH);
-        tile(vb, c0 + TCH, 1);
+        stile(vb, c0 + TCH, 1);
     }
     __syncthreads(); // the last tile's prefixes and every head slot written
     if (streamed) {
@@ -1742,133 +1828,110 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
         if (ce == span) ee = carry;
     }
 
-    // ---- head: parse ----------------------------------------------------------
-    uint4 c[4];
+    // ---- head: parse, checksum, probe, verdict ------------------------------------
+    if (__ballot(direct) != 0ull) { // rare (wave-uniform branch): heads from HBM
+        uint4 hd[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = direct ? hd[k] : s_hd[tid * 4u + k];
+        for (int k = 0; k < 4; ++k) hd[k] = ldg16<false>(direct && 16 * k < cp ? fb + 16 * k : pkts);
+        if (direct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = chunk_below(c[j], 16 * j, cp); // past caplen reads as 0
-    const uint32_t et = c[0].w & 0xFFFFu;
-    const uint32_t tl = rx_bswap16(c[1].x & 0xFFFFu);
-    const uint32_t proto = c[1].y >> 24;
-    const uint32_t sip = (c[1].z >> 16) | (c[1].w << 16);
-    const uint32_t dip = (c[1].w >> 16) | (c[2].x << 16);
-    const uint32_t sport = c[2].x >> 16;
-    const uint32_t dport = c[2].y & 0xFFFFu;
-    const uint32_t dgl = rx_bswap16(c[2].y >> 16);
-    const uint32_t hl = ((c[2].w >> 16) & 0xFFu) >> 4;
-    uint32_t cl, nd;
-    if (et == 0x0608u) {
-        cl = RXG_CLS_ARP;
-        nd = 42;
-    } else if (et != 0x0008u) {
-        cl = RXG_CLS_NON_IP;
-        nd = 14;
-    } else if (proto == 17u) {
-        cl = RXG_CLS_UDP;
-        nd = 42;
-    } else if (proto == 6u) {
-        cl = RXG_CLS_TCP;
-        nd = 54;
-    } else {
-        cl = RXG_CLS_IPV4_OTHER;
-        nd = 24;
+            for (int k = 0; k < 4; ++k) s_hd[tid * 4u + k] = hd[k];
     }
-    const bool is_udp = cl == RXG_CLS_UDP, is_tcp = cl == RXG_CLS_TCP;
-    const bool l4 = is_udp || is_tcp;
-    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
-    const bool do_sum = l4 && tl >= 20u;
-    if (l4 && 34u + l4n > nd) nd = 34u + l4n;
-    int32_t e = do_sum ? 34 + (int32_t)l4n : 0;
-    if (e > cp) e = cp;
-
-    // ---- flow probe loads (consumed below, after the sums) --------------------
-    const bool probe = valid && l4;
-    const uint32_t ka = is_udp ? dip : sip;
-    const uint32_t kb = is_udp ? dport : dip;
-    const uint32_t kc = is_udp ? 17u : (sport | (dport << 16));
-    const uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
-    const bool probe0 = probe && maxp > 0 && !(ABL & 1);
-    const bool udp_port = is_udp && ft.udp_port != nullptr;
-    const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
-    const uint32_t pe = (ABL & 1) ? RXG_FLOW_NONE : ptab[l4 ? dport : 0u];
-    const bool hash0 = probe0 && !udp_port;
-    const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
-                                   (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
-                             : reinterpret_cast<const uint4 *>(fb);
-    const uint4 sl0 = ld_slot(sp0);
-
-    // ---- checksum -----------------------------------------------------------------
+    uint4 c[4];
+    head_of(c);
+    issue_probe(c);
+    const sh_head h = sh_parse(c, cp);
     uint4 h1 = c[1], h2 = c[2], h3 = c[3];
     h1.x = 0;
     h1.y = 0;
     h1.z &= 0xFFFF0000u;
-    if (is_udp) h2.z &= 0xFFFF0000u;
-    if (is_tcp) h3.x &= 0x0000FFFFu;
+    if (h.is_udp) h2.z &= 0xFFFF0000u;
+    if (h.is_tcp) h3.x &= 0x0000FFFFu;
+    const int32_t e = h.e;
     uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
     acc = lane_chunk_sum(acc, h2, 32, e);
     acc = lane_chunk_sum(acc, h3, 48, e);
-    if (do_sum) acc += (proto << 8) + rx_bswap16(l4n); // pseudo-header words
-    const uint32_t stored = is_udp ? (c[2].z & 0xFFFFu) : (is_tcp ? (c[3].x >> 16) : 0u);
+    if (h.do_sum) acc += (h.proto << 8) + rx_bswap16(h.l4n); // pseudo-header words
     // the sum ends where the capture does (the common case): tail from the
     // stream prefixes, the partial chunk from pcv; otherwise re-sum from HBM
-    const bool fast = streamed && e == cp;
-    if (do_sum && e > 64) {
-        if (fast) {
+    if (h.do_sum && e > 64) {
+        if (streamed && e == cp) {
             if (tailf) acc += ee - es;
             if (cf < cp && cf >= 64) acc = lane_chunk_sum(acc, pcv, cf, e);
         } else {
             for (int32_t s = 64; s < e; s += 16) acc = lane_chunk_sum(acc, ldg16<false>(fb + s), s, e);
         }
     }
-
-    // ---- verdict --------------------------------------------------------------------
+    uint32_t ck = 0;
+    if (h.do_sum) {
+        ck = (~fold16(acc)) & 0xFFFFu;
+        if (ck == 0u && h.proto == 17u) ck = 0xFFFFu;
+    }
+    const bool probe = valid && h.l4;
+    const uint32_t maxp = h.is_udp ? ft.udp_probe : ft.tcp_probe;
+    const bool probe0 = probe && maxp > 0 && !(ABL & 1);
+    const bool udp_port = h.is_udp && ft.udp_port != nullptr;
+    const bool hash0 = probe0 && !udp_port;
     uint32_t flags = 0, poff = 0, plen = 0;
-    if (is_udp) {
+    if (h.is_udp) {
         poff = 42;
-        plen = dgl > 8u ? dgl - 8u : 0u;
-        if (dgl <= 8u) flags |= RXG_F_UDP_SHORT;
-    } else if (is_tcp) {
-        const int32_t pl = (int32_t)tl - 20 - 4 * (int32_t)hl;
-        poff = 34u + 4u * hl;
+        plen = h.dgl > 8u ? h.dgl - 8u : 0u;
+        if (h.dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+    } else if (h.is_tcp) {
+        const int32_t pl = (int32_t)h.tl - 20 - 4 * (int32_t)h.hl;
+        poff = 34u + 4u * h.hl;
         if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
         plen = pl < 0 ? 0u : (uint32_t)pl;
     }
-    const bool trunc = (int32_t)nd > cp;
-    const bool trunc_ok = trunc || (is_udp && (int32_t)(42u + plen) > cp);
+    const bool trunc = (int32_t)h.nd > cp;
+    const bool trunc_ok = trunc || (h.is_udp && (int32_t)(42u + plen) > cp);
     uint32_t flow = RXG_FLOW_NONE;
     int32_t rc = RXG_RC_KNI;
     bool hashed = probe0;
-    if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, ka, ft.udp_dip, &flow);
+    if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, h.ka, ft.udp_dip, &flow);
     if (hashed) {
-        const uint4 *tb = is_udp ? ft.udp : ft.tcp;
-        const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
-        uint32_t pj = rx_hash3(ka, kb, kc) & mk;
-        uint4 sl = hash0 ? sl0 : ld_slot(tb + pj); // a UDP key on a shared port: load now
-        for (uint32_t pr = 0;;) {
+        const uint4 *tb = h.is_udp ? ft.udp : ft.tcp;
+        const uint32_t mk = h.is_udp ? ft.udp_mask : ft.tcp_mask;
+        uint32_t pj = rx_hash3(h.ka, h.kb, h.kc) & mk;
+        uint32_t pr = 0;
+        bool done = false;
+        if (hash0) { // the window loaded with the head
+#pragma unroll
+            for (int w = 0; w < PW; ++w) {
+                if (!done) {
+                    const uint4 sl = sw[w];
+                    if (sl.w == RX_SLOT_EMPTY) {
+                        done = true;
+                    } else if (sl.x == h.ka && sl.y == h.kb && sl.z == h.kc) {
+                        flow = sl.w;
+                        done = true;
+                    } else if (++pr >= maxp) {
+                        done = true;
+                    } else {
+                        pj = (pj + 1) & mk;
+                    }
+                }
+            }
+        }
+        while (!done) { // past the window, or a UDP key on a shared port
+            const uint4 sl = ld_slot(tb + pj);
             if (sl.w == RX_SLOT_EMPTY) break;
-            if (sl.x == ka && sl.y == kb && sl.z == kc) {
+            if (sl.x == h.ka && sl.y == h.kb && sl.z == h.kc) {
                 flow = sl.w;
                 break;
             }
             if (++pr >= maxp) break;
             pj = (pj + 1) & mk;
-            sl = ld_slot(tb + pj);
         }
     }
-    if constexpr ((ABL & 1) != 0) flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
-    if (is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
-    if (is_udp)
+    if constexpr ((ABL & 1) != 0) flow = probe ? (h.kb & 0x3FFu) : RXG_FLOW_NONE;
+    if (h.is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener (prefetched)
+    if (h.is_udp)
         rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
                                    : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
     if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
-    uint32_t ck = 0;
-    if (do_sum) {
-        ck = (~fold16(acc)) & 0xFFFFu;
-        if (ck == 0u && proto == 17u) ck = 0xFFFFu;
-    }
-    const bool ok = l4 && stored == ck;
-    if (is_tcp) {
+    const bool ok = h.l4 && h.stored == ck;
+    if (h.is_tcp) {
         if (!ok) flow = RXG_FLOW_NONE;
         rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
     }
@@ -1876,11 +1939,11 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
         uint4 vd;
         vd.x = flow;
         vd.y = (poff & 0xFFFFu) | (plen << 16);
-        vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
-        vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+        vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+        vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
         stg16(&out[p], vd);
         const uint32_t cidx =
-            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (h.is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
         lane_count(cidx, counts, hist, lds_bins);
         if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
     }
@@ -1893,14 +1956,14 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     }
 }
 
-template <int ABL = 0>
+template <int ABL = 0, int PW = 1>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                      const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rx_classify_sh_kernel<ABL>, dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2252,14 +2315,18 @@ static const variant_entry k_variants[] = {
     // diagnostic ablations of pipe 46 (wrong verdicts by construction): no
     // flow probe (146), no tail stream (246), no head loads (446), neither
     // heads nor stream (646)
-    // 54: pipe 38 with the heads gathered four lanes per head (HG)
+    // 54: pipe 38 with the heads gathered four lanes per head (HG); 55: 54
+    // with a four-slot first probe window
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>},
+    {0, 1, 1, 55, launch_stream<true, 0, 3, 4, true, false, true>},
     {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, true>},
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
     {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, true>},
     // 60: heads taken out of the block stream (SH kernel)
+    // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
+    {0, 1, 1, 63, launch_sh<0, 2>}, {0, 1, 1, 64, launch_sh<0, 4>},
 };
 
 } // namespace

@@ -22,6 +22,7 @@
 // Listeners (tcp_stream_search pass 2: dport + LISTEN, dst ip ignored) are a
 // direct u32[65536] table indexed by the raw dport.
 #define RX_SLOT_EMPTY 0xFFFFFFFFu
+#define RX_FT_MIRROR 3 // slots past the table's end that mirror its first ones
 #define RX_WINDOW 4
 
 struct rx_ft_dev {
