@@ -2315,10 +2315,10 @@ static const variant_entry k_variants[] = {
     // diagnostic ablations of pipe 46 (wrong verdicts by construction): no
     // flow probe (146), no tail stream (246), no head loads (446), neither
     // heads nor stream (646)
-    // 54: pipe 38 with the heads gathered four lanes per head (HG); 55: 54
-    // with a four-slot first probe window
+    // 54: pipe 38 with the heads gathered four lanes per head (HG).  (54 with
+    // a four-slot first probe window, PW = 4, ran 8% slower: 96 VGPRs and the
+    // window held across the stream, profiles/r02ab)
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>},
-    {0, 1, 1, 55, launch_stream<true, 0, 3, 4, true, false, true>},
     {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, true>},
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
@@ -2343,12 +2343,11 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // and pipe 14 is best at 2 blocks/CU (0.2328-0.2343 vs 0.2346-0.2352 for pipe 12 at
         // 4-6, r02m, r02o)
         *g = 1, *p = 4, *fpg = 1, *pipe = 14;
-    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel, flow probe after the
-        // tail stream at 5 blocks/CU (HO = 3): 1-3% ahead of pipe 30 in every interleaved
-        // sweep (r01g); one barrier per tail tile (B1) takes another 0.7% (r01g); heads
-        // gathered four lanes per head (HG, pipe 54): 1.2668 vs 1.3204 ms (no counts) and
-        // 1.3347 vs 1.3824 (counts), r02s
-        *g = 0, *p = 0, *fpg = 0, *pipe = 54;
+    } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
+        // out of the block stream and a four-slot first probe window (SH, pipe 64): 1.2704 vs
+        // 1.3417 ms for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716
+        // on another (counts on, interleaved sweeps, profiles/r02ab)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 64;
     } else if (len_hint <= 1536) { // cfg3: 1500 B
         *g = 8, *p = 2, *fpg = 2, *pipe = 0;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), the

@@ -64,7 +64,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
                    (0, 0, 0, 46),  # 38 with the span from the descriptors
-                   (0, 0, 0, 54), (0, 0, 0, 55),  # 38 with heads gathered four lanes per head
+                   (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
                    (0, 0, 0, 60),  # heads taken out of the block stream
                    (0, 0, 0, 63), (0, 0, 0, 64)]  # 60 with a 2 / 4-slot probe window
 

@@ -245,7 +245,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
-                                     (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 55), (0, 0, 0, 60),
+                                     (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 60),
                                      (0, 0, 0, 63), (0, 0, 0, 64), (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor
