@@ -736,6 +736,41 @@ __device__ __forceinline__ void lane_count(uint32_t idx, unsigned long long *__r
     }
 }
 
+// The count indices of a wave's 64 consecutive frames (frame p = p0 + lane,
+// p0 a multiple of 64; every lane active) stored as whole 16-B pieces: lane
+// 8k (2-B indices) or 4k (4-B indices) gathers its neighbours' indices over
+// DPP row shifts and stores them, non-temporally (the slab pass reads them
+// from HBM anyway; in the L2 they would displace the flow table the SH
+// kernel probes at the end of each block); the slab pass reads
+// indices past n never, so the last wave's pieces may cover frames >= n (the
+// index buffer has room for 4 B per frame, rounded to 256 B).
+__device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t p, uint32_t idx,
+                                                   uint32_t lane) {
+    if (!ft.count_idx) return;
+    if (ft.cidx16) {
+        const uint32_t v = idx & 0xFFFFu;
+        const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x101, 0xF, 0xF, false));
+        const uint32_t x2 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x102, 0xF, 0xF, false));
+        const uint32_t x3 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x103, 0xF, 0xF, false));
+        const uint32_t x4 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x104, 0xF, 0xF, false));
+        const uint32_t x5 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x105, 0xF, 0xF, false));
+        const uint32_t x6 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x106, 0xF, 0xF, false));
+        const uint32_t x7 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x107, 0xF, 0xF, false));
+        if ((lane & 7u) == 0u) {
+            const rx_u32x4 w = {v | (x1 << 16), x2 | (x3 << 16), x4 | (x5 << 16), x6 | (x7 << 16)};
+            __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p));
+        }
+    } else {
+        const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x101, 0xF, 0xF, false));
+        const uint32_t x2 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x102, 0xF, 0xF, false));
+        const uint32_t x3 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x103, 0xF, 0xF, false));
+        if ((lane & 3u) == 0u) {
+            const rx_u32x4 w = {idx, x1, x2, x3};
+            __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(static_cast<uint32_t *>(ft.count_idx) + p));
+        }
+    }
+}
+
 template <bool ST_NT>
 __device__ __forceinline__ void lane_store(uint4 *__restrict__ out, uint64_t p, uint4 v) {
     if constexpr (ST_NT)
@@ -1555,6 +1590,9 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             if (!ok) flow = RXG_FLOW_NONE;
             rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
         }
+        const uint32_t cidx = valid && rc == RXG_RC_OK && flow != RXG_FLOW_NONE
+                                  ? (is_tcp ? ft.nu : 0u) + flow
+                                  : 0xFFFFFFFFu;
         if (valid) {
             uint4 vd;
             vd.x = flow;
@@ -1562,11 +1600,9 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
             vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
             stg16(&out[p], vd);
-            const uint32_t cidx =
-                rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
             lane_count(cidx, counts, hist, lds_bins);
-            if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
         }
+        put_count_idx_wave(ft, p, cidx, lane);
     } // tile
     if (lds_bins) {
         __syncthreads();
@@ -1671,8 +1707,11 @@ __device__ __forceinline__ sh_head sh_parse(const uint4 (&c)[4], int32_t cp) {
 // (1, 2 or 4 consecutive slots of the hashed table loaded together; the table
 // mirrors its first slots past its end), so a displaced key costs no dependent
 // second round trip at the end of the block (pipes 60 / 63 / 64).
-template <int ABL = 0, int PW = 1>
-__global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
+// MAPC: span chunks the head map covers.  (A map for 256 frames of 1500 B,
+// 388 KiB of span at 3 blocks/CU, ran cfg3 at 1.161 vs 1.042 ms for the G=8
+// group kernel: profiles/r02ac.)
+template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC>
+__global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
@@ -1681,7 +1720,7 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     constexpr uint32_t TCH = 256u * LPT; // chunks per tile (16 KiB)
     __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
-    __shared__ __attribute__((aligned(16))) uint8_t s_map[SH_MAPC];
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[MAPC];
     __shared__ __attribute__((aligned(16))) uint4 s_hd[256 * 4];
     __shared__ uint16_t s_rel[256]; // each frame's first chunk in the span
     __shared__ unsigned long long s_lo, s_hi;
@@ -1696,7 +1735,7 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     }
     {
         uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
-        for (uint32_t i = tid; i < SH_MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t i = tid; i < MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
     const bool valid = p < n;
@@ -1714,7 +1753,7 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     __syncthreads();
     const uint64_t lo = s_lo, hi = s_hi;
     const uint32_t tsum = s_tail;
-    const bool streamed = hi > lo && hi - lo <= SH_MAPC && hi - lo <= 2ull * tsum + TCH;
+    const bool streamed = hi > lo && hi - lo <= MAPC && hi - lo <= 2ull * tsum + TCH;
     const uint32_t span = streamed ? (uint32_t)(hi - lo) : 0u;
     const uint8_t *sb = streamed ? pkts + (lo << 4) : fb;
     auto tile_load = [&](uint4 *v, uint32_t c0) {
@@ -1935,6 +1974,9 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
         if (!ok) flow = RXG_FLOW_NONE;
         rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
     }
+    const uint32_t cidx = valid && rc == RXG_RC_OK && flow != RXG_FLOW_NONE
+                              ? (h.is_tcp ? ft.nu : 0u) + flow
+                              : 0xFFFFFFFFu;
     if (valid) {
         uint4 vd;
         vd.x = flow;
@@ -1942,11 +1984,9 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
         vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
         stg16(&out[p], vd);
-        const uint32_t cidx =
-            rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (h.is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
         lane_count(cidx, counts, hist, lds_bins);
-        if (ft.count_idx) rx_put_count_idx(ft, p, cidx);
     }
+    put_count_idx_wave(ft, p, cidx, lane);
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -1956,14 +1996,14 @@ __global__ __launch_bounds__(256, 5) void rx_classify_sh_kernel(
     }
 }
 
-template <int ABL = 0, int PW = 1>
+template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                      const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2005,6 +2045,7 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
     __syncthreads();
     const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
     const uint32_t lim = min(nflows - f0, SLAB_MAX_FLOWS);
+    const bool amb = nflows > 0xFFFFu; // a 2-B all-ones index may be flow 65535
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
     uint32_t mine = 0;
@@ -2022,7 +2063,7 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
     };
     auto index_of = [&](uint32_t x, uint64_t k) -> uint32_t {
         if constexpr (sizeof(T) == 2)
-            if (x == 0xFFFFu) return from_verdict(verd[k]);
+            if (x == 0xFFFFu) return amb ? from_verdict(verd[k]) : ~0u;
         return x;
     };
     // 4E indices per thread per trip (four 16-B loads in flight); b0 is a
@@ -2035,10 +2076,11 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
             v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * E * 1024));
         if constexpr (sizeof(T) == 2) {
             // an all-ones index is flow 65535 iff the frame's rc is RXG_RC_OK
-            // (rc OK <=> a control block matched): every lane loads one rc
-            // dword per index, its own frame's for all-ones indices and one
-            // shared dword otherwise, so the loads need no branch and all are
-            // in flight before any is consumed
+            // (rc OK <=> a control block matched); only with 65536 flows is it
+            // ambiguous.  Then every lane loads one rc dword per index, its own
+            // frame's for all-ones indices and one shared dword otherwise, so
+            // the loads need no branch and all are in flight before any is
+            // consumed
             const uint32_t *vz = reinterpret_cast<const uint32_t *>(verd) + 2;
             uint32_t rx[4][8], z[4][8];
 #pragma unroll
@@ -2048,15 +2090,18 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
                 for (int j = 0; j < 8; ++j) {
                     rx[u][j] = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
                     const uint64_t k = i + (uint64_t)u * E * 1024 + j;
-                    z[u][j] = vz[4 * (rx[u][j] == 0xFFFFu ? k : b0)];
+                    // (a load under `amb ?` became a branch with a full wait per
+                    // index: 51 vs 27 us at cfg4, profiles/r02ac)
+                    z[u][j] = vz[4 * (amb && rx[u][j] == 0xFFFFu ? k : b0)];
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    count(rx[u][j] != 0xFFFFu ? rx[u][j]
-                                              : ((int8_t)(z[u][j] >> 24) == RXG_RC_OK ? 0xFFFFu : ~0u));
+                    count(rx[u][j] != 0xFFFFu
+                              ? rx[u][j]
+                              : ((amb && (int8_t)(z[u][j] >> 24) == RXG_RC_OK) ? 0xFFFFu : ~0u));
         } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u) count(v[u].x), count(v[u].y), count(v[u].z), count(v[u].w);
@@ -2072,7 +2117,9 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
     __syncthreads();
     const bool wrapped = sum != tally; // block-uniform
     uint32_t *dst = slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words;
-    for (uint32_t k = tid; k < words; k += 1024) dst[k] = wrapped ? 0u : bins[k];
+    // non-temporal: 32 MiB of slabs through the L2 would evict the flow tables
+    // the next burst's classify probes
+    for (uint32_t k = tid; k < words; k += 1024) __builtin_nontemporal_store(wrapped ? 0u : bins[k], &dst[k]);
     if (wrapped)
         for (uint64_t k = b0 + tid; k < b1; k += 1024) {
             const uint32_t f = index_of(cidx[k], k) - f0;
@@ -2105,7 +2152,7 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
         lo.w += x.w & 0xFFFFu, hi.w += x.w >> 16;
     };
     uint32_t b = wv;
-    for (; b + 16 * 3 < nslabs; b += 16 * 4) {
+    for (; b + 16 * 3 < nslabs; b += 16 * 4) { // (8 in flight spills at 1024 threads)
         uint4 x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)

@@ -3,7 +3,7 @@
 # smoke, PMC HBM bytes of every workload (stamped with this librxgpu.so's SHA
 # and copied into profiles/ so the bench publishes roofline.traffic from it),
 # the bench line (with the PCIe-inclusive leg), rocprofv3 kernel stats and
-# per-workload dispatch durations.  Each GPU step has its own time limit; a
+# per-workload dispatch durations, and an N = 2 rehearsal.  Each GPU step has its own time limit; a
 # failing step ends the script.     TAG=r02ab bash tools/gpu_final.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -22,4 +22,9 @@ step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/pr
     -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
 f=$(find $OUT/prof_$TAG -name '*kernel_trace.csv' | head -1)
 [ -n "$f" ] && python tools/trace_durations.py "$f" > $OUT/trace_durations_$TAG.txt
+# N = 2 rehearsal of the split path: two ranks on this one GPU (gloo carries
+# the counts when the ranks share a GPU; the driver's N-GPU run uses RCCL)
+step n2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 || exit $?
+grep '^{' $OUT/n2.log > $OUT/bench_n2_$TAG.json || true
 echo ALLDONE
