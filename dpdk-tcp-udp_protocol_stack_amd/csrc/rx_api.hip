@@ -618,11 +618,20 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                        unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
     const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr, 2);
     const bool split = cs && cs != s && pipe != 20 && rx_count_uses_slabs(c->ft, d_counts != nullptr);
+    // counts the classify kernel adds itself (few flows), or the binned path's:
+    // the count stream is ordered after this burst's kernels, as promised
+    auto join_cs = [&]() -> int {
+        if (cs && cs != s && d_counts) {
+            HIPCHK(hipEventRecord(c->ev_k1, s));
+            HIPCHK(hipStreamWaitEvent(cs, c->ev_k1, 0));
+        }
+        return RXG_OK;
+    };
     rx_set_bpc_cap(c->tune_bpc);
     if (!ws) {
         HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
                                   d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
-        return RXG_OK;
+        return join_cs();
     }
     const size_t layout = ws ^ ((size_t)n << 40) ^ ((size_t)(pipe == 20) << 39);
     int rc = ws_prepare(c, ws, layout, s);
@@ -634,7 +643,7 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                                   d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
         HIPCHK(ws_mark(c, WS_BUF0, s));
         HIPCHK(ws_mark(c, WS_SLAB, s));
-        return RXG_OK;
+        return join_cs();
     }
     const uint32_t b = c->ws_flip;
     c->ws_flip ^= 1u;

@@ -204,13 +204,15 @@ def test_one_context_two_streams_share_workspace(torch_dev):
         assert np.array_equal(c.cpu().numpy().view(np.uint64), 4 * wcnt)
 
 
-@pytest.mark.parametrize("nu,nt,n", [(6000, 6000, 40000), (40000, 30000, 12000)])
+@pytest.mark.parametrize("nu,nt,n", [(6000, 6000, 40000), (40000, 30000, 12000), (300, 300, 40000)])
 def test_counts_on_a_second_stream(torch_dev, nu, nt, n):
     """rxg_classify_dev_cs: verdicts on the classify stream, the slab count on a
     count stream, overlapping the next burst's classify (two index buffers in
     the context).  Two different bursts alternate, a plain rxg_classify_dev
     burst and a burst of another size (the workspace regions move) are mixed
-    in: every verdict is bit-exact and the counts add up to the histograms"""
+    in: every verdict is bit-exact and the counts add up to the histograms.
+    With few flows the classify kernel counts itself (no slab passes) and the
+    count stream is still ordered after it"""
     torch, dev = torch_dev
     cfg = rxdist.gen_cfg("cfg4", n_udp=nu, n_tcp=nt, other_per10k=300)
     udp, tcb = R.gen_flows(cfg)
