@@ -136,7 +136,7 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
         assert np.array_equal(cnt, wcnt), (name, hint)
 
 
-@pytest.mark.parametrize("variant", R.KERNEL_VARIANTS)
+@pytest.mark.parametrize("variant", R.KERNEL_VARIANTS, ids=lambda v: "v" + "-".join(map(str, v)))
 def test_every_kernel_variant(ctx, torch_dev, variant):
     """each compiled (lanes, passes, frames-per-group) variant, on mixed sizes"""
     fl = np.load(os.path.join(GOLD, "edge_flows.npz"))
