@@ -86,8 +86,13 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     alg_bytes = frame_bytes + 22 * n  # frame + off(4) + len(2) read + verdict(16) written
     # N > 1: step k's counts go to step_counts[k & 1]; the all-reduce runs on
     # the collective stream cs while step k+1's kernel runs, then adds into counts
-    cs = torch.cuda.Stream(dev) if (world > 1 or COUNT_STREAM) else None
-    csh = cs.cuda_stream if (cs is not None and COUNT_STREAM) else None
+    # the count stream only where the counts are separate passes (slab path,
+    # R.SLAB_MIN_FLOWS flows and up); below that the classify kernel counts
+    # itself and the stream would only add an event per step (~3 us of GPU
+    # idle between bursts, r02j)
+    use_cs = COUNT_STREAM and COUNTS and nflows >= R.SLAB_MIN_FLOWS
+    cs = torch.cuda.Stream(dev) if (world > 1 or use_cs) else None
+    csh = cs.cuda_stream if use_cs else None
     step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)] if world > 1 else None
     k_ev = [torch.cuda.Event(), torch.cuda.Event()]
     done_ev = [torch.cuda.Event(), torch.cuda.Event()]

@@ -159,6 +159,7 @@ _group_close = _sig("rxg_group_close", None, _vp)
 _counts_allreduce = _sig("rxg_counts_allreduce", _i32, _vp, _vp, _u32, _vp)
 _ctx_counts_allreduce = _sig("rxg_ctx_counts_allreduce", _i32, _vp, _vp)
 PIPE_DEPTH = 3
+SLAB_MIN_FLOWS = 8193  # from here up the per-flow counts are slab passes after the classify kernel
 MAX_SHARDS = 64
 GROUP_ID_BYTES = 128
 
