@@ -244,7 +244,14 @@ struct rxg_ctx {
         hipStream_t st = nullptr;
         bool used = false;
     } wu[3];
-    size_t ws_layout = 0; // region offsets depend on the burst shape; a change waits on all
+    // region offsets depend on the burst shape (frame count, binned path, size);
+    // a change of shape waits on every region
+    struct ws_shape {
+        uint32_t n = 0;
+        bool lists = false;
+        size_t bytes = 0;
+        bool operator!=(const ws_shape &o) const { return n != o.n || lists != o.lists || bytes != o.bytes; }
+    } ws_layout;
     uint32_t ws_flip = 0; // index buffer of the next split-stream burst
     hipEvent_t ev_k1 = nullptr; // split-stream burst: classify done (count stream waits on it)
     void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
@@ -597,7 +604,7 @@ static hipError_t ws_mark(rxg_ctx *c, int r, hipStream_t s) {
 // size the workspace for a burst before its launches (growth drains every use
 // of the old one) and, when the burst shape moves the regions, order stream s
 // after every earlier use
-static int ws_prepare(rxg_ctx *c, size_t ws, size_t layout, hipStream_t s) {
+static int ws_prepare(rxg_ctx *c, size_t ws, const rxg_ctx::ws_shape &layout, hipStream_t s) {
     if (ws > c->d_ws_cap) {
         for (rxg_ctx::ws_use &u : c->wu)
             if (u.used) HIPCHK(hipEventSynchronize(u.ev));
@@ -633,7 +640,10 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                                   d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
         return join_cs();
     }
-    const size_t layout = ws ^ ((size_t)n << 40) ^ ((size_t)(pipe == 20) << 39);
+    rxg_ctx::ws_shape layout;
+    layout.n = n;
+    layout.lists = pipe == 20;
+    layout.bytes = ws;
     int rc = ws_prepare(c, ws, layout, s);
     if (rc) return rc;
     if (!split) {
