@@ -2152,7 +2152,7 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
         lo.w += x.w & 0xFFFFu, hi.w += x.w >> 16;
     };
     uint32_t b = wv;
-    for (; b + 16 * 3 < nslabs; b += 16 * 4) { // (8 in flight spills at 1024 threads)
+    for (; b + 16 * 3 < nslabs; b += 16 * 4) {
         uint4 x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -2167,7 +2167,7 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
     __syncthreads();
     if (wv == 0 && w < words) {
         lo = hi = make_uint4(0, 0, 0, 0);
-#pragma unroll
+#pragma unroll 4 // (fully unrolled it spilled 8 VGPRs at the 1024-thread budget)
         for (int k = 0; k < 16; ++k) {
             const uint4 a = part[0][k][lane], c = part[1][k][lane];
             lo.x += a.x, lo.y += a.y, lo.z += a.z, lo.w += a.w;
