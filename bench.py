@@ -690,7 +690,9 @@ def sweep(ctx, names, steps, warmup, dev, only="", with_counts=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 50 steps: a 12-ms timed window at cfg2 (0.23 ms per burst), less exposed
+    # to a single host-side hiccup than 20 (4.6 ms)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2,cfg3,cfg4,cfg5",
                     help="BASELINE configs to run; the first is the headline line (cfg2 = configs[1])")
