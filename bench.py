@@ -35,6 +35,76 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "dpdk-tcp-udp_protocol_stack_amd")
 sys.path.insert(0, PKG)
 
+
+def _gpus_arg(argv):
+    """--gpus N from the command line, read before anything touches the GPU"""
+    for k, a in enumerate(argv):
+        if a == "--gpus" and k + 1 < len(argv):
+            return int(argv[k + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` with no launcher: start N rank processes of this
+    script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set), as
+    torch.distributed.run would, and exit with the worst child status.  Runs
+    before torch or librxgpu is imported, so this process never touches the
+    GPU (children are started, never exec'd).  Rank 0 prints the JSON line on
+    the inherited stdout.  When a rank fails, the others get 60 s to finish
+    and are then terminated (a peer stuck in a barrier would wait forever)."""
+    import subprocess
+    import time as _t
+    env0 = dict(os.environ)
+    env0.setdefault("MASTER_ADDR", "127.0.0.1")
+    env0.setdefault("MASTER_PORT", str(_free_port()))
+    env0["WORLD_SIZE"] = str(n)
+    env0["LOCAL_WORLD_SIZE"] = str(n)
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    print(f"bench: launched {n} ranks (pids {[p.pid for p in procs]}, "
+          f"MASTER {env0['MASTER_ADDR']}:{env0['MASTER_PORT']})", file=sys.stderr, flush=True)
+    deadline = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if deadline is None and any(rc not in (None, 0) for rc in rcs):
+            deadline = _t.monotonic() + 60.0
+        if deadline is not None and _t.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = _t.monotonic() + 1e9
+        _t.sleep(0.2)
+    rcs = [p.returncode for p in procs]
+    print(f"bench: rank exit codes {rcs}", file=sys.stderr, flush=True)
+    bad = [rc for rc in rcs if rc != 0]
+    return 0 if not bad else (bad[0] if bad[0] > 0 else 128 - bad[0])
+
+
+if __name__ == "__main__":
+    _n = _gpus_arg(sys.argv[1:])
+    _ws = os.environ.get("WORLD_SIZE")
+    if _n > 1 and _ws is None:
+        sys.exit(launch_ranks(_n, sys.argv[1:]))
+    if _ws is not None and int(_ws) != _n:
+        print(f"bench: --gpus {_n} but the launcher started WORLD_SIZE={_ws} ranks; "
+              "they must agree", file=sys.stderr, flush=True)
+        sys.exit(2)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -47,6 +117,7 @@ COUNTS = True
 COUNT_STREAM = True
 TX = True
 RAMP_MS = 200.0
+JSON_OUT = sys.stdout
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 
 
@@ -152,7 +223,30 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         torch.distributed.barrier()
     el = time.perf_counter() - t0
     kms = [ev[0].elapsed_time(ev[1]) / max(steps, 1)]
-    if world > 1:  # max over ranks (gloo: control plane on the host)
+    per_rank = None
+    ar_ms = None
+    if world > 1:
+        # the collective alone: `steps` count all-reduces back to back on the
+        # collective stream (HIP events on that stream), after the timed region
+        aev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        aev[0].record(cs)
+        for _ in range(steps):
+            coll(step_counts[0], cs)
+        aev[1].record(cs)
+        torch.cuda.synchronize(dev)
+        ar_ms = aev[0].elapsed_time(aev[1]) / max(steps, 1)
+        # per-rank wall step, kernel-stream step and all-reduce times, then the
+        # max over ranks (gloo: control plane on the host)
+        mine = torch.tensor([el / max(steps, 1) * 1e3, kms[0], ar_ms, float(n)],
+                            dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(allr, mine)
+        per_rank = [dict(rank=r, ms_per_step=round(float(x[0]), 4),
+                         stream_ms_per_step=round(float(x[1]), 4),
+                         allreduce_ms=round(float(x[2]), 4), frames=int(x[3]))
+                    for r, x in enumerate(allr)]
         t = torch.tensor([el], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
@@ -183,6 +277,10 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         rc0_frac=n_ok / max(n, 1), counts_ok=(expect is None or counted == expect),
         setup_s=round(t_setup, 2), count_stream=bool(COUNTS and csh is not None),
     )
+    if world > 1:
+        res["allreduce_ms"] = round(ar_ms, 4)
+        res["allreduce_bytes"] = 8 * nflows
+        res["per_rank"] = per_rank
     achieved = alg_bytes / (kavg * 1e-3) / 1e9  # this rank's kernel (HIP events)
     res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                            unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
@@ -202,6 +300,11 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
                                 "oracle/ref_cpu.c", seconds=round(time.perf_counter() - t_par, 2))
     if first_bad:
         log(f"PARITY FAILURE {name}: {first_bad}")
+    t_dg = time.perf_counter()
+    res["digest"] = burst_digest(name, out, n, gidx, counts, warmup + steps, rank, world)
+    res["digest"]["seconds"] = round(time.perf_counter() - t_dg, 2)
+    if res["digest"]["digest_ok"] is False:
+        log(f"DIGEST MISMATCH {name}: {res['digest']}")
     if TX and world == 1:  # K2 (TX checksum fill) over the same burst, in place
         tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for _ in range(warmup):
@@ -220,6 +323,56 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
+
+
+def burst_digest(name, out, n, gidx, counts, total_steps, rank, world):
+    """the whole burst against tests/golden/digests.json (the oracle's verdicts
+    of every frame of the workload's burst, computed offline by
+    tests/golden/make_digests.py): N = 1, the SHA-256 of all n x 16 verdict
+    bytes, the order-free frame digest and the per-flow histogram (the
+    counts after the run / the bursts counted); N > 1, the frame digest of the
+    golden burst's frames (global index < n) summed over the ranks that hold
+    them."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import digest as D  # parity leg only
+    try:
+        gold = D.load_golden().get(name)
+    except OSError:
+        gold = None
+    r = dict(golden=gold is not None)
+    dev = out.device
+    v = out[:n * 16]
+    if world == 1:
+        idx = torch.arange(n, dtype=torch.int64, device=dev)
+        r["frames"] = n
+        r["frame_digest"] = f"{D.frame_digest_torch(idx, v):016x}"
+        r["verdict_sha256"] = D.sha256_bytes(v.cpu().numpy())
+        c = counts.cpu().numpy().view(np.uint64)
+        whole = bool(np.all(c % np.uint64(total_steps) == 0))
+        r["counts_sha256"] = D.counts_sha256(c // np.uint64(total_steps)) if whole else None
+        if gold is not None:
+            r["digest_ok"] = (n == gold["frames"] and r["verdict_sha256"] == gold["verdict_sha256"]
+                              and r["frame_digest"] == gold["frame_digest"]
+                              and (not COUNTS or r["counts_sha256"] == gold["counts_sha256"]))
+    else:
+        g = torch.from_numpy(gidx).to(dev)
+        lim = gold["frames"] if gold is not None else rxdist.WORKLOADS[name]["n"]
+        keep = torch.nonzero(g < lim).flatten()
+        part = D.frame_digest_torch(g.index_select(0, keep),
+                                    v.view(n, 16).index_select(0, keep)) if len(keep) else 0
+        t = torch.tensor([part - (1 << 64) if part >= 1 << 63 else part, len(keep)],
+                         dtype=torch.int64)
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(allr, t)
+        tot = sum(int(x[0]) for x in allr) & D._M64
+        r["frames"] = sum(int(x[1]) for x in allr)
+        r["frame_digest"] = f"{tot:016x}"
+        r["scope"] = "frames 0..n-1 of the global burst (the golden burst), over all ranks"
+        if gold is not None:
+            r["digest_ok"] = (r["frames"] == gold["frames"]
+                              and r["frame_digest"] == gold["frame_digest"])
+    r.setdefault("digest_ok", None)  # None: no golden entry for this workload
+    return r
 
 
 def lib_sha256():
@@ -725,11 +878,31 @@ def main():
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
+    # stdout carries the one JSON line only: native libraries (gloo, RCCL, HIP)
+    # print to fd 1 as well, so fd 1 is pointed at stderr and the line goes to
+    # a private duplicate of the original stdout
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
+    log(f"bench: rank {rank} of {world} (local {local}, pid {os.getpid()}, {ndev} GPU(s) visible)")
+    if ndev == 0:
+        # no GPU: the rank set and the rendezvous are still checked (gloo),
+        # then every rank fails loudly; nothing is measured without the device
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.distributed.init_process_group("gloo")
+            t = torch.ones(1)
+            torch.distributed.all_reduce(t)
+            log(f"bench: rank {rank}: rendezvous ok, all_reduce saw {int(t.item())} ranks")
+            torch.distributed.destroy_process_group()
+        log(f"bench: rank {rank}: no GPU visible; librxgpu has no CPU path (exit 4)")
+        sys.exit(4)
     if world > 1 and ndev < world:  # rehearsal with ranks sharing GPUs (never RCCL then)
         local = local % max(ndev, 1)
     group = nccl_group = None
@@ -801,7 +974,8 @@ def main():
             results[nm]["e2e_pcie"] = r
 
     parity_bad = sum(r["parity"]["mismatches"] for r in results.values()) + \
-        (cfg1["parity"]["mismatches"] if cfg1 else 0)
+        (cfg1["parity"]["mismatches"] if cfg1 else 0) + \
+        sum(r["digest"]["digest_ok"] is False for r in results.values())
     if rank == 0:
         line = {
             "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
@@ -826,11 +1000,16 @@ def main():
             "roofline": head["roofline"],
             "cpu_baseline": head.get("cpu_baseline"),
             "parity": head["parity"],
+            "digest": head["digest"],
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
             "hbm_copy_peak_gbs": copy_peak,
             "librxgpu_sha256": lib_sha256()[:16],
         }
+        if world > 1:
+            line["allreduce_ms"] = head["allreduce_ms"]
+            line["allreduce_bytes"] = head["allreduce_bytes"]
+            line["per_rank"] = head["per_rank"]
         if "tx_cksum" in head:
             line["tx_cksum"] = head["tx_cksum"]
         if "e2e_pcie" in head:
@@ -841,7 +1020,7 @@ def main():
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=JSON_OUT, flush=True)
     ctx.close()
     if group is not None:
         group.close()

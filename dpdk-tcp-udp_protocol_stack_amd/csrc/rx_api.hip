@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "rx_common.h"
+#include "rx_flows.h"
 
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
 void rx_set_bpc_cap(uint32_t cap);
@@ -87,149 +88,75 @@ hipError_t rx_occupancy(const void *fn, uint32_t threads, size_t lds, int *cu, i
         if (e_ != hipSuccess) return rx_set_hip_error(e_);                                         \
     } while (0)
 
-// ---------------------------------------------------------------------------
-// Host flow-table image (see rx_common.h for the device layout)
-struct ft_host {
-    std::vector<uint4> slots;
-    uint32_t mask = 0, probe = 1;
-
-    // entries: x,y,z = key, w = value, in creation order (newest wins); load
-    // factor <= 2^-load_log2 (>= 1: always an empty slot)
-    void build(const std::vector<uint4> &entries, uint32_t load_log2) {
-        const uint64_t n = entries.size();
-        uint64_t ns = 16;
-        while (ns < (n << load_log2)) ns <<= 1;
-        // RX_FT_MIRROR slots past the end mirror slots 0.., so a probe window of
-        // up to RX_FT_MIRROR + 1 slots at any index reads in bounds (the stream
-        // kernels' first probe)
-        slots.assign(ns + RX_FT_MIRROR, make_uint4(0, 0, 0, RX_SLOT_EMPTY));
-        mask = (uint32_t)(ns - 1);
-        probe = 1;
-        for (const uint4 &e : entries) {
-            uint32_t i = rx_hash3(e.x, e.y, e.z) & mask;
-            for (uint32_t d = 0;; ++d, i = (i + 1) & mask) {
-                uint4 &sl = slots[i];
-                if (sl.w == RX_SLOT_EMPTY) {
-                    sl = e;
-                } else if (sl.x == e.x && sl.y == e.y && sl.z == e.z) {
-                    sl.w = e.w; // a newer control block with the same key wins
-                } else {
-                    continue;
-                }
-                probe = std::max(probe, d + 1);
-                break;
-            }
-        }
-        for (uint32_t k = 0; k < RX_FT_MIRROR; ++k) slots[ns + k] = slots[k];
-    }
-
-    uint32_t lookup(uint32_t a, uint32_t b, uint32_t c) const {
-        uint32_t i = rx_hash3(a, b, c) & mask;
-        for (uint32_t d = 0; d < probe; ++d, i = (i + 1) & mask) {
-            const uint4 &sl = slots[i];
-            if (sl.w == RX_SLOT_EMPTY) break;
-            if (sl.x == a && sl.y == b && sl.z == c) return sl.w;
-        }
-        return RXG_FLOW_NONE;
-    }
+// one incremental table write (rxg_flows_commit): rx_delta_kernel stores v
+// at element idx of table `which`
+enum { RX_D_UDP = 0, RX_D_TCP = 1, RX_D_LISTEN = 2, RX_D_PORT = 3, RX_D_UDPC = 4, RX_D_UDPW = 5 };
+struct rx_delta {
+    uint32_t which, idx, _r0, _r1;
+    uint4 v;
 };
+#define RX_DELTA_CAP 65536u // records per commit; more: whole arrays are uploaded
 
-// Compact UDP table for socket sets of <= RX_UDPC_MAX_FLOWS: the same keys and
-// flow ids as the main table (already deduplicated, newest wins), 8-B slots at
-// load <= 1/2 so the lane kernel can keep it in LDS.
-static void build_udpc(const ft_host &u, uint32_t nu, std::vector<uint2> *out, uint32_t *probe) {
-    out->clear();
-    *probe = 0;
-    if (nu == 0 || nu > RX_UDPC_MAX_FLOWS) return;
-    uint32_t ns = 16;
-    while (ns < 2 * nu) ns <<= 1;
-    out->assign(ns, make_uint2(0, 0xFFFFFFFFu));
-    const uint32_t mask = ns - 1;
-    for (uint32_t j = 0; j <= u.mask; ++j) { // (past the mask: mirrors)
-        const uint4 &sl = u.slots[j];
-        if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> flow
-        uint32_t i = rx_hash3(sl.x, sl.y, sl.z) & mask;
-        uint32_t d = 0;
-        while ((*out)[i].y != 0xFFFFFFFFu) i = (i + 1) & mask, ++d;
-        (*out)[i] = make_uint2(sl.x, (sl.y & 0xFFFFu) | (sl.w << 16));
-        *probe = std::max(*probe, d + 1);
+__global__ __launch_bounds__(256) void rx_delta_kernel(const rx_delta *__restrict__ d, uint32_t n,
+                                                       uint4 *udp, uint4 *tcp, uint32_t *listen,
+                                                       uint32_t *port, uint4 *udpc, uint4 *udpw) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const rx_delta r = d[i];
+    switch (r.which) {
+    case RX_D_UDP: udp[r.idx] = r.v; break;
+    case RX_D_TCP: tcp[r.idx] = r.v; break;
+    case RX_D_LISTEN: listen[r.idx] = r.v.x; break;
+    case RX_D_PORT: port[r.idx] = r.v.x; break;
+    case RX_D_UDPC: udpc[r.idx] = r.v; break;
+    default: udpw[r.idx] = r.v; break;
     }
 }
 
-// UDP direct port table (rx_common.h): the address most sockets are bound to
-// gets a u32[65536] entry per port (flow id, or RX_PORT_NONE); a port that also
-// has a socket on another address is flagged RX_PORT_HASHED, and lookups for
-// those other addresses probe the hashed table, which holds every key.
-static uint32_t build_udp_port(const ft_host &u, std::vector<uint32_t> *port) {
-    std::unordered_map<uint32_t, uint32_t> dips; // dip -> sockets bound to it
-    for (uint32_t i = 0; i <= u.mask; ++i)
-        if (u.slots[i].w != RX_SLOT_EMPTY) ++dips[u.slots[i].x];
-    uint32_t dip = 0, best = 0;
-    for (const auto &d : dips)
-        if (d.second > best || (d.second == best && d.first < dip)) best = d.second, dip = d.first;
-    port->assign(65536, RX_PORT_NONE);
-    for (uint32_t i = 0; i <= u.mask; ++i) { // (past the mask: mirrors)
-        const uint4 &sl = u.slots[i];
-        if (sl.w == RX_SLOT_EMPTY) continue; // key (dip, dport, 17) -> newest flow
-        uint32_t &e = (*port)[sl.y & 0xFFFFu];
-        if (sl.x == dip)
-            e = (e & RX_PORT_HASHED) | sl.w;
-        else
-            e |= RX_PORT_HASHED;
-    }
-    return dip;
+// fold of two u64 count vectors: base += delta, delta = 0 (the all-reduced
+// increment of rxg_ctx_counts_allreduce joins the running total)
+__global__ __launch_bounds__(256) void rx_counts_fold_kernel(unsigned long long *base,
+                                                             unsigned long long *delta, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    base[i] += delta[i];
+    delta[i] = 0;
 }
 
-// UDP port window (rx_common.h): the host-order port range of the sockets
-// bound to udp_dip, when it spans <= RX_UDPW_MAX_PORTS ports and the compact
-// table exists; u16 flow ids, 0xFFFF = no socket on (udp_dip, port).  Empty
-// otherwise.  *lo = its first port.
-static void build_udpw(const std::vector<uint32_t> &port, bool compact, std::vector<uint16_t> *w,
-                       uint32_t *lo) {
-    w->clear();
-    *lo = 0;
-    if (!compact || port.empty()) return;
-    uint32_t mn = 65536, mx = 0;
-    for (uint32_t r = 0; r < 65536; ++r)
-        if ((port[r] & RX_PORT_NONE) != RX_PORT_NONE) {
-            const uint32_t h = ((r & 0xFFu) << 8) | (r >> 8);
-            mn = std::min(mn, h);
-            mx = std::max(mx, h);
-        }
-    if (mn > mx || mx - mn + 1 > RX_UDPW_MAX_PORTS) return;
-    w->assign(mx - mn + 1, 0xFFFFu);
-    for (uint32_t h = mn; h <= mx; ++h) {
-        const uint32_t f = port[((h & 0xFFu) << 8) | (h >> 8)] & RX_PORT_NONE;
-        if (f != RX_PORT_NONE) (*w)[h - mn] = (uint16_t)f; // < RX_UDPC_MAX_FLOWS
-    }
-    *lo = mn;
-}
+// a stream bursts of this context ran on, and the event recorded after its
+// last burst: table writes wait on it, so they never overtake a burst still
+// reading the tables (a per-context wait, never a device-wide one)
+struct rx_track {
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    uint64_t commit_seen = 0; // last table commit this stream is ordered after
+    uint64_t last_use = 0;
+    bool used = false;
+};
+#define RX_TRACK 4
 
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // flow tables
-    ft_host h_udp, h_tcp;
-    std::vector<uint32_t> h_listen;
-    std::vector<uint2> h_udpc; // compact UDP table (small socket sets), empty if none
-    uint32_t udpc_probe = 0;
+    // flow tables: host images + registry (rx_flows.h), device copies
+    rx_flowset fs;
+    bool dirty = false; // host changes not yet on the device (rxg_flows_commit)
     uint4 *d_udp = nullptr, *d_tcp = nullptr;
-    uint2 *d_udpc = nullptr;
-    size_t d_udp_cap = 0, d_tcp_cap = 0, d_udpc_cap = 0;
-    uint32_t *d_listen = nullptr;
-    std::vector<uint32_t> h_udp_port; // UDP direct port table (empty: not built)
-    uint32_t udp_dip = 0;
-    uint32_t *d_udp_port = nullptr;
-    std::vector<uint16_t> h_udpw; // UDP port window (empty: not built)
-    uint32_t udpw_lo = 0;
-    uint16_t *d_udpw = nullptr;
-    size_t d_udpw_cap = 0;
+    size_t d_udp_cap = 0, d_tcp_cap = 0; // bytes
+    uint32_t *d_listen = nullptr;   // 65536
+    uint32_t *d_udp_port = nullptr; // 65536
+    uint2 *d_udpc = nullptr;        // up to 2 * RX_UDPC_MAX_FLOWS slots
+    uint16_t *d_udpw = nullptr;     // up to RX_UDPW_MAX_PORTS
+    rx_delta *h_delta = nullptr, *d_delta = nullptr; // pinned staging + device copy
+    hipEvent_t ev_commit = nullptr; // after the last commit's writes
+    uint64_t commit_gen = 0;
+    rx_track trk[RX_TRACK];
+    uint64_t use_clock = 0;
     uint32_t tune_tables = 0; // rxg_tune_tables flags
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
     uint32_t tune_tx = RXG_TX_AUTO, tune_tx_bpc = 0; // rxg_tune_tx
-    uint32_t ft_load_log2 = RX_FT_LOAD_LOG2;           // rxg_tune_flow_load
     // launch workspace, grown on demand: [binned lists][count indices x 2][count
     // slabs].  Three regions are tracked, each by the event of its last use and
     // that use's stream: index buffer 0 (with the lists), index buffer 1, the
@@ -256,8 +183,12 @@ struct rxg_ctx {
     hipEvent_t ev_k1 = nullptr; // split-stream burst: classify done (count stream waits on it)
     void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
     size_t d_aux_cap = 0;
-    // context-owned per-flow counts (host-buffer path)
-    unsigned long long *d_counts = nullptr;
+    hipEvent_t ev_aux = nullptr; // after the last split / gather that used d_aux
+    hipStream_t aux_st = nullptr;
+    bool aux_used = false;
+    // context-owned per-flow counts (host-buffer path): d_counts since the last
+    // rxg_ctx_counts_allreduce, d_counts_base the all-reduced total before it
+    unsigned long long *d_counts = nullptr, *d_counts_base = nullptr;
     uint32_t counts_cap = 0;
     // host-buffer path: a ring of RXG_PIPE_DEPTH staging slots; burst t uses
     // slot t % depth.  Copies in run on s_h2d, kernels on `stream`, verdict
@@ -292,9 +223,269 @@ static int ensure_dev(void **p, size_t *cap, size_t bytes) {
     return RXG_OK;
 }
 
+// a flow-table array of at least `bytes`, stream-ordered on s (hipMallocAsync /
+// hipFreeAsync: neither synchronises the device, unlike hipFree)
+static int ensure_dev_async(void **p, size_t *cap, size_t bytes, hipStream_t s) {
+    if (*cap >= bytes && *p) return RXG_OK;
+    if (*p) HIPCHK(hipFreeAsync(*p, s));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMallocAsync(p, bytes, s));
+    *cap = bytes;
+    return RXG_OK;
+}
+
+// Save the calling thread's current device, switch to the context's, restore
+// it on scope exit: the API never leaves a C host thread on another device.
+struct dev_guard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit dev_guard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~dev_guard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+#define DEVGUARD(c)                                                                                \
+    dev_guard dg_((c)->device);                                                                    \
+    HIPCHK(dg_.err)
+
+// a fresh hash seed (rx_hash3s): random at rxg_open, then a mix on reseeds
+static uint32_t next_seed(uint32_t s) {
+    uint64_t z = rx_mix64(((uint64_t)s << 32) ^ 0xA0761D6478BD642Full);
+    return (uint32_t)(z >> 32) | 1u;
+}
+static uint32_t random_seed() {
+    uint32_t s = 0;
+    FILE *f = fopen("/dev/urandom", "rb");
+    if (f) {
+        if (fread(&s, sizeof(s), 1, f) != 1) s = 0;
+        fclose(f);
+    }
+    s ^= (uint32_t)(uintptr_t)&s ^ (uint32_t)clock();
+    return next_seed(s);
+}
+
+// ---- burst tracking ----------------------------------------------------
+// the tracking entry of stream s (an LRU slot; an evicted stream's last burst
+// is waited for on the host first, so its table reads stay ordered)
+static int track_slot(rxg_ctx *c, hipStream_t s, rx_track **out) {
+    rx_track *t = nullptr, *old = &c->trk[0];
+    for (rx_track &x : c->trk) {
+        if (x.used && x.s == s) t = &x;
+        if (!x.used || (old->used && x.last_use < old->last_use)) old = &x;
+    }
+    if (!t) {
+        t = old;
+        if (t->used) HIPCHK(hipEventSynchronize(t->ev));
+        t->s = s;
+        t->used = true;
+        t->commit_seen = c->commit_gen; // (a new stream: tables already on the device
+                                        // unless a commit is pending, which runs on s)
+        if (c->commit_gen) HIPCHK(hipStreamWaitEvent(s, c->ev_commit, 0));
+    }
+    t->last_use = ++c->use_clock;
+    *out = t;
+    return RXG_OK;
+}
+
+// before a burst on s: the pending table changes, then order s after the last commit
+static int commit_on(rxg_ctx *c, hipStream_t s);
+static int burst_begin(rxg_ctx *c, hipStream_t s) {
+    if (c->dirty) {
+        int rc = commit_on(c, s);
+        if (rc) return rc;
+    }
+    rx_track *t;
+    int rc = track_slot(c, s, &t);
+    if (rc) return rc;
+    if (t->commit_seen < c->commit_gen) {
+        HIPCHK(hipStreamWaitEvent(s, c->ev_commit, 0));
+        t->commit_seen = c->commit_gen;
+    }
+    return RXG_OK;
+}
+// after a burst's launches on s
+static int burst_end(rxg_ctx *c, hipStream_t s) {
+    if (c->tune_tables & RXG_TT_NO_TRACK) return RXG_OK;
+    for (rx_track &x : c->trk)
+        if (x.used && x.s == s) {
+            HIPCHK(hipEventRecord(x.ev, s));
+            return RXG_OK;
+        }
+    return RXG_OK;
+}
+// host wait for every burst of this context (a table rebuild in place)
+static int bursts_drain(rxg_ctx *c) {
+    for (rx_track &x : c->trk)
+        if (x.used) HIPCHK(hipEventSynchronize(x.ev));
+    for (rxg_ctx::ws_use &u : c->wu)
+        if (u.used) HIPCHK(hipEventSynchronize(u.ev));
+    if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->s_h2d) HIPCHK(hipStreamSynchronize(c->s_h2d));
+    if (c->s_d2h) HIPCHK(hipStreamSynchronize(c->s_d2h));
+    return RXG_OK;
+}
+
+// ---- device upload of the flow tables ------------------------------------
+static void ft_fill(rxg_ctx *c) {
+    const rx_flowset &fs = c->fs;
+    c->ft.udp = c->d_udp;
+    c->ft.tcp = c->d_tcp;
+    c->ft.listen = c->d_listen;
+    c->ft.udp_mask = fs.udp.tab.mask;
+    c->ft.tcp_mask = fs.tcp.tab.mask;
+    c->ft.udp_probe = fs.udp.live ? fs.udp.tab.probe : 0;
+    c->ft.tcp_probe = fs.tcp.live ? fs.tcp.tab.probe : 0;
+    c->ft.hseed = fs.seed;
+    c->ft.udpc = fs.udpc.empty() ? nullptr : c->d_udpc;
+    c->ft.udpc_mask = fs.udpc.empty() ? 0 : (uint32_t)fs.udpc.size() - 1;
+    c->ft.udpc_probe = fs.udpc_probe;
+    c->ft.udp_port = fs.port.empty() ? nullptr : c->d_udp_port;
+    c->ft.udp_dip = fs.udp_dip;
+    c->ft.udpw = fs.udpw.empty() ? nullptr : c->d_udpw;
+    c->ft.udpw_lo = fs.udpw_lo;
+    c->ft.udpw_n = (uint32_t)fs.udpw.size();
+}
+
+// whole arrays (a rebuild, or more changes than one delta batch holds), on s;
+// the host waits for the copies (pageable sources)
+static int upload_tab(rx_slot_table &t, uint4 **d, size_t *cap, hipStream_t s) {
+    const size_t bytes = t.slots.size() * sizeof(uint4);
+    int rc = ensure_dev_async((void **)d, cap, bytes, s);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(*d, t.slots.data(), bytes, hipMemcpyHostToDevice, s));
+    t.all_dirty = false;
+    t.dirty.clear();
+    return RXG_OK;
+}
+
+// the counts follow the id space: UDP ids [0, nu), TCP ids at nu + id; a
+// grown id space moves the context's own count vectors to the new layout
+static int counts_layout(rxg_ctx *c, uint32_t nu, uint32_t nt, hipStream_t s) {
+    const uint32_t onu = c->ft.nu, ont = c->ft.nt;
+    const uint32_t nf = std::max(nu + nt, 1u);
+    if (c->d_counts && nu == onu && nt == ont) return RXG_OK;
+    unsigned long long *a = nullptr, *b = nullptr;
+    HIPCHK(hipMallocAsync((void **)&a, (size_t)nf * 8, s));
+    HIPCHK(hipMallocAsync((void **)&b, (size_t)nf * 8, s));
+    HIPCHK(hipMemsetAsync(a, 0, (size_t)nf * 8, s));
+    HIPCHK(hipMemsetAsync(b, 0, (size_t)nf * 8, s));
+    if (c->d_counts) {
+        unsigned long long *src[2] = {c->d_counts, c->d_counts_base}, *dst[2] = {a, b};
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t ku = std::min(onu, nu), kt = std::min(ont, nt);
+            if (ku) HIPCHK(hipMemcpyAsync(dst[k], src[k], ku * 8ull, hipMemcpyDeviceToDevice, s));
+            if (kt)
+                HIPCHK(hipMemcpyAsync(dst[k] + nu, src[k] + onu, kt * 8ull, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipFreeAsync(src[k], s));
+        }
+    }
+    c->d_counts = a;
+    c->d_counts_base = b;
+    c->counts_cap = nf;
+    c->ft.nu = nu;
+    c->ft.nt = nt;
+    return RXG_OK;
+}
+
+// every pending host change of the flow tables onto the device, in stream
+// order on s (after the bursts of other streams that may still read them)
+static int commit_on(rxg_ctx *c, hipStream_t s) {
+    if (c->device == RXG_HOST_ONLY) {
+        c->dirty = false;
+        return RXG_OK;
+    }
+    rx_flowset &fs = c->fs;
+    for (rx_track &x : c->trk)
+        if (x.used && x.s != s) HIPCHK(hipStreamWaitEvent(s, x.ev, 0));
+    for (rxg_ctx::ws_use &u : c->wu)
+        if (u.used && u.st != s) HIPCHK(hipStreamWaitEvent(s, u.ev, 0));
+    int rc = counts_layout(c, fs.udp.id_space(), fs.tcp.id_space(), s);
+    if (rc) return rc;
+    // the previous commit's staging copy must be done before it is refilled
+    if (c->commit_gen) HIPCHK(hipEventSynchronize(c->ev_commit));
+    const size_t nrec = fs.udp.tab.dirty.size() + fs.tcp.tab.dirty.size() +
+                        fs.listen_dirty.size() + fs.port_dirty.size() +
+                        (fs.small_dirty ? (fs.udpc.size() / 2 + (fs.udpw.size() + 7) / 8) : 0);
+    const bool whole = nrec > RX_DELTA_CAP;
+    bool sync = false;
+    if (fs.udp.tab.all_dirty || whole) {
+        if ((rc = upload_tab(fs.udp.tab, &c->d_udp, &c->d_udp_cap, s))) return rc;
+        sync = true;
+    }
+    if (fs.tcp.tab.all_dirty || whole) {
+        if ((rc = upload_tab(fs.tcp.tab, &c->d_tcp, &c->d_tcp_cap, s))) return rc;
+        sync = true;
+    }
+    if (fs.listen_all_dirty || whole) {
+        HIPCHK(hipMemcpyAsync(c->d_listen, fs.listen.data(), 65536 * 4, hipMemcpyHostToDevice, s));
+        fs.listen_all_dirty = false;
+        fs.listen_dirty.clear();
+        sync = true;
+    }
+    if ((fs.port_all_dirty || whole) && !fs.port.empty()) {
+        HIPCHK(hipMemcpyAsync(c->d_udp_port, fs.port.data(), 65536 * 4, hipMemcpyHostToDevice, s));
+        sync = true;
+    }
+    if (fs.port_all_dirty || whole) fs.port_all_dirty = false, fs.port_dirty.clear();
+    uint32_t n = 0;
+    rx_delta *r = c->h_delta;
+    auto put = [&](uint32_t which, uint32_t idx, uint4 v) {
+        r[n].which = which;
+        r[n].idx = idx;
+        r[n]._r0 = r[n]._r1 = 0;
+        r[n].v = v;
+        ++n;
+    };
+    for (uint32_t i : fs.udp.tab.dirty) put(RX_D_UDP, i, fs.udp.tab.slots[i]);
+    for (uint32_t i : fs.tcp.tab.dirty) put(RX_D_TCP, i, fs.tcp.tab.slots[i]);
+    for (uint32_t p : fs.listen_dirty) put(RX_D_LISTEN, p, make_uint4(fs.listen[p], 0, 0, 0));
+    if (!fs.port.empty())
+        for (uint32_t p : fs.port_dirty) put(RX_D_PORT, p, make_uint4(fs.port[p], 0, 0, 0));
+    if (fs.small_dirty) {
+        for (size_t k = 0; 2 * k < fs.udpc.size(); ++k) {
+            const uint2 x = fs.udpc[2 * k], y = fs.udpc[2 * k + 1];
+            put(RX_D_UDPC, (uint32_t)k, make_uint4(x.x, x.y, y.x, y.y));
+        }
+        for (size_t k = 0; 8 * k < fs.udpw.size(); ++k) {
+            uint32_t w[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            for (size_t j = 0; j < 8 && 8 * k + j < fs.udpw.size(); ++j) {
+                const uint32_t sh = 16u * (uint32_t)(j & 1);
+                w[j / 2] = (w[j / 2] & ~(0xFFFFu << sh)) | ((uint32_t)fs.udpw[8 * k + j] << sh);
+            }
+            put(RX_D_UDPW, (uint32_t)k, make_uint4(w[0], w[1], w[2], w[3]));
+        }
+        fs.small_dirty = false;
+    }
+    fs.udp.tab.dirty.clear();
+    fs.tcp.tab.dirty.clear();
+    fs.listen_dirty.clear();
+    fs.port_dirty.clear();
+    if (n) {
+        HIPCHK(hipMemcpyAsync(c->d_delta, c->h_delta, n * sizeof(rx_delta), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(rx_delta_kernel, dim3((n + 255) / 256), dim3(256), 0, s, c->d_delta, n,
+                           c->d_udp, c->d_tcp, c->d_listen, c->d_udp_port,
+                           reinterpret_cast<uint4 *>(c->d_udpc), reinterpret_cast<uint4 *>(c->d_udpw));
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev_commit, s));
+    ++c->commit_gen;
+    for (rx_track &x : c->trk)
+        if (x.used && x.s == s) x.commit_seen = c->commit_gen;
+    ft_fill(c);
+    c->dirty = false;
+    if (sync) HIPCHK(hipStreamSynchronize(s)); // (pageable whole-array sources)
+    return RXG_OK;
+}
+
 extern "C" {
 
 const char *rxg_strerror(int err) {
+
     switch (err) {
     case RXG_OK:
         return "ok";
@@ -326,6 +517,7 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
         c = new (std::nothrow) rxg_ctx();
         if (!c) return RXG_ENOMEM;
         c->device = RXG_HOST_ONLY;
+        c->fs.seed = random_seed();
         rc = rxg_flows_sync(c, nullptr, 0, nullptr, 0);
         if (rc != RXG_OK) {
             rxg_close(c);
@@ -340,16 +532,31 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
     c = new (std::nothrow) rxg_ctx();
     if (!c) return RXG_ENOMEM;
     c->device = device;
+    c->fs.seed = random_seed();
+    dev_guard dg(device);
     do {
-        if ((rc = rx_set_hip_error(hipSetDevice(device)))) break;
+        if ((rc = rx_set_hip_error(dg.err))) break;
         if ((rc = rx_set_hip_error(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))))
             break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_listen, 65536 * sizeof(uint32_t))))) break;
+        if ((rc = rx_set_hip_error(hipMalloc(&c->d_udp_port, 65536 * sizeof(uint32_t))))) break;
+        if ((rc = rx_set_hip_error(hipMalloc(&c->d_udpc, 2 * RX_UDPC_MAX_FLOWS * sizeof(uint2))))) break;
+        if ((rc = rx_set_hip_error(hipMalloc(&c->d_udpw, RX_UDPW_MAX_PORTS * sizeof(uint16_t))))) break;
+        const size_t dbytes = (RX_DELTA_CAP + 2048) * sizeof(rx_delta);
+        if ((rc = rx_set_hip_error(hipHostMalloc((void **)&c->h_delta, dbytes, 0)))) break;
+        if ((rc = rx_set_hip_error(hipMalloc(&c->d_delta, dbytes)))) break;
+        if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ev_commit, hipEventDisableTiming))))
+            break;
+        for (rx_track &t : c->trk)
+            if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming)))) break;
+        if (rc) break;
         for (rxg_ctx::ws_use &u : c->wu)
             if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming))))
                 break;
         if (rc) break;
         if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming))))
+            break;
+        if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming))))
             break;
         c->max_pkts = max_pkts;
         c->max_bytes = (max_bytes + 15) & ~15ull;
@@ -388,22 +595,27 @@ void rxg_close(rxg_ctx *c) {
         delete c;
         return;
     }
-    (void)hipSetDevice(c->device);
-    if (c->s_h2d) (void)hipStreamSynchronize(c->s_h2d);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->s_d2h) (void)hipStreamSynchronize(c->s_d2h);
+    dev_guard dg(c->device);
+    (void)bursts_drain(c);
     (void)hipFree(c->d_udp);
     (void)hipFree(c->d_tcp);
     (void)hipFree(c->d_listen);
     (void)hipFree(c->d_udp_port);
-    (void)hipFree(c->d_counts);
-    (void)hipFree(c->d_ws);
-    (void)hipFree(c->d_aux);
     (void)hipFree(c->d_udpc);
     (void)hipFree(c->d_udpw);
+    (void)hipFree(c->d_delta);
+    if (c->h_delta) (void)hipHostFree(c->h_delta);
+    (void)hipFree(c->d_counts);
+    (void)hipFree(c->d_counts_base);
+    (void)hipFree(c->d_ws);
+    (void)hipFree(c->d_aux);
     for (rxg_ctx::ws_use &u : c->wu)
         if (u.ev) (void)hipEventDestroy(u.ev);
+    for (rx_track &t : c->trk)
+        if (t.ev) (void)hipEventDestroy(t.ev);
+    if (c->ev_commit) (void)hipEventDestroy(c->ev_commit);
     if (c->ev_k1) (void)hipEventDestroy(c->ev_k1);
+    if (c->ev_aux) (void)hipEventDestroy(c->ev_aux);
     for (rxg_ctx::slot &sl : c->slots) {
         (void)hipFree(sl.d_pkts);
         (void)hipFree(sl.d_off);
@@ -422,97 +634,243 @@ void rxg_close(rxg_ctx *c) {
     delete c;
 }
 
-int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t, uint32_t nt) {
-    if (!c || (nu && !u) || (nt && !t)) return RXG_EINVAL;
-    // UDP: get_hostinfo_fromip_port matches (dip, dport, proto); every socket
-    // the reference creates has protocol 17 (nsocket, common.c:281), and the
-    // lookup is only ever called with 17 (udp.c:14), so others never match.
-    std::vector<uint4> ue;
-    ue.reserve(nu);
-    for (uint32_t i = 0; i < nu; ++i)
-        if (u[i].protocol == 17) ue.push_back(make_uint4(u[i].localip, u[i].localport, 17u, i));
-    std::vector<uint4> te;
-    te.reserve(nt);
-    for (uint32_t i = 0; i < nt; ++i)
-        te.push_back(make_uint4(t[i].sip, t[i].dip,
-                                (uint32_t)t[i].sport | ((uint32_t)t[i].dport << 16), i));
-    c->h_udp.build(ue, c->ft_load_log2);
-    c->h_tcp.build(te, c->ft_load_log2);
-    build_udpc(c->h_udp, nu, &c->h_udpc, &c->udpc_probe);
-    c->h_udp_port.clear();
-    if (!ue.empty() && !(c->tune_tables & RXG_TT_NO_UDP_PORT))
-        c->udp_dip = build_udp_port(c->h_udp, &c->h_udp_port);
-    build_udpw(c->h_udp_port, !c->h_udpc.empty(), &c->h_udpw, &c->udpw_lo);
-    c->h_listen.assign(65536, RXG_FLOW_NONE);
-    for (uint32_t i = 0; i < nt; ++i)
-        if (t[i].status == RXG_TCP_STATUS_LISTEN) c->h_listen[t[i].dport] = i;
-    c->ft.nu = nu;
-    c->ft.nt = nt;
-    if (c->device == RXG_HOST_ONLY) return RXG_OK;
-    HIPCHK(hipSetDevice(c->device));
+// ---- control blocks (rx_flows.h) ------------------------------------------
+static void udp_set(rx_block &x, const rxg_udp_sock &u) {
+    x.a = u.localip;
+    x.b = u.localport;
+    x.c = 17u;
+    x.status = u.protocol;
+    // get_hostinfo_fromip_port matches (dip, dport, proto); every socket the
+    // reference creates has protocol 17 (nsocket, common.c:281) and the lookup
+    // is only called with 17 (udp.c:14), so other protocols never match
+    x.keyed = u.protocol == 17;
+}
+static void tcp_set(rx_block &x, const rxg_tcb &t) {
+    x.a = t.sip;
+    x.b = t.dip;
+    x.c = (uint32_t)t.sport | ((uint32_t)t.dport << 16);
+    x.status = t.status;
+    x.keyed = true;
+}
 
-    // control-plane operation: wait for in-flight bursts before replacing tables
-    HIPCHK(hipDeviceSynchronize());
-    int rc;
-    if ((rc = ensure_dev((void **)&c->d_udp, &c->d_udp_cap, c->h_udp.slots.size() * sizeof(uint4))))
-        return rc;
-    if ((rc = ensure_dev((void **)&c->d_tcp, &c->d_tcp_cap, c->h_tcp.slots.size() * sizeof(uint4))))
-        return rc;
-    HIPCHK(hipMemcpy(c->d_udp, c->h_udp.slots.data(), c->h_udp.slots.size() * sizeof(uint4),
-                     hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_tcp, c->h_tcp.slots.data(), c->h_tcp.slots.size() * sizeof(uint4),
-                     hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_listen, c->h_listen.data(), 65536 * sizeof(uint32_t),
-                     hipMemcpyHostToDevice));
-    c->ft.udpc = nullptr;
-    c->ft.udpc_mask = c->ft.udpc_probe = 0;
-    if (!c->h_udpc.empty()) {
-        if ((rc = ensure_dev((void **)&c->d_udpc, &c->d_udpc_cap, c->h_udpc.size() * sizeof(uint2))))
-            return rc;
-        HIPCHK(hipMemcpy(c->d_udpc, c->h_udpc.data(), c->h_udpc.size() * sizeof(uint2),
-                         hipMemcpyHostToDevice));
-        c->ft.udpc = c->d_udpc;
-        c->ft.udpc_mask = (uint32_t)c->h_udpc.size() - 1;
-        c->ft.udpc_probe = c->udpc_probe;
+// the whole flow set, then every device table: a control-plane operation that
+// waits for this context's own bursts (never the device's other work)
+static int full_upload(rxg_ctx *c) {
+    c->fs.rebuild_all(next_seed);
+    c->dirty = true;
+    if (c->device == RXG_HOST_ONLY) {
+        c->ft.nu = c->fs.udp.id_space();
+        c->ft.nt = c->fs.tcp.id_space();
+        c->ft.hseed = c->fs.seed;
+        c->dirty = false;
+        return RXG_OK;
     }
-    c->ft.udp_port = nullptr;
-    if (!c->h_udp_port.empty()) {
-        if (!c->d_udp_port) HIPCHK(hipMalloc(&c->d_udp_port, 65536 * sizeof(uint32_t)));
-        HIPCHK(hipMemcpy(c->d_udp_port, c->h_udp_port.data(), 65536 * sizeof(uint32_t),
-                         hipMemcpyHostToDevice));
-        c->ft.udp_port = c->d_udp_port;
-        c->ft.udp_dip = c->udp_dip;
-    }
-    c->ft.udpw = nullptr;
-    c->ft.udpw_lo = c->ft.udpw_n = 0;
-    if (!c->h_udpw.empty()) {
-        if ((rc = ensure_dev((void **)&c->d_udpw, &c->d_udpw_cap, c->h_udpw.size() * sizeof(uint16_t))))
-            return rc;
-        HIPCHK(hipMemcpy(c->d_udpw, c->h_udpw.data(), c->h_udpw.size() * sizeof(uint16_t),
-                         hipMemcpyHostToDevice));
-        c->ft.udpw = c->d_udpw;
-        c->ft.udpw_lo = c->udpw_lo;
-        c->ft.udpw_n = (uint32_t)c->h_udpw.size();
-    }
-    c->ft.udp = c->d_udp;
-    c->ft.tcp = c->d_tcp;
-    c->ft.listen = c->d_listen;
-    c->ft.udp_mask = c->h_udp.mask;
-    c->ft.tcp_mask = c->h_tcp.mask;
-    c->ft.udp_probe = c->h_udp.probe;
-    c->ft.tcp_probe = c->h_tcp.probe;
-    // context counts follow the flow set
-    const uint32_t nf = nu + nt;
-    if (c->counts_cap < nf || !c->d_counts) {
-        (void)hipFree(c->d_counts);
-        c->d_counts = nullptr;
-        c->counts_cap = 0;
-        HIPCHK(hipMalloc(&c->d_counts, (size_t)std::max(nf, 1u) * 8));
-        c->counts_cap = std::max(nf, 1u);
-    }
-    HIPCHK(hipMemset(c->d_counts, 0, (size_t)c->counts_cap * 8));
+    DEVGUARD(c);
+    int rc = bursts_drain(c);
+    if (rc) return rc;
+    rc = commit_on(c, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;
 }
+
+int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t, uint32_t nt) {
+    if (!c || (nu && !u) || (nt && !t)) return RXG_EINVAL;
+    rx_flowset &fs = c->fs;
+    fs.clear();
+    fs.port_table = !(c->tune_tables & RXG_TT_NO_UDP_PORT);
+    fs.udp.blk.resize(nu);
+    for (uint32_t i = 0; i < nu; ++i) {
+        rx_block &x = fs.udp.blk[i];
+        udp_set(x, u[i]);
+        x.seq = fs.udp.seq_next++;
+        x.live = true;
+    }
+    fs.udp.live = nu;
+    fs.tcp.blk.resize(nt);
+    for (uint32_t i = 0; i < nt; ++i) {
+        rx_block &x = fs.tcp.blk[i];
+        tcp_set(x, t[i]);
+        x.seq = fs.tcp.seq_next++;
+        x.live = true;
+    }
+    fs.tcp.live = nt;
+    for (uint32_t i = 0; i < nt; ++i)
+        if (t[i].status == RXG_TCP_STATUS_LISTEN) fs.listen_add(i);
+    int rc = full_upload(c); // (rebuild_all places each key's newest block)
+    if (rc) return rc;
+    // chains of duplicate keys, newest first: one walk over the blocks, newest first
+    for (rx_registry *r : {&fs.udp, &fs.tcp}) {
+        std::vector<uint32_t> tail(r->tab.ns(), RXG_FLOW_NONE);
+        for (uint32_t id = (uint32_t)r->blk.size(); id-- > 0;) {
+            rx_block &x = r->blk[id];
+            x.older = RXG_FLOW_NONE;
+            if (!x.keyed) continue;
+            const uint32_t i = r->tab.find(x.a, x.b, x.c);
+            if (tail[i] != RXG_FLOW_NONE) r->blk[tail[i]].older = id;
+            tail[i] = id;
+        }
+    }
+    if (c->device != RXG_HOST_ONLY) { // context counts follow the flow set
+        DEVGUARD(c);
+        HIPCHK(hipMemsetAsync(c->d_counts, 0, (size_t)c->counts_cap * 8, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_counts_base, 0, (size_t)c->counts_cap * 8, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return RXG_OK;
+}
+
+// a table past load 1/2 or a probe sequence past RX_PROBE_CAP: rebuilt whole
+// (the next commit uploads it); the registry changes stay O(1) otherwise
+static void after_change(rxg_ctx *c, bool cap_ok) {
+    rx_flowset &fs = c->fs;
+    if (!cap_ok || fs.needs_rebuild(fs.udp, false) || fs.needs_rebuild(fs.tcp, false))
+        fs.rebuild_all(next_seed);
+    c->dirty = true;
+}
+
+static bool udp_link(rx_flowset &fs, uint32_t id) {
+    rx_block &x = fs.udp.blk[id];
+    if (!x.keyed) return true;
+    const bool ok = fs.udp.link(id);
+    if (fs.port_table && (fs.port.empty() || (fs.on_dip == 0 && x.a != fs.udp_dip)))
+        fs.port_rebuild(); // first socket, or none left on the table's address
+    else
+        fs.port_track(x, +1);
+    return ok;
+}
+static void udp_unlink(rx_flowset &fs, uint32_t id) {
+    rx_block &x = fs.udp.blk[id];
+    if (!x.keyed) return;
+    fs.udp.unlink(id);
+    fs.port_track(x, -1);
+}
+
+int rxg_flows_add(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t, uint32_t nt,
+                  uint32_t *udp_ids, uint32_t *tcp_ids) {
+    if (!c || (nu && (!u || !udp_ids)) || (nt && (!t || !tcp_ids))) return RXG_EINVAL;
+    rx_flowset &fs = c->fs;
+    const uint32_t onu = fs.udp.id_space(), ont = fs.tcp.id_space();
+    // room first: no table may pass load 1/2 while the batch goes in
+    if ((uint64_t)(fs.udp.tab.used + nu) * 2 > fs.udp.tab.ns() ||
+        (uint64_t)(fs.tcp.tab.used + nt) * 2 > fs.tcp.tab.ns())
+        fs.rebuild_all(next_seed, nu, nt);
+    bool ok = true;
+    for (uint32_t k = 0; k < nu; ++k) {
+        const uint32_t id = fs.udp.alloc_id();
+        rx_block &x = fs.udp.blk[id];
+        udp_set(x, u[k]);
+        x.seq = fs.udp.seq_next++;
+        x.live = true;
+        x.older = RXG_FLOW_NONE;
+        ++fs.udp.live;
+        ok &= udp_link(fs, id);
+        udp_ids[k] = id;
+    }
+    for (uint32_t k = 0; k < nt; ++k) {
+        const uint32_t id = fs.tcp.alloc_id();
+        rx_block &x = fs.tcp.blk[id];
+        tcp_set(x, t[k]);
+        x.seq = fs.tcp.seq_next++;
+        x.live = true;
+        x.older = RXG_FLOW_NONE;
+        ++fs.tcp.live;
+        ok &= fs.tcp.link(id); // tcp_stream_create + LL_ADD (tcp.c:3-52)
+        if (x.status == RXG_TCP_STATUS_LISTEN) fs.listen_add(id);
+        tcp_ids[k] = id;
+    }
+    if (nu) fs.small_rebuild();
+    after_change(c, ok);
+    // 1: the count layout (rxg_num_udp_ids) grew
+    return (fs.udp.id_space() != onu && ont + onu > 0 && fs.tcp.id_space() > 0) ? 1 : 0;
+}
+
+int rxg_flows_remove(rxg_ctx *c, const uint32_t *udp_ids, uint32_t nu, const uint32_t *tcp_ids,
+                     uint32_t nt) {
+    if (!c || (nu && !udp_ids) || (nt && !tcp_ids)) return RXG_EINVAL;
+    rx_flowset &fs = c->fs;
+    for (uint32_t k = 0; k < nu; ++k)
+        if (udp_ids[k] >= fs.udp.id_space() || !fs.udp.blk[udp_ids[k]].live) return RXG_EINVAL;
+    for (uint32_t k = 0; k < nt; ++k)
+        if (tcp_ids[k] >= fs.tcp.id_space() || !fs.tcp.blk[tcp_ids[k]].live) return RXG_EINVAL;
+    for (uint32_t k = 0; k < nu; ++k) {
+        const uint32_t id = udp_ids[k];
+        if (!fs.udp.blk[id].live) continue; // (listed twice)
+        udp_unlink(fs, id);
+        fs.udp.blk[id].live = false;
+        --fs.udp.live;
+        fs.udp.free_ids.push_back(id);
+    }
+    for (uint32_t k = 0; k < nt; ++k) {
+        const uint32_t id = tcp_ids[k];
+        rx_block &x = fs.tcp.blk[id];
+        if (!x.live) continue;
+        if (x.status == RXG_TCP_STATUS_LISTEN) fs.listen_del(id);
+        fs.tcp.unlink(id); // LL_REMOVE (tcp.c:321, common.c:620,660)
+        x.live = false;
+        --fs.tcp.live;
+        fs.tcp.free_ids.push_back(id);
+    }
+    if (nu) fs.small_rebuild();
+    after_change(c, true);
+    return RXG_OK;
+}
+
+int rxg_flows_update_udp(rxg_ctx *c, uint32_t id, const rxg_udp_sock *u) {
+    if (!c || !u) return RXG_EINVAL;
+    rx_flowset &fs = c->fs;
+    if (id >= fs.udp.id_space() || !fs.udp.blk[id].live) return RXG_EINVAL;
+    udp_unlink(fs, id);
+    udp_set(fs.udp.blk[id], *u); // nbind (common.c:350-353): same list position
+    const bool ok = udp_link(fs, id);
+    fs.small_rebuild();
+    after_change(c, ok);
+    return RXG_OK;
+}
+
+int rxg_flows_update_tcb(rxg_ctx *c, uint32_t id, const rxg_tcb *t) {
+    if (!c || !t) return RXG_EINVAL;
+    rx_flowset &fs = c->fs;
+    if (id >= fs.tcp.id_space() || !fs.tcp.blk[id].live) return RXG_EINVAL;
+    rx_block &x = fs.tcp.blk[id];
+    const bool was_listen = x.status == RXG_TCP_STATUS_LISTEN;
+    const uint32_t c2 = (uint32_t)t->sport | ((uint32_t)t->dport << 16);
+    const bool rekey = x.a != t->sip || x.b != t->dip || x.c != c2;
+    const bool is_listen = t->status == RXG_TCP_STATUS_LISTEN;
+    if (!rekey && was_listen == is_listen) { // a state change the tables do not see
+        x.status = t->status;
+        return RXG_OK;
+    }
+    if (was_listen) fs.listen_del(id);
+    bool ok = true;
+    if (rekey) {
+        fs.tcp.unlink(id);
+        tcp_set(x, *t); // nbind / nlisten (common.c:358-386): same list position
+        ok = fs.tcp.link(id);
+    } else {
+        x.status = t->status;
+    }
+    if (is_listen) fs.listen_add(id);
+    after_change(c, ok);
+    return RXG_OK;
+}
+
+int rxg_flows_commit(rxg_ctx *c, void *stream) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) {
+        c->dirty = false;
+        return RXG_OK;
+    }
+    DEVGUARD(c);
+    const hipStream_t s = (hipStream_t)stream;
+    int rc = burst_begin(c, s); // commits on s and tracks s
+    if (rc) return rc;
+    return burst_end(c, s);
+}
+
+uint32_t rxg_num_udp_ids(const rxg_ctx *c) { return c ? c->fs.udp.id_space() : 0; }
+
+uint32_t rxg_flows_rebuilds(const rxg_ctx *c) { return c ? c->fs.rebuilds : 0; }
 
 int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline) {
@@ -552,7 +910,8 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B))) return RXG_EINVAL;
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_NO_TRACK)))
+        return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
     return RXG_OK;
@@ -560,25 +919,29 @@ int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
 
 int rxg_tune_flow_load(rxg_ctx *c, uint32_t load_log2) {
     if (!c || load_log2 > 4) return RXG_EINVAL;
-    c->ft_load_log2 = load_log2 ? load_log2 : RX_FT_LOAD_LOG2;
+    c->fs.load_log2 = load_log2 ? load_log2 : RX_FT_LOAD_LOG2;
     return RXG_OK;
 }
 
-uint32_t rxg_num_flows(const rxg_ctx *c) { return c ? c->ft.nu + c->ft.nt : 0; }
+// the count layout of the next burst (pending changes included)
+uint32_t rxg_num_flows(const rxg_ctx *c) {
+    return c ? c->fs.udp.id_space() + c->fs.tcp.id_space() : 0;
+}
 
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *c, uint32_t dip, uint16_t dport) {
     if (!c) return RXG_FLOW_NONE;
+    const rx_flowset &fs = c->fs;
     uint32_t f;
-    if (!c->h_udp_port.empty() && rx_udp_port_decide(c->h_udp_port[dport], dip, c->udp_dip, &f))
-        return f;
-    return c->h_udp.lookup(dip, dport, 17u);
+    if (!fs.port.empty() && rx_udp_port_decide(fs.port[dport], dip, fs.udp_dip, &f)) return f;
+    return fs.udp.tab.lookup(dip, dport, 17u);
 }
 
 uint32_t rxg_ft_lookup_tcp(const rxg_ctx *c, uint32_t sip, uint32_t dip, uint16_t sport,
                            uint16_t dport) {
     if (!c) return RXG_FLOW_NONE;
-    uint32_t f = c->h_tcp.lookup(sip, dip, (uint32_t)sport | ((uint32_t)dport << 16));
-    if (f == RXG_FLOW_NONE && !c->h_listen.empty()) f = c->h_listen[dport];
+    const rx_flowset &fs = c->fs;
+    uint32_t f = fs.tcp.tab.lookup(sip, dip, (uint32_t)sport | ((uint32_t)dport << 16));
+    if (f == RXG_FLOW_NONE) f = fs.listen[dport];
     return f;
 }
 
@@ -619,7 +982,7 @@ static int ws_prepare(rxg_ctx *c, size_t ws, const rxg_ctx::ws_shape &layout, hi
 
 // one burst on the workspace: classify + count on s (count_stream null or s),
 // or classify on s and the slab count on count_stream (double-buffered indices)
-static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
                        uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
                        unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
@@ -670,6 +1033,20 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     return RXG_OK;
 }
 
+// a burst: pending flow-table changes first (stream-ordered on s), then the
+// launches, then the tracking event that later table writes wait on
+static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                       const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
+                       uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
+                       unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
+    int rc = burst_begin(c, s);
+    if (rc) return rc;
+    rc = classify_ws_body(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, d_out,
+                          d_counts, s, cs);
+    if (rc) return rc;
+    return burst_end(c, s);
+}
+
 static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                              const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
                              uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
@@ -679,7 +1056,7 @@ static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *
     if (n == 0) return RXG_OK;
     if (!d_pkts || !d_off || !d_len || !d_out) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
     return classify_ws(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe,
@@ -759,7 +1136,7 @@ int rxg_submit(rxg_ctx *c, const uint8_t *pkts, uint64_t span_bytes, const uint3
     if (!out) return RXG_EINVAL;
     int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2);
     if (rc) return rc;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     const uint64_t t = c->next_ticket++;
     rc = submit_slot(c, c->slots[t % RXG_PIPE_DEPTH], pkts, span_bytes, off, len, n,
                      off_unit_log2, out, t);
@@ -775,7 +1152,7 @@ int rxg_wait(rxg_ctx *c, uint64_t ticket) {
     const rxg_ctx::slot &sl = c->slots[ticket % RXG_PIPE_DEPTH];
     // a slot reused by a later burst: its events now mark that burst, which
     // completes after this one (stream order), so waiting on it is safe
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     HIPCHK(hipEventSynchronize(sl.ev_done));
     return RXG_OK;
 }
@@ -808,7 +1185,7 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
     if (n == 0) return RXG_OK;
     if (!m || !out) return RXG_EINVAL;
     if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
     if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_stage
@@ -836,7 +1213,7 @@ int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const u
     if (n == 0) return RXG_OK;
     if (!d_pkts || !d_off || !d_len) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     HIPCHK(tx_cksum_launch(d_pkts, d_off, d_len, n, off_unit_log2, len_hint, c->tune_tx,
                            c->tune_tx_bpc, (hipStream_t)stream));
     return RXG_OK;
@@ -848,7 +1225,7 @@ int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t 
     if (n == 0) return c ? RXG_OK : RXG_EINVAL;
     int rc = check_host_burst(c, pkts, span_bytes, off, len, n, off_unit_log2);
     if (rc) return rc;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     const uint64_t span = span_bytes;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
@@ -871,6 +1248,25 @@ int rxg_tx_cksum(rxg_ctx *c, uint8_t *pkts, uint64_t span_bytes, const uint32_t 
     return RXG_OK;
 }
 
+// the split / gather workspace d_aux: a use on another stream than the last
+// one waits for it (event), growth waits on the host for the last use only
+static int aux_begin(rxg_ctx *c, size_t ws, hipStream_t s) {
+    if (ws > c->d_aux_cap) {
+        if (c->aux_used) HIPCHK(hipEventSynchronize(c->ev_aux));
+        int rc = ensure_dev_async(&c->d_aux, &c->d_aux_cap, ws, s);
+        if (rc) return rc;
+    } else if (c->aux_used && c->aux_st != s) {
+        HIPCHK(hipStreamWaitEvent(s, c->ev_aux, 0));
+    }
+    return RXG_OK;
+}
+static int aux_end(rxg_ctx *c, hipStream_t s) {
+    HIPCHK(hipEventRecord(c->ev_aux, s));
+    c->aux_st = s;
+    c->aux_used = true;
+    return RXG_OK;
+}
+
 int rxg_rss_split_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                       const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t n_shards,
                       uint32_t *d_first, uint32_t *d_perm, void *stream) {
@@ -878,17 +1274,14 @@ int rxg_rss_split_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
     if (n && (!d_pkts || !d_off || !d_len || !d_perm)) return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     const hipStream_t s = (hipStream_t)stream;
     const size_t ws = rx_split_ws_bytes(n, n_shards);
-    if (ws > c->d_aux_cap) { // grows between bursts only
-        HIPCHK(hipDeviceSynchronize());
-        int rc = ensure_dev(&c->d_aux, &c->d_aux_cap, ws);
-        if (rc) return rc;
-    }
+    int rc = aux_begin(c, ws, s);
+    if (rc) return rc;
     HIPCHK(rx_split_launch(d_pkts, d_off, d_len, n, off_unit_log2, n_shards, d_first, d_perm,
                            c->d_aux, s));
-    return RXG_OK;
+    return aux_end(c, s);
 }
 
 int rxg_gather_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
@@ -902,14 +1295,11 @@ int rxg_gather_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     if (!d_pkts || !d_off || !d_len || !d_idx || !d_dst || !d_dst_off || !d_dst_len)
         return RXG_EINVAL;
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
     const hipStream_t s = (hipStream_t)stream;
     const size_t ws = rx_gather_ws_bytes(count);
-    if (ws > c->d_aux_cap) {
-        HIPCHK(hipDeviceSynchronize());
-        int rc = ensure_dev(&c->d_aux, &c->d_aux_cap, ws);
-        if (rc) return rc;
-    }
+    int rc = aux_begin(c, ws, s);
+    if (rc) return rc;
     HIPCHK(rx_gather_launch(d_pkts, d_off, d_len, off_unit_log2, d_idx, count, d_dst, dst_cap,
                             d_dst_off, d_dst_len, c->d_aux, s));
     // the packed size (64-B units) sits after the per-chunk sums
@@ -918,18 +1308,27 @@ int rxg_gather_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
     HIPCHK(hipMemcpyAsync(&units, reinterpret_cast<uint64_t *>(c->d_aux) + nchunks, 8,
                           hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if ((rc = aux_end(c, s))) return rc;
     if (span) *span = units << 6;
     if ((units << 6) > dst_cap || units > 0xFFFFFFFFull) return RXG_ERANGE;
     return RXG_OK;
 }
 
+// the increment since the last call is all-reduced and folded into the
+// running total, so repeated calls never multiply earlier traffic by the ranks
 int rxg_ctx_counts_allreduce(rxg_ctx *c, rxg_group *g) {
     if (!c || !g) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    HIPCHK(hipSetDevice(c->device));
-    const uint32_t nf = c->ft.nu + c->ft.nt;
-    int rc = rx_group_allreduce_u64(g, c->d_counts, nf, c->stream); // after the bursts' kernels
+    DEVGUARD(c);
+    int rc = bursts_drain(c); // every burst counted; the counts' stream order
     if (rc) return rc;
+    const uint32_t nf = c->ft.nu + c->ft.nt;
+    if (!nf) return RXG_OK;
+    rc = rx_group_allreduce_u64(g, c->d_counts, nf, c->stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rx_counts_fold_kernel, dim3((nf + 255) / 256), dim3(256), 0, c->stream,
+                       c->d_counts_base, c->d_counts, nf);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return RXG_OK;
 }
@@ -939,18 +1338,26 @@ int rxg_flow_counts(rxg_ctx *c, uint64_t *counts, uint32_t ncounts) {
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
     const uint32_t nf = c->ft.nu + c->ft.nt;
     if (ncounts < nf) return RXG_ERANGE;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream)); // every submitted burst's kernel has counted
-    if (nf) HIPCHK(hipMemcpy(counts, c->d_counts, nf * 8ull, hipMemcpyDeviceToHost));
+    DEVGUARD(c);
+    int rc = bursts_drain(c); // every submitted burst's kernel has counted
+    if (rc) return rc;
+    if (!nf) return RXG_OK;
+    std::vector<uint64_t> base(nf);
+    HIPCHK(hipMemcpy(counts, c->d_counts, nf * 8ull, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(base.data(), c->d_counts_base, nf * 8ull, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < nf; ++i) counts[i] += base[i];
     return RXG_OK;
 }
 
 int rxg_counts_reset(rxg_ctx *c) {
     if (!c) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    HIPCHK(hipSetDevice(c->device));
+    DEVGUARD(c);
+    int rc = bursts_drain(c);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->d_counts, 0, (size_t)c->counts_cap * 8, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_counts_base, 0, (size_t)c->counts_cap * 8, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemset(c->d_counts, 0, (size_t)c->counts_cap * 8));
     return RXG_OK;
 }
 

@@ -65,6 +65,21 @@ namespace {
 static thread_local uint32_t g_bpc_cap = 0;
 
 // Frames of one lane group for one trip: descriptors and the first P passes.
+// flow 65535 at exactly 65536 flows with 2-B count indices (rx_ft_dev::
+// count_ffff): its frames are added here, one atomic per wave
+__device__ __forceinline__ void count_ffff(const rx_ft_dev &ft, uint32_t idx) {
+    const bool hit = idx == 0xFFFFu; // (not counted = 0xFFFFFFFF)
+    const uint64_t m = __ballot(hit);
+    if (m && hit && __lane_id() == (uint32_t)__builtin_ctzll(m))
+        atomicAdd(ft.count_ffff, (unsigned long long)__popcll(m));
+}
+
+// per-lane count index (lane kernels, group kernels)
+__device__ __forceinline__ void put_count_idx(const rx_ft_dev &ft, uint64_t p, uint32_t idx) {
+    if (ft.count_ffff) count_ffff(ft, idx);
+    rx_put_count_idx(ft, p, idx);
+}
+
 template <int FPG, int P>
 struct group_frames {
     uint64_t pf[FPG]; // frame index (the verdict slot)
@@ -288,7 +303,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             probe[f] = false;
         flow[f] = fd;
         const uint32_t mask = udp ? ft.udp_mask : ft.tcp_mask;
-        slot[f] = rx_hash3(ka[f], kb[f], kc[f]) & mask;
+        slot[f] = rx_hash3s(ft.hseed, ka[f], kb[f], kc[f]) & mask;
         sl[f] = make_uint4(0, 0, 0, RX_SLOT_EMPTY);
         if (probe[f] && gl < RX_WINDOW) sl[f] = ld_slot((udp ? ft.udp : ft.tcp) + ((slot[f] + gl) & mask));
     }
@@ -360,7 +375,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
                 else
                     atomicAdd(&counts[idx], 1ull);
             }
-            if (ft.count_idx) rx_put_count_idx(ft, S.pf[f], counted ? idx : 0xFFFFFFFFu);
+            if (ft.count_idx) put_count_idx(ft, S.pf[f], counted ? idx : 0xFFFFFFFFu);
         }
     }
 }
@@ -661,7 +676,7 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
             const uint32_t e = lw[k];
             flow = e == 0xFFFFu ? RXG_FLOW_NONE : e;
         } else {
-            uint32_t i = rx_hash3(dip, dport, 17u) & ft.udpc_mask;
+            uint32_t i = rx_hash3s(ft.hseed, dip, dport, 17u) & ft.udpc_mask;
             for (uint32_t pr = 0; pr < ft.udpc_probe; ++pr, i = (i + 1) & ft.udpc_mask) {
                 const uint2 sl = lt[i];
                 if (sl.y == 0xFFFFFFFFu) break;
@@ -680,7 +695,7 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
         uint32_t maxp = is_udp ? ft.udp_probe : ft.tcp_probe;
         if (is_udp && ft.udp_port && rx_udp_port_decide(ft.udp_port[dport], dip, ft.udp_dip, &flow))
             maxp = 0; // decided by the direct port table
-        uint32_t i = rx_hash3(ka, kb, kc) & mask;
+        uint32_t i = rx_hash3s(ft.hseed, ka, kb, kc) & mask;
         for (uint32_t pr = 0; pr < maxp; ++pr, i = (i + 1) & mask) { // ~1.2 trips expected
             const uint4 sl = ld_slot(tbl + i);
             if (sl.w == RX_SLOT_EMPTY) break;
@@ -747,6 +762,7 @@ __device__ __forceinline__ void lane_count(uint32_t idx, unsigned long long *__r
 __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t p, uint32_t idx,
                                                    uint32_t lane) {
     if (!ft.count_idx) return;
+    if (ft.count_ffff) count_ffff(ft, idx);
     if (ft.cidx16) {
         const uint32_t v = idx & 0xFFFFu;
         const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x101, 0xF, 0xF, false));
@@ -794,7 +810,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         else
             lane_store<ST_NT>(out, L.p, v);
         lane_count(idx, counts, hist, lds_bins);
-        if (ft.count_idx) rx_put_count_idx(ft, L.p, idx);
+        if (ft.count_idx) put_count_idx(ft, L.p, idx);
     }
 }
 
@@ -854,7 +870,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             pend_p = L.p;
             pend_valid = L.valid;
             lane_count(idx, counts, hist, lds_bins);
-            if (ft.count_idx && L.valid) rx_put_count_idx(ft, L.p, idx);
+            if (ft.count_idx && L.valid) put_count_idx(ft, L.p, idx);
             L.p = np;
             L.valid = nvalid;
             L.fb = pkts + ((uint64_t)noff << unit_log2);
@@ -1396,7 +1412,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
         // a dummy load of the frame's own head then)
         const bool hash0 = probe0 && !udp_port;
         const uint4 *sp0 = hash0 ? (is_udp ? ft.udp : ft.tcp) +
-                                       (rx_hash3(ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
+                                       (rx_hash3s(ft.hseed, ka, kb, kc) & (is_udp ? ft.udp_mask : ft.tcp_mask))
                                  : reinterpret_cast<const uint4 *>(fb);
         static_assert(PW == 1 || PW == 2 || PW == 4, "probe window");
         uint4 sw[PW];
@@ -1457,7 +1473,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
                 const uint4 *tb = is_udp ? ft.udp : ft.tcp;
                 const uint32_t mk = is_udp ? ft.udp_mask : ft.tcp_mask;
                 const uint32_t mp = is_udp ? ft.udp_probe : ft.tcp_probe;
-                uint32_t pj = rx_hash3(ka, kb, kc) & mk;
+                uint32_t pj = rx_hash3s(ft.hseed, ka, kb, kc) & mk;
                 uint32_t pr = 0;
                 bool done = false;
                 if (hash0) { // the window loaded with the head
@@ -1793,7 +1809,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         const bool hash0 = probe0 && !udp_port;
         const uint4 *sp0 =
             hash0 ? (h.is_udp ? ft.udp : ft.tcp) +
-                        (rx_hash3(h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask))
+                        (rx_hash3s(ft.hseed, h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask))
                   : reinterpret_cast<const uint4 *>(pkts);
         pe = (ABL & 1) ? RXG_FLOW_NONE : ptab[h.l4 ? dport : 0u];
 #pragma unroll
@@ -1931,7 +1947,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     if (hashed) {
         const uint4 *tb = h.is_udp ? ft.udp : ft.tcp;
         const uint32_t mk = h.is_udp ? ft.udp_mask : ft.tcp_mask;
-        uint32_t pj = rx_hash3(h.ka, h.kb, h.kc) & mk;
+        uint32_t pj = rx_hash3s(ft.hseed, h.ka, h.kb, h.kc) & mk;
         uint32_t pr = 0;
         bool done = false;
         if (hash0) { // the window loaded with the head
@@ -2014,8 +2030,9 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
 // memory-side request): the classify kernel writes one count index per frame
 // (ft.count_idx: 2 B when the flows fit one 65536-flow range, else 4 B), and
-// a slab histogram sums them.  A 2-B index of all ones is flow 65535 or a
-// frame not counted: the slab pass reads that frame's verdict to tell which.  Pass 1: block b (1024 threads, one per CU: 128
+// a slab histogram sums them.  A 2-B index of all ones is a frame not counted
+// (flow 65535 of exactly 65536 is counted by the classify kernel itself,
+// rx_ft_dev::count_ffff).  Pass 1: block b (1024 threads, one per CU: 128
 // KiB of LDS) adds the indices of its share of the frames that fall in its
 // 65536-flow range (blockIdx.y) into 16-bit LDS bins, two per dword (lo =
 // even flow, hi = odd), and writes the bins out as slab b.  A bin overflows
@@ -2030,8 +2047,7 @@ constexpr uint32_t SLAB_MIN_FLOWS = 8193;   // below: LDS histogram in the class
 
 template <typename T> // count index: uint16_t (one range, <= 65536 flows) or uint32_t
 __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict__ cidx,
-                                                              const uint4 *__restrict__ verd,
-                                                              uint32_t nu, uint32_t n, uint32_t per,
+                                                              uint32_t n, uint32_t per,
                                                               uint32_t words, uint32_t nflows,
                                                               uint32_t *__restrict__ slab,
                                                               unsigned long long *__restrict__ counts) {
@@ -2045,7 +2061,6 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
     __syncthreads();
     const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
     const uint32_t lim = min(nflows - f0, SLAB_MAX_FLOWS);
-    const bool amb = nflows > 0xFFFFu; // a 2-B all-ones index may be flow 65535
     const uint64_t b0 = (uint64_t)blockIdx.x * per;
     const uint64_t b1 = min((uint64_t)n, b0 + per);
     uint32_t mine = 0;
@@ -2056,14 +2071,12 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
             ++mine;
         }
     };
-    // a 2-B all-ones index: flow 65535 or not counted, from the frame's verdict
-    auto from_verdict = [&](uint4 v) -> uint32_t {
-        const bool counted = (int8_t)(v.z >> 24) == RXG_RC_OK && v.x != RXG_FLOW_NONE;
-        return counted ? (((v.z >> 16) & 0xFFu) == RXG_CLS_TCP ? nu : 0u) + v.x : ~0u;
-    };
-    auto index_of = [&](uint32_t x, uint64_t k) -> uint32_t {
+    // a 2-B all-ones index is never counted here: with fewer than 65536 flows
+    // it is no flow, and with exactly 65536 flow 65535 was counted by the
+    // classify kernel (rx_ft_dev::count_ffff)
+    auto index_of = [&](uint32_t x) -> uint32_t {
         if constexpr (sizeof(T) == 2)
-            if (x == 0xFFFFu) return amb ? from_verdict(verd[k]) : ~0u;
+            if (x == 0xFFFFu) return ~0u;
         return x;
     };
     // 4E indices per thread per trip (four 16-B loads in flight); b0 is a
@@ -2074,41 +2087,22 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * E * 1024));
-        if constexpr (sizeof(T) == 2) {
-            // an all-ones index is flow 65535 iff the frame's rc is RXG_RC_OK
-            // (rc OK <=> a control block matched); only with 65536 flows is it
-            // ambiguous.  Then every lane loads one rc dword per index, its own
-            // frame's for all-ones indices and one shared dword otherwise, so
-            // the loads need no branch and all are in flight before any is
-            // consumed
-            const uint32_t *vz = reinterpret_cast<const uint32_t *>(verd) + 2;
-            uint32_t rx[4][8], z[4][8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    rx[u][j] = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                    const uint64_t k = i + (uint64_t)u * E * 1024 + j;
-                    // (a load under `amb ?` became a branch with a full wait per
-                    // index: 51 vs 27 us at cfg4, profiles/r02ac)
-                    z[u][j] = vz[4 * (amb && rx[u][j] == 0xFFFFu ? k : b0)];
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (sizeof(T) == 2) {
+                    count(index_of(w[j] & 0xFFFFu));
+                    count(index_of(w[j] >> 16));
+                } else {
+                    count(w[j]);
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    count(rx[u][j] != 0xFFFFu
-                              ? rx[u][j]
-                              : ((amb && (int8_t)(z[u][j] >> 24) == RXG_RC_OK) ? 0xFFFFu : ~0u));
-        } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) count(v[u].x), count(v[u].y), count(v[u].z), count(v[u].w);
         }
     }
     for (; i < b1; i += (uint64_t)E * 1024)
-        for (uint64_t k = i; k < i + E && k < b1; ++k) count(index_of(cidx[k], k));
+        for (uint64_t k = i; k < i + E && k < b1; ++k) count(index_of(cidx[k]));
     if (mine) atomicAdd(&tally, mine);
     __syncthreads();
     uint32_t part = 0;
@@ -2122,7 +2116,7 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
     for (uint32_t k = tid; k < words; k += 1024) __builtin_nontemporal_store(wrapped ? 0u : bins[k], &dst[k]);
     if (wrapped)
         for (uint64_t k = b0 + tid; k < b1; k += 1024) {
-            const uint32_t f = index_of(cidx[k], k) - f0;
+            const uint32_t f = index_of(cidx[k]) - f0;
             if (f < lim) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
         }
 }
@@ -2258,18 +2252,18 @@ static bool use_slab(const rx_ft_dev &ft, bool counts) {
 // u16 count indices: the flows fit one range
 static bool cidx16(const rx_ft_dev &ft) { return ft.nu + ft.nt <= SLAB_MAX_FLOWS; }
 
-static hipError_t launch_count_slab(const void *cidx, const uint4 *verd, uint32_t n, const rx_ft_dev &ft,
+static hipError_t launch_count_slab(const void *cidx, uint32_t n, const rx_ft_dev &ft,
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
     slab_geometry(n, nr, &nslabs, &per);
     if (ft.cidx16)
         hipLaunchKernelGGL(rx_count_slab_kernel<uint16_t>, dim3(nslabs, nr), dim3(1024), 0, s,
-                           static_cast<const uint16_t *>(cidx), verd, ft.nu, n, per, words, nf,
+                           static_cast<const uint16_t *>(cidx), n, per, words, nf,
                            slab, counts);
     else
         hipLaunchKernelGGL(rx_count_slab_kernel<uint32_t>, dim3(nslabs, nr), dim3(1024), 0, s,
-                           static_cast<const uint32_t *>(cidx), verd, ft.nu, n, per, words, nf,
+                           static_cast<const uint32_t *>(cidx), n, per, words, nf,
                            slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -2457,6 +2451,7 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
     rx_ft_dev ft = ft_in;
     ft.count_idx = cidx;
     ft.cidx16 = slab && cidx16(ft_in) && !ft_in.count_4b;
+    ft.count_ffff = (ft.cidx16 && nflows == SLAB_MAX_FLOWS) ? counts + 0xFFFFu : nullptr;
     if (phase != RX_PH_COUNT) {
         unsigned long long *kcounts = slab ? nullptr : counts; // slab: counted after classify
         const uint32_t lds_bins = (kcounts && nflows > 0 && nflows <= 8192u) ? nflows : 0u;
@@ -2480,5 +2475,5 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
     if (!slab || phase == RX_PH_CLASSIFY) return hipSuccess;
     uint32_t *slabs = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + lists +
                                                    ws_cidx_bytes(n) * std::max(nbuf, 1u));
-    return launch_count_slab(cidx, out, n, ft, counts, slabs, s);
+    return launch_count_slab(cidx, n, ft, counts, slabs, s);
 }

@@ -31,7 +31,8 @@ struct rx_ft_dev {
     const uint32_t *listen; // 65536 entries
     uint32_t udp_mask, tcp_mask;   // slots - 1 (power of two)
     uint32_t udp_probe, tcp_probe; // longest probe sequence (slots) of any present key
-    uint32_t nu, nt;
+    uint32_t nu, nt;   // count layout: UDP ids [0, nu), then TCP ids at nu + id
+    uint32_t hseed;    // rx_hash3s seed of every hashed table (exact keys, compact UDP)
     // compact UDP table for small socket sets (null otherwise), copied into LDS
     // by the lane kernel: slot = {dip, dport | flow << 16}, empty = y ~0u
     const uint2 *udpc;
@@ -54,6 +55,13 @@ struct rx_ft_dev {
     // indices when cidx16 (at most 65535 flows: one slab range), u32 otherwise
     void *count_idx;
     uint32_t cidx16;
+    // 2-B indices with exactly 65536 flows: all ones would be both flow 65535
+    // and "not counted", so the classify kernel adds flow 65535's frames to
+    // this count itself (wave-aggregated atomics; its slab bin stays 0 and the
+    // reduce never writes it), and all ones always means "not counted" to the
+    // slab pass — which then never reads the verdicts (a later burst may be
+    // rewriting them on another stream).  Null otherwise.
+    unsigned long long *count_ffff;
     // rxg_tune_tables(RXG_TT_COUNT_4B): 4-B count indices whatever the flow
     // count (the round-1 count path, for A/B)
     uint32_t count_4b;
@@ -95,8 +103,10 @@ RX_HD bool rx_udp_port_decide(uint32_t e, uint32_t dip, uint32_t udp_dip, uint32
 // threads with their own contexts (and devices) never share mutable state.
 hipError_t rx_occupancy(const void *fn, uint32_t threads, size_t lds, int *cu, int *occ);
 
-RX_HD uint32_t rx_hash3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t h = 0x9E3779B9u ^ a;
+// seed: per context (rx_ft_dev::hseed, drawn at rxg_open), so the slot a key
+// lands in cannot be predicted from the key alone
+RX_HD uint32_t rx_hash3s(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t h = seed ^ a;
     h *= 0x85EBCA6Bu;
     h ^= h >> 15;
     h += b;

@@ -40,9 +40,12 @@ static int comm_error(ncclResult_t r, ncclComm_t comm, const char *what) {
 int rx_group_allreduce_u64(rxg_group *g, void *d, uint32_t n, hipStream_t s) {
     if (!g || (n && !d)) return RXG_EINVAL;
     if (n == 0) return RXG_OK;
-    int rc = rx_set_hip_error(hipSetDevice(g->device));
+    int prev = -1; // the caller's current device, restored on return
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    int rc = prev == g->device ? RXG_OK : rx_set_hip_error(hipSetDevice(g->device));
     if (rc) return rc;
     ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, g->comm, s);
+    if (prev >= 0 && prev != g->device) (void)hipSetDevice(prev);
     return r == ncclSuccess ? RXG_OK : comm_error(r, g->comm, "ncclAllReduce");
 }
 
@@ -64,8 +67,16 @@ int rxg_group_open(rxg_group **out, int device, uint32_t nranks, uint32_t rank,
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RXG_ENODEV;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     int rc = rx_set_hip_error(hipSetDevice(device));
     if (rc) return rc;
+    struct restore {
+        int d;
+        ~restore() {
+            if (d >= 0) (void)hipSetDevice(d);
+        }
+    } rs{prev};
     rxg_group *g = new (std::nothrow) rxg_group();
     if (!g) return RXG_ENOMEM;
     g->device = device;

@@ -97,6 +97,7 @@ struct localhost {
     struct localhost *prev, *next;
     pthread_cond_t cond;
     pthread_mutex_t mutex;
+    uint32_t flow_id; /* stable id in the GPU flow tables (verdict flow_id) */
 };
 
 struct offload {
@@ -122,6 +123,7 @@ struct tcp_stream {
     pthread_cond_t cond;
     pthread_mutex_t mutex;
     pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
+    uint32_t flow_id;           /* stable id in the GPU flow tables (verdict flow_id) */
 };
 
 struct tcp_fragment {
@@ -157,8 +159,8 @@ static struct tcp_stream *g_tcb_set;
 static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
 static rxg_ctx *g_ctx;
-static int g_dirty = 1;
-static uint64_t g_snap_gen; /* generation of the snapshot the flow ids refer to */
+static int g_dirty = 1;       /* the creation-order export (nstack_flows) is stale */
+static uint64_t g_snap_gen; /* bumped whenever a lookup result may change */
 static int g_burst_stale;   /* the burst's verdicts were made for an older snapshot */
 static uint64_t g_stat[5];
 static unsigned int g_isn_seed; /* tcp_stream_create seeds rand_r with time(NULL) (tcp.c:30-31) */
@@ -176,14 +178,21 @@ static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 
-/* snapshot: creation-order arrays given to rxg_flows_sync, and the blocks
- * their flow ids name */
-static rxg_udp_sock *s_udp;
+/* the control block of each stable flow id (NULL: free id).  Blocks are
+ * registered with the GPU flow tables as they are created, changed and freed
+ * (rxg_flows_add / update / remove: the incremental path, committed with the
+ * next burst), never by rebuilding the tables. */
 static struct localhost **s_udp_cb;
-static uint32_t s_nu, s_udp_cap;
-static rxg_tcb *s_tcb;
+static uint32_t s_udp_cap;
 static struct tcp_stream **s_tcb_cb;
-static uint32_t s_nt, s_tcb_cap;
+static uint32_t s_tcb_cap;
+/* export (nstack_flows / nstack_flow_ids): the lists in creation order */
+static rxg_udp_sock *s_udp;
+static uint32_t *s_udp_id;
+static uint32_t s_nu, s_udp_xcap;
+static rxg_tcb *s_tcb;
+static uint32_t *s_tcb_id;
+static uint32_t s_nt, s_tcb_xcap;
 static rxg_verdict *s_v;
 static uint32_t s_v_cap;
 
@@ -229,25 +238,25 @@ static int grow(void **p, uint32_t *cap, uint32_t need, size_t elem) {
     return 0;
 }
 
-/* rebuild the creation-order snapshot (g_lock held) */
+/* the creation-order export of the lists (g_lock held) */
 static int snapshot(void) {
     uint32_t nu = 0, nt = 0;
     struct localhost *h, *hlast = NULL;
     struct tcp_stream *s, *slast = NULL;
     for (h = g_pstHost; h; h = h->next) nu++, hlast = h;
     for (s = g_tcb_set; s; s = s->next) nt++, slast = s;
-    uint32_t cu = s_udp_cap, ct = s_tcb_cap;
-    if (grow((void **)&s_udp, &s_udp_cap, nu, sizeof(rxg_udp_sock))) return RXG_ENOMEM;
-    if (grow((void **)&s_udp_cb, &cu, nu, sizeof(void *))) return RXG_ENOMEM;
-    if (grow((void **)&s_tcb, &s_tcb_cap, nt, sizeof(rxg_tcb))) return RXG_ENOMEM;
-    if (grow((void **)&s_tcb_cb, &ct, nt, sizeof(void *))) return RXG_ENOMEM;
+    uint32_t cu = s_udp_xcap, ct = s_tcb_xcap;
+    if (grow((void **)&s_udp, &s_udp_xcap, nu, sizeof(rxg_udp_sock))) return RXG_ENOMEM;
+    if (grow((void **)&s_udp_id, &cu, nu, sizeof(uint32_t))) return RXG_ENOMEM;
+    if (grow((void **)&s_tcb, &s_tcb_xcap, nt, sizeof(rxg_tcb))) return RXG_ENOMEM;
+    if (grow((void **)&s_tcb_id, &ct, nt, sizeof(uint32_t))) return RXG_ENOMEM;
     uint32_t i = 0;
     for (h = hlast; h; h = h->prev, i++) { /* tail = oldest */
         s_udp[i].localip = h->localip;
         s_udp[i].localport = h->localport;
         s_udp[i].protocol = h->protocol;
         s_udp[i]._pad = 0;
-        s_udp_cb[i] = h;
+        s_udp_id[i] = h->flow_id;
     }
     i = 0;
     for (s = slast; s; s = s->prev, i++) {
@@ -256,14 +265,85 @@ static int snapshot(void) {
         s_tcb[i].sport = s->sport;
         s_tcb[i].dport = s->dport;
         s_tcb[i].status = (uint32_t)s->status;
-        s_tcb_cb[i] = s;
+        s_tcb_id[i] = s->flow_id;
     }
     s_nu = nu;
     s_nt = nt;
-    g_snap_gen++; /* flow ids of earlier snapshots may now name other blocks */
-    int rc = rxg_flows_sync(g_ctx, s_udp, nu, s_tcb, nt);
-    if (rc == RXG_OK) g_dirty = 0;
-    return rc;
+    g_dirty = 0;
+    return RXG_OK;
+}
+
+/* ---- registration with the GPU flow tables (g_lock held) ----------------- */
+static rxg_udp_sock udp_key(const struct localhost *h) {
+    rxg_udp_sock u;
+    u.localip = h->localip;
+    u.localport = h->localport;
+    u.protocol = h->protocol;
+    u._pad = 0;
+    return u;
+}
+static rxg_tcb tcb_key(const struct tcp_stream *s) {
+    rxg_tcb t;
+    t.sip = s->sip;
+    t.dip = s->dip;
+    t.sport = s->sport;
+    t.dport = s->dport;
+    t.status = (uint32_t)s->status;
+    return t;
+}
+static int reg_udp(struct localhost *h) { /* LL_ADD (common.c:302) */
+    const rxg_udp_sock u = udp_key(h);
+    uint32_t id;
+    int rc = rxg_flows_add(g_ctx, &u, 1, NULL, 0, &id, NULL);
+    if (rc < 0) return rc;
+    uint32_t cap = s_udp_cap;
+    if (grow((void **)&s_udp_cb, &s_udp_cap, id + 1, sizeof(void *))) return RXG_ENOMEM;
+    if (s_udp_cap > cap) memset(s_udp_cb + cap, 0, (s_udp_cap - cap) * sizeof(void *));
+    s_udp_cb[id] = h;
+    h->flow_id = id;
+    g_snap_gen++;
+    g_dirty = 1;
+    return RXG_OK;
+}
+static int reg_tcb(struct tcp_stream *s) { /* LL_ADD (tcp.c:52, common.c:336) */
+    const rxg_tcb t = tcb_key(s);
+    uint32_t id;
+    int rc = rxg_flows_add(g_ctx, NULL, 0, &t, 1, NULL, &id);
+    if (rc < 0) return rc;
+    uint32_t cap = s_tcb_cap;
+    if (grow((void **)&s_tcb_cb, &s_tcb_cap, id + 1, sizeof(void *))) return RXG_ENOMEM;
+    if (s_tcb_cap > cap) memset(s_tcb_cb + cap, 0, (s_tcb_cap - cap) * sizeof(void *));
+    s_tcb_cb[id] = s;
+    s->flow_id = id;
+    g_snap_gen++;
+    g_dirty = 1;
+    return RXG_OK;
+}
+static void unreg_udp(struct localhost *h) { /* LL_REMOVE (common.c:620) */
+    (void)rxg_flows_remove(g_ctx, &h->flow_id, 1, NULL, 0);
+    if (h->flow_id < s_udp_cap) s_udp_cb[h->flow_id] = NULL;
+    g_snap_gen++;
+    g_dirty = 1;
+}
+static void unreg_tcb(struct tcp_stream *s) { /* LL_REMOVE (tcp.c:321, common.c:660) */
+    (void)rxg_flows_remove(g_ctx, NULL, 0, &s->flow_id, 1);
+    if (s->flow_id < s_tcb_cap) s_tcb_cb[s->flow_id] = NULL;
+    g_snap_gen++;
+    g_dirty = 1;
+}
+static void rekey_udp(struct localhost *h) { /* nbind */
+    const rxg_udp_sock u = udp_key(h);
+    (void)rxg_flows_update_udp(g_ctx, h->flow_id, &u);
+    g_snap_gen++;
+    g_dirty = 1;
+}
+/* key or status of a tcb changed (nbind, nlisten, the state machine); only
+ * key and LISTEN changes move lookups (the library ignores the rest) */
+static void restate_tcb(struct tcp_stream *s, int lookup_moves) {
+    const rxg_tcb t = tcb_key(s);
+    (void)rxg_flows_update_tcb(g_ctx, s->flow_id, &t);
+    if (lookup_moves) g_snap_gen++;
+    g_dirty = 1;
 }
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -311,9 +391,11 @@ void nstack_fini(void) {
         free(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
-    free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v);
-    s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL;
-    s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = 0;
+    free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v), free(s_udp_id),
+        free(s_tcb_id);
+    s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL, s_udp_id = NULL,
+    s_tcb_id = NULL;
+    s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = s_udp_xcap = s_tcb_xcap = 0;
     memset(g_stat, 0, sizeof(g_stat));
     g_isn_seed = 0;
     while (g_arp) {
@@ -333,6 +415,10 @@ void nstack_fini(void) {
 int nsocket(int domain, int type, int protocol) {
     (void)domain, (void)protocol;
     pthread_mutex_lock(&g_lock);
+    if (!g_ctx) { /* nstack_init first: the blocks live in its flow tables */
+        pthread_mutex_unlock(&g_lock);
+        return -1;
+    }
     int fd = get_fd_frombitmap();
     if (fd < 0) {
         pthread_mutex_unlock(&g_lock);
@@ -353,6 +439,12 @@ int nsocket(int domain, int type, int protocol) {
         }
         pthread_cond_init(&h->cond, NULL);
         pthread_mutex_init(&h->mutex, NULL);
+        if (reg_udp(h)) {
+            ring_free(h->rcvbuf);
+            ring_free(h->sndbuf);
+            free(h);
+            goto fail;
+        }
         LL_ADD(h, g_pstHost);
     } else if (type == SOCK_STREAM) { /* :304-337 */
         struct tcp_stream *s = calloc(1, sizeof(*s));
@@ -370,9 +462,14 @@ int nsocket(int domain, int type, int protocol) {
         pthread_cond_init(&s->cond, NULL);
         pthread_cond_init(&s->accept_cond, NULL);
         pthread_mutex_init(&s->mutex, NULL);
+        if (reg_tcb(s)) {
+            ring_free(s->rcvbuf);
+            ring_free(s->sndbuf);
+            free(s);
+            goto fail;
+        }
         LL_ADD(s, g_tcb_set);
     }
-    g_dirty = 1;
     pthread_mutex_unlock(&g_lock);
     return fd;
 fail:
@@ -394,14 +491,15 @@ int nbind(int sockfd, const struct sockaddr *addr, socklen_t addrlen) { /* :342-
             h->localport = a->sin_port;
             memcpy(&h->localip, &a->sin_addr.s_addr, 4);
             memcpy(h->localmac, g_local_mac, 6);
+            rekey_udp(h);
         } else {
             struct tcp_stream *s = info;
             s->dport = a->sin_port;
             memcpy(&s->dip, &a->sin_addr.s_addr, 4);
             memcpy(s->localmac, g_local_mac, 6);
             s->status = TCP_STATUS_CLOSED;
+            restate_tcb(s, 1);
         }
-        g_dirty = 1;
         rc = 0;
     }
     pthread_mutex_unlock(&g_lock);
@@ -414,8 +512,10 @@ int nlisten(int sockfd, int backlog) { /* :373-386 */
     struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
     int rc = -1;
     if (s) {
-        if (s->protocol == IPPROTO_TCP) s->status = TCP_STATUS_LISTEN;
-        g_dirty = 1;
+        if (s->protocol == IPPROTO_TCP) {
+            s->status = TCP_STATUS_LISTEN;
+            restate_tcb(s, 1);
+        }
         rc = 0;
     }
     pthread_mutex_unlock(&g_lock);
@@ -605,6 +705,7 @@ int nclose(int fd) { /* :609-666 */
     }
     struct localhost *h = info;
     if (h->protocol == IPPROTO_UDP) {
+        unreg_udp(h);
         LL_REMOVE(h, g_pstHost);
         void *p;
         while (ring_dequeue(h->rcvbuf, &p) == 0) {
@@ -636,8 +737,10 @@ int nclose(int fd) { /* :609-666 */
                 pthread_mutex_unlock(&s->mutex);
             }
             s->status = TCP_STATUS_LAST_ACK;
+            restate_tcb(s, 0);
             set_fd_frombitmap(fd);
         } else {
+            unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
@@ -645,7 +748,6 @@ int nclose(int fd) { /* :609-666 */
             /* the reference leaves the listener's fd set in the bitmap here */
         }
     }
-    g_dirty = 1;
     pthread_mutex_unlock(&g_lock);
     return 0;
 }
@@ -772,18 +874,25 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
             struct tcp_stream *syn = tcb_new(cap >= 30 ? rd32(f + 26) : 0, cap >= 34 ? rd32(f + 30) : 0,
                                              sport, dport, TCP_STATUS_LISTEN);
             if (!syn) return;
+            /* registered as it ends this handler: SYN_RCVD (the LISTEN of
+             * tcp_stream_create is overwritten before any other lookup) */
+            syn->status = TCP_STATUS_SYN_RCVD;
+            if (reg_tcb(syn)) {
+                ring_free(syn->rcvbuf);
+                ring_free(syn->sndbuf);
+                free(syn);
+                return;
+            }
             LL_ADD(syn, g_tcb_set);
             g_burst_mutated = 1;
-            g_dirty = 1;
             syn->rcv_nxt = seq + 1;
             queue_ctl(syn, dport, sport, TCP_SYN | TCP_ACK);
-            syn->status = TCP_STATUS_SYN_RCVD;
         }
         break;
     case TCP_STATUS_SYN_RCVD: /* tcp_handle_syn_rcvd, tcp.c:89-131 */
         if (fl & TCP_ACK) {
             s->status = TCP_STATUS_ESTABLISHED; /* acknum == snd_nxt + 1 only printed */
-            g_dirty = 1;
+            restate_tcb(s, 0);
             wake_acceptors(s->dport);
         }
         break;
@@ -798,7 +907,7 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
         }
         if (fl & TCP_FIN) {
             s->status = TCP_STATUS_CLOSE_WAIT;
-            g_dirty = 1;
+            restate_tcb(s, 0);
             tcp_enqueue_rcv(s, f, cap, (cap > 46 ? f[46] : 0) >> 4); /* EOF marker */
             s->rcv_nxt = s->rcv_nxt + 1;
             s->snd_nxt = ack;
@@ -809,6 +918,7 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
     case TCP_STATUS_LAST_ACK: /* tcp_handle_last_ack, tcp.c:312-331 */
         if (fl & TCP_ACK) {
             s->status = TCP_STATUS_CLOSED;
+            unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
             void *p;
             while (ring_dequeue(s->rcvbuf, &p) == 0) {
@@ -823,7 +933,6 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
             ring_free(s->sndbuf);
             free(s);
             g_burst_mutated = 1;
-            g_dirty = 1;
         }
         break;
     default: /* CLOSED, SYN_SENT, FIN_WAIT_*, CLOSING, TIME_WAIT, CLOSE_WAIT: no-ops */
@@ -846,7 +955,7 @@ static int deliver_tcp(const rxg_mbuf *m, const rxg_verdict *v) {
         s = tcb_search(cap >= 30 ? rd32(f + 26) : 0, cap >= 34 ? rd32(f + 30) : 0,
                        cap >= 36 ? rd16(f + 34) : 0, cap >= 38 ? rd16(f + 36) : 0);
     else
-        s = (v->rc == RXG_RC_OK && v->flow_id < s_nt) ? s_tcb_cb[v->flow_id] : NULL;
+        s = (v->rc == RXG_RC_OK && v->flow_id < s_tcb_cap) ? s_tcb_cb[v->flow_id] : NULL;
     if (!s) return RXG_RC_TCP_NO_TCB;
     g_stat[2]++;
     tcp_dispatch(s, f, cap);
@@ -878,7 +987,7 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v, int *rc) {
                  : ((v->flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
         if (*rc != RXG_RC_OK) return 0;
     } else {
-        if (v->rc != RXG_RC_OK || v->flow_id >= s_nu) return 0;
+        if (v->rc != RXG_RC_OK || v->flow_id >= s_udp_cap || !s_udp_cb[v->flow_id]) return 0;
         h = s_udp_cb[v->flow_id];
     }
     struct offload *o = calloc(1, sizeof(*o));
@@ -960,10 +1069,9 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
     if (!m || !v) return n ? RXG_EINVAL : 0;
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
-    if (rc == RXG_OK && g_dirty) rc = snapshot();
     int delivered = 0;
     if (rc == RXG_OK) {
-        g_burst_stale = gen != g_snap_gen; /* classified against another snapshot */
+        g_burst_stale = gen != g_snap_gen; /* classified against other lists */
         delivered = deliver_burst(m, n, v, rc_out);
     }
     pthread_mutex_unlock(&g_lock);
@@ -974,7 +1082,6 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     if (!m && n) return RXG_EINVAL;
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
-    if (rc == RXG_OK && g_dirty) rc = snapshot();
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
     if (rc == RXG_OK) rc = rxg_process_mbufs(g_ctx, m, n, s_v);
@@ -1035,13 +1142,19 @@ uint32_t nstack_tcb_count(void) {
 
 int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status) {
     pthread_mutex_lock(&g_lock);
-    struct tcp_stream *s = tcb_new(sip, dip, sport, dport, status);
+    struct tcp_stream *s = g_ctx ? tcb_new(sip, dip, sport, dport, status) : NULL;
     if (!s) {
         pthread_mutex_unlock(&g_lock);
         return -1;
     }
+    if (reg_tcb(s)) {
+        ring_free(s->rcvbuf);
+        ring_free(s->sndbuf);
+        free(s);
+        pthread_mutex_unlock(&g_lock);
+        return -1;
+    }
     LL_ADD(s, g_tcb_set); /* tcp.c:52 */
-    g_dirty = 1;
     wake_acceptors(dport);
     pthread_mutex_unlock(&g_lock);
     return 0;
@@ -1058,6 +1171,18 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
         if (gen) *gen = g_snap_gen;
         if (u) memcpy(u, s_udp, (size_t)(s_nu < cap_u ? s_nu : cap_u) * sizeof(*u));
         if (t) memcpy(t, s_tcb, (size_t)(s_nt < cap_t ? s_nt : cap_t) * sizeof(*t));
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t) {
+    pthread_mutex_lock(&g_lock);
+    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    if (rc == RXG_OK && g_dirty) rc = snapshot();
+    if (rc == RXG_OK) {
+        if (uid) memcpy(uid, s_udp_id, (size_t)(s_nu < cap_u ? s_nu : cap_u) * sizeof(*uid));
+        if (tid) memcpy(tid, s_tcb_id, (size_t)(s_nt < cap_t ? s_nt : cap_t) * sizeof(*tid));
     }
     pthread_mutex_unlock(&g_lock);
     return rc;

@@ -115,6 +115,13 @@ _close = _sig("rxg_close", None, _vp)
 _strerror = _sig("rxg_strerror", C.c_char_p, _i32)
 _last_hip = _sig("rxg_last_hip_error", C.c_char_p)
 _flows_sync = _sig("rxg_flows_sync", _i32, _vp, _vp, _u32, _vp, _u32)
+_flows_add = _sig("rxg_flows_add", _i32, _vp, _vp, _u32, _vp, _u32, _vp, _vp)
+_flows_remove = _sig("rxg_flows_remove", _i32, _vp, _vp, _u32, _vp, _u32)
+_flows_update_udp = _sig("rxg_flows_update_udp", _i32, _vp, _u32, _vp)
+_flows_update_tcb = _sig("rxg_flows_update_tcb", _i32, _vp, _u32, _vp)
+_flows_commit = _sig("rxg_flows_commit", _i32, _vp, _vp)
+_num_udp_ids = _sig("rxg_num_udp_ids", _u32, _vp)
+_flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
                         _vp, _vp)
@@ -131,6 +138,7 @@ _tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
 _tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
 TT_NO_UDP_PORT = 0x1
 TT_COUNT_4B = 0x2
+TT_NO_TRACK = 0x4
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
@@ -164,6 +172,8 @@ MAX_SHARDS = 64
 GROUP_ID_BYTES = 128
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
+            "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
+            "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
@@ -242,6 +252,45 @@ class Context:
         _check(_flows_sync(self._h, _ptr(udp) if len(udp) else None, len(udp),
                            _ptr(tcb) if len(tcb) else None, len(tcb)), "rxg_flows_sync")
         self.nu, self.nt = len(udp), len(tcb)
+
+    def flows_add(self, udp: np.ndarray | None = None, tcb: np.ndarray | None = None):
+        """add control blocks as the newest ones (rxg_flows_add); returns
+        (udp_ids, tcp_ids, count_layout_moved)"""
+        udp = np.ascontiguousarray(udp if udp is not None else np.zeros(0, UDP_SOCK_DTYPE),
+                                   UDP_SOCK_DTYPE)
+        tcb = np.ascontiguousarray(tcb if tcb is not None else np.zeros(0, TCB_DTYPE), TCB_DTYPE)
+        uid = np.zeros(max(len(udp), 1), np.uint32)
+        tid = np.zeros(max(len(tcb), 1), np.uint32)
+        rc = _flows_add(self._h, _ptr(udp) if len(udp) else None, len(udp),
+                        _ptr(tcb) if len(tcb) else None, len(tcb), _ptr(uid), _ptr(tid))
+        if rc < 0:
+            _check(rc, "rxg_flows_add")
+        return uid[:len(udp)], tid[:len(tcb)], rc == 1
+
+    def flows_remove(self, udp_ids=None, tcp_ids=None):
+        u = np.ascontiguousarray(udp_ids if udp_ids is not None else [], np.uint32)
+        t = np.ascontiguousarray(tcp_ids if tcp_ids is not None else [], np.uint32)
+        _check(_flows_remove(self._h, _ptr(u) if len(u) else None, len(u),
+                             _ptr(t) if len(t) else None, len(t)), "rxg_flows_remove")
+
+    def flows_update_udp(self, fid: int, sock):
+        a = np.ascontiguousarray(np.asarray(sock, UDP_SOCK_DTYPE).reshape(1))
+        _check(_flows_update_udp(self._h, fid, _ptr(a)), "rxg_flows_update_udp")
+
+    def flows_update_tcb(self, fid: int, tcb):
+        a = np.ascontiguousarray(np.asarray(tcb, TCB_DTYPE).reshape(1))
+        _check(_flows_update_tcb(self._h, fid, _ptr(a)), "rxg_flows_update_tcb")
+
+    def flows_commit(self, stream=None):
+        _check(_flows_commit(self._h, stream), "rxg_flows_commit")
+
+    @property
+    def num_udp_ids(self) -> int:
+        return _num_udp_ids(self._h)
+
+    @property
+    def flows_rebuilds(self) -> int:
+        return _flows_rebuilds(self._h)
 
     def tune(self, lanes_per_frame: int = 0, passes: int = 0, frames_per_group: int = 0,
              pipeline: int = 0xFFFFFFFF):
@@ -544,6 +593,7 @@ class NStack:
                    ("nstack_deliver", _i32, [_vp, _u32, _vp, _u64, _vp]),
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
+                   ("nstack_flow_ids", _i32, [_vp, _u32, _vp, _u32]),
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
                    ("nstack_tcb_count", _u32, []),
@@ -606,8 +656,26 @@ class NStack:
         return self.lib.nstack_tcb_add(ip_raw(sip), ip_raw(dip), port_raw(sport),
                                        port_raw(dport), status)
 
+    def flow_ids(self):
+        """(udp_ids, tcp_ids): the stable flow id of each block of flows()"""
+        u, t = self.flows()
+        uid = np.zeros(max(len(u), 1), np.uint32)
+        tid = np.zeros(max(len(t), 1), np.uint32)
+        _check(self.lib.nstack_flow_ids(_ptr(uid), len(u), _ptr(tid), len(t)), "nstack_flow_ids")
+        return uid[:len(u)], tid[:len(t)]
+
+    def to_ids(self, v: np.ndarray) -> np.ndarray:
+        """verdicts made against flows()'s arrays (creation-order indices, e.g. by
+        the oracle) with their flow ids turned into the blocks' stable ids"""
+        uid, tid = self.flow_ids()
+        v = np.array(v, VERDICT_DTYPE, copy=True)
+        for cls, ids in ((CLS_UDP, uid), (CLS_TCP, tid)):
+            m = (v["cls"] == cls) & (v["flow_id"] != FLOW_NONE)
+            v["flow_id"][m] = ids[v["flow_id"][m]]
+        return v
+
     def flows(self, with_gen: bool = False):
-        """the snapshot lists (and, with_gen, their generation for deliver)"""
+        """the lists in creation order (and, with_gen, their generation for deliver)"""
         nu, nt, gen = C.c_uint32(), C.c_uint32(), _u64()
         _check(self.lib.nstack_flows(None, 0, C.byref(nu), None, 0, C.byref(nt), None),
                "nstack_flows")
@@ -650,12 +718,14 @@ class NStack:
         arr = (C.POINTER(Mbuf) * len(ms))(*[C.pointer(m) for m in ms])
         return arr, (bufs, ms)
 
+    STALE = 0xFFFFFFFFFFFFFFFF  # a generation no list state has: re-look every frame up
+
     def deliver(self, frames: list[bytes], verdicts: np.ndarray, rcs: np.ndarray | None = None,
-                gen: int | None = None) -> int:
-        """apply verdicts made for the snapshot of generation `gen` (None = the
-        current one); rcs (int32[n], optional) receives the per-frame return codes"""
-        if gen is None:
-            gen = self.flows(with_gen=True)[2]
+                gen: int = STALE) -> int:
+        """apply verdicts (flow ids = stable ids, see to_ids) made against the
+        lists of generation `gen`; the default trusts no flow id and looks every
+        frame up again on the live lists.  rcs (int32[n], optional) receives the
+        per-frame return codes"""
         arr, keep = self.mbufs(frames)
         verdicts = np.ascontiguousarray(verdicts, VERDICT_DTYPE)
         r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts), gen, _ptr(rcs))

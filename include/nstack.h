@@ -72,12 +72,13 @@ int nclose(int fd);
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 
 /* Delivery half only: apply verdicts computed by rxg_* to the frames (UDP ->
- * socket receive rings, TCP -> state machine).  `gen` = the snapshot
- * generation nstack_flows returned with the lists the verdicts were
- * classified against: if the lists changed since (a socket or tcb closed,
- * which renumbers later blocks), every frame of the burst is looked up again
- * on the live lists, as the reference's per-frame lookups would, instead of
- * trusting stale flow ids.  rc_out (nullable) as for nstack_rx_burst. */
+ * socket receive rings, TCP -> state machine).  Verdict flow ids are the
+ * blocks' stable ids (nstack_flow_ids).  `gen` = the generation nstack_flows
+ * returned with the lists the verdicts were classified against: if the lists
+ * changed since (a block created, rebound, made a listener or freed — a freed
+ * id may be reused), every frame of the burst is looked up again on the live
+ * lists, as the reference's per-frame lookups would, instead of trusting the
+ * flow ids.  rc_out (nullable) as for nstack_rx_burst. */
 int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
                    int *rc_out);
 
@@ -85,11 +86,18 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
  * wake a blocked naccept (tcp.c:108-116).  All values raw network order. */
 int nstack_tcb_add(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int status);
 
-/* The current control-block snapshot in creation order (what rxg_flows_sync
- * receives) and its generation (nullable; for nstack_deliver).  Counts are
- * always written; arrays up to their capacities. */
+/* The control blocks in creation order (the lists rxg_flows_sync would
+ * take) and the generation of the lists (nullable; for nstack_deliver).
+ * Counts are always written; arrays up to their capacities.  Every block is
+ * registered with the context's GPU flow tables as it is created, bound,
+ * made a listener and freed (nsocket / nbind / nlisten / SYN / last ACK /
+ * nclose: rxg_flows_add / update / remove, committed with the next burst), so
+ * no burst ever waits for a table rebuild. */
 int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint32_t cap_t,
                  uint32_t *nt, uint64_t *gen);
+/* The stable flow id (verdict flow_id, count index) of each block of the
+ * nstack_flows arrays, in the same order. */
+int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t);
 
 /* Diagnostics (tests): the tcb with this exact 4-tuple (raw network order):
  * status, rcv_nxt, snd_nxt, fd; and the k-th fragment queued in its send

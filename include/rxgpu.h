@@ -18,6 +18,8 @@
  * checksum).  Plain pointers and sizes only; no C++ or torch types.
  *
  * Threading: one rxg_ctx per rx thread; a context is not thread-safe.
+ * Every call that touches the device switches the calling thread to the
+ * context's device and back: the thread's current device is unchanged.
  * Errors: API calls return 0 or a negative RXG_E* code (rxg_strerror);
  * the library never exits the process (the reference rte_exit()s).
  */
@@ -142,10 +144,53 @@ const char *rxg_last_hip_error(void);
 /* Mirror of the reference's control-block lists, given in CREATION order
  * (oldest first = the reverse of the head-inserted list, common.h:43-49), so
  * that on duplicate keys the highest index (the newest block) wins exactly as
- * the reference's first-match list scan does.  Builds the device flow table
- * (bucketised hash for exact keys, direct port table for listeners). */
+ * the reference's first-match list scan does.  Builds the device flow tables
+ * (linear-probed exact keys under the context's random hash seed, direct
+ * port tables for listeners and UDP sockets).  Blocking: waits for this
+ * context's own bursts still reading the old tables (never for other work on
+ * the device), uploads, and returns with the tables in place. */
 int rxg_flows_sync(rxg_ctx *ctx, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t,
                    uint32_t nt);
+
+/* Incremental control-block changes, between bursts.  The reference creates
+ * a tcb on every SYN (tcp_stream_create + LL_ADD, tcp.c:3-52), creates and
+ * binds sockets (nsocket / nbind / nlisten, common.c:262-386) and frees
+ * blocks on the last ACK and on close (tcp.c:321, common.c:620,660); these
+ * calls mirror exactly that on the context's tables in O(1) host work each,
+ * instead of a rebuild through rxg_flows_sync.
+ *
+ * Flow ids are stable: rxg_flows_sync gives block i of its arrays id i; an
+ * added block gets a free id (freed ids are reused, else the id space grows)
+ * and keeps it until removed.  Verdicts name blocks by these ids, and the
+ * per-flow counts are laid out as UDP ids [0, rxg_num_udp_ids()) followed by
+ * TCP ids (count index rxg_num_udp_ids() + id); rxg_num_flows() = the length.
+ * An added block is the NEWEST (it wins duplicate keys, as LL_ADD's head
+ * insert makes it); an update keeps the block's creation order (nbind and
+ * nlisten do not move a block in the list) and changes its key and/or
+ * status; removing the newest of a duplicate key exposes the next older one.
+ *
+ * Changes are host-side until committed: rxg_flows_commit(stream), or
+ * implicitly by the next burst call, on that burst's stream.  A commit writes
+ * only the changed table slots (a small kernel on `stream`), ordered after
+ * every earlier burst of this context on any stream and before every later
+ * one: it never synchronises the device or the host (a table past load 1/2,
+ * or a probe sequence past the cap, is rebuilt whole: that commit waits for
+ * its host-to-device copies).
+ *
+ * rxg_flows_add returns 1 (not an error) when it grew the UDP id space, i.e.
+ * moved the TCP count indices: callers keeping their own d_counts vectors
+ * re-size them to rxg_num_flows(); the context's own counts move by themselves. */
+int rxg_flows_add(rxg_ctx *ctx, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb *t, uint32_t nt,
+                  uint32_t *udp_ids, uint32_t *tcp_ids);
+int rxg_flows_remove(rxg_ctx *ctx, const uint32_t *udp_ids, uint32_t nu, const uint32_t *tcp_ids,
+                     uint32_t nt);
+int rxg_flows_update_udp(rxg_ctx *ctx, uint32_t id, const rxg_udp_sock *u);
+int rxg_flows_update_tcb(rxg_ctx *ctx, uint32_t id, const rxg_tcb *t);
+int rxg_flows_commit(rxg_ctx *ctx, void *stream);
+/* UDP part of the count layout (see above) */
+uint32_t rxg_num_udp_ids(const rxg_ctx *ctx);
+/* whole-table rebuilds so far (growth, reseeds): diagnostics */
+uint32_t rxg_flows_rebuilds(const rxg_ctx *ctx);
 
 /* Device-resident burst: all pointers are device pointers.  Frame i starts at
  * d_pkts + (d_off[i] << off_unit_log2) (off_unit_log2 >= 4: 16-byte aligned
@@ -252,6 +297,9 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
  * <= 65536 flows.  Verdicts and counts depend on neither. */
 #define RXG_TT_NO_UDP_PORT 0x1u
 #define RXG_TT_COUNT_4B 0x2u
+/* A/B only, unsafe: no per-burst tracking event (table commits and
+ * rxg_flows_sync are then no longer ordered after bursts on other streams) */
+#define RXG_TT_NO_TRACK 0x4u
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
@@ -319,7 +367,10 @@ void rxg_group_close(rxg_group *g);
  * `stream` (every rank must call it with the same n). */
 int rxg_counts_allreduce(rxg_group *g, uint64_t *d_counts, uint32_t n, void *stream);
 /* The same for the context-owned counts (rxg_classify / rxg_process_mbufs),
- * after every burst submitted so far; synchronous. */
+ * after every burst submitted so far; synchronous.  Only the increment since
+ * the previous call is reduced and then added to the running total, so the
+ * context's counts (rxg_flow_counts) are the global totals after each call,
+ * however often it is called. */
 int rxg_ctx_counts_allreduce(rxg_ctx *ctx, rxg_group *g);
 
 /* ---- pcap ingest (the NIC stand-in: rte_eth_rx_burst into the in-ring,

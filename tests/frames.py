@@ -129,3 +129,37 @@ def read_pcap(path: str) -> list[bytes]:
         out.append(data[pos:pos + incl])
         pos += incl
     return out
+
+
+# ---- vectorized builders (many frames at once, numpy) ----------------------
+def tcp64_frames(sip, dip, sport, dport, seq=1000) -> np.ndarray:
+    """n x 64-B TCP/IPv4 frames (PSH|ACK, 10 payload bytes) for raw
+    network-order (sip, dip, sport, dport) arrays, L4 checksum as
+    rte_ipv4_udptcp_cksum computes it (tl = 50, L4 = bytes [34, 64))"""
+    n = len(sip)
+    f = np.zeros((n, 64), np.uint8)
+    f[:, 0:6] = np.frombuffer(LOCAL_MAC, np.uint8)
+    f[:, 6:12] = np.frombuffer(PEER_MAC, np.uint8)
+    f[:, 12:14] = (0x08, 0x00)
+    f[:, 14:24] = np.frombuffer(bytes([0x45, 0, 0, 50, 0, 1, 0x40, 0, 64, 6]), np.uint8)
+    f32 = f
+    f32[:, 26:30] = np.asarray(sip, np.uint32).view(np.uint8).reshape(n, 4)
+    f32[:, 30:34] = np.asarray(dip, np.uint32).view(np.uint8).reshape(n, 4)
+    f32[:, 34:36] = np.asarray(sport, np.uint16).view(np.uint8).reshape(n, 2)
+    f32[:, 36:38] = np.asarray(dport, np.uint16).view(np.uint8).reshape(n, 2)
+    f32[:, 38:42] = np.frombuffer(struct.pack(">I", seq), np.uint8)
+    f32[:, 46] = 0x50
+    f32[:, 47] = 0x18
+    f32[:, 48:50] = (0x39, 0x08)
+    f32[:, 54:64] = np.arange(10, dtype=np.uint8)
+    ip = f32[:, 14:34].copy().view("<u2").astype(np.uint64)
+    s = ip.sum(axis=1)
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    f32[:, 24:26] = ((~s) & 0xFFFF).astype("<u2").view(np.uint8).reshape(n, 2)
+    wd = f32.view("<u2").astype(np.uint64)  # 32 LE words; L4 = words 17..31, field = word 25
+    s = wd[:, 13:17].sum(axis=1) + wd[:, 17:32].sum(axis=1) - wd[:, 25] + 0x0600 + 0x1E00
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    f32[:, 50:52] = ((~s) & 0xFFFF).astype("<u2").view(np.uint8).reshape(n, 2)
+    return f

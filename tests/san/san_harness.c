@@ -216,6 +216,11 @@ static void deliver(burst *b, int *rc) {
     rxg_verdict v[64];
     oracle_classify(tb, b->buf, b->off, b->len, b->n, 6, v, NULL);
     oracle_tables_free(tb);
+    uint32_t uid[64], tid[64]; /* oracle index (creation order) -> stable flow id */
+    CHECK(nstack_flow_ids(uid, 64, tid, 64) == RXG_OK);
+    for (uint32_t i = 0; i < b->n; ++i)
+        if (v[i].flow_id != RXG_FLOW_NONE)
+            v[i].flow_id = v[i].cls == RXG_CLS_TCP ? tid[v[i].flow_id] : uid[v[i].flow_id];
     rxg_mbuf mb[64], *mp[64];
     memset(mb, 0, sizeof mb);
     for (uint32_t i = 0; i < b->n; ++i) {

@@ -156,7 +156,7 @@ class Pair:
         else:
             u, t, gen = self.ns.flows(with_gen=True)
             buf, off, lens = F.pack_frames(frames)
-            v = O.Tables(u, t).classify(buf, off, lens, 6)
+            v = self.ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))
             self.ns.deliver(frames, v, rcs, gen)
         assert list(rcs) == want, (list(rcs), want)
 
@@ -273,7 +273,7 @@ def test_stale_verdicts_after_close(ns_host):
               for port in (1001, 1002, 1000)]
     u, t, gen = ns.flows(with_gen=True)
     buf, off, lens = F.pack_frames(frames)
-    v = O.Tables(u, t).classify(buf, off, lens, 6)   # flow ids 1, 2, 0
+    v = ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))   # flow ids 1, 2, 0
     assert list(v["flow_id"]) == [1, 2, 0]
     assert ns.close(fds[0]) == os_.close(fds[0]) == 0  # 1001 -> id 0, 1002 -> id 1
     rcs = np.zeros(3, np.int32)

@@ -22,9 +22,10 @@ def ns():
 
 
 def _verdicts(ns, frames):
+    """oracle verdicts against the stack's lists, flow ids as stable ids"""
     u, t = ns.flows()
     buf, off, lens = F.pack_frames(frames)
-    return O.Tables(u, t).classify(buf, off, lens, 6)
+    return ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))
 
 
 def test_udp_echo_slice(ns):
