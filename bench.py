@@ -667,6 +667,114 @@ def run_cfg1(local, dev, steps, warmup, budget_s, cores):
     return res
 
 
+SOCK_CASES = {
+    # BASELINE configs[1]: 1024 UDP sockets bound to :20000-21023, 64-B datagrams
+    "cfg2": dict(burst=32768, bursts=30),
+    # BASELINE configs[2]: 4096 connections to the listener on :9999 (each
+    # established by a SYN / ACK exchange through the stack), 1500-B segments
+    "cfg3": dict(burst=16384, bursts=20),
+}
+
+
+def socket_api(local, name, budget_s, cores, with_cpu=True):
+    """The kept socket API's rate: bursts through
+    nstack_rx_burst — GPU classify (rxg_process_mbufs: staging, PCIe, K1) then
+    host delivery into the sockets' receive rings with the reference's
+    offload / tcp_fragment semantics (udp.c:25-52, tcp.c:133-185) — and the
+    application reading every socket (nrecvfrom / nrecv, common.c:462-565).
+    CPU baseline: oracle/ref_stack.c, the reference's per-frame
+    udp_process / tcp_process and socket calls, over the same frames."""
+    import ctypes as C
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name)
+    ul = w["unit_log2"]
+    sc = SOCK_CASES[name]
+    B, K = sc["burst"], sc["bursts"]
+    udp, tcb = R.gen_flows(cfg)
+    L = "192.168.100.77"
+    ns = R.NStack(local, max_burst=B, max_bytes=B * cfg.slot_bytes + 4096)
+    res = dict(workload=name, frames_per_burst=B)
+    try:
+        setup = []  # (frames for the handshake), applied to both stacks
+        if name == "cfg2":
+            for u in udp:
+                fd = ns.socket(R.SOCK_DGRAM)
+                ns.bind(fd, L, int.from_bytes(int(u["localport"]).to_bytes(2, "little"), "big"))
+        else:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import frames as F  # test infrastructure: the handshake frames
+            lfd = ns.socket(R.SOCK_STREAM)
+            ns.bind(lfd, L, 9999)
+            ns.listen(lfd)
+            for t in tcb[1:]:
+                sip = ".".join(str(b) for b in int(t["sip"]).to_bytes(4, "little"))
+                sp = int.from_bytes(int(t["sport"]).to_bytes(2, "little"), "big")
+                setup.append((F.tcp_frame(sip, sp, L, 9999, b"", flags=0x02, seq=1),
+                              F.tcp_frame(sip, sp, L, 9999, b"", flags=0x10, seq=2)))
+            for k in (0, 1):
+                for j in range(0, len(setup), 4096):
+                    fr = [s[k] for s in setup[j:j + 4096]]
+                    ns.rx_burst(fr)
+            res["established"] = int(ns.tcb_count()) - 1
+        pk, off, ln = R.gen_host(cfg, 0, B, ul)
+        arr, keep = R.NStack.mbufs_over(pk, off, ln, ul)
+        rbuf = np.zeros(65536, np.uint8)
+        ns.rx_burst_mbufs(arr, B)  # warm (staging, tables committed)
+        ns.drain_all(rbuf)
+        t_rx = t_dr = 0.0
+        items = nbytes = delivered = 0
+        for _ in range(K):
+            t0 = time.perf_counter()
+            delivered += ns.rx_burst_mbufs(arr, B)
+            t1 = time.perf_counter()
+            g, nb = ns.drain_all(rbuf)
+            t2 = time.perf_counter()
+            t_rx += t1 - t0
+            t_dr += t2 - t1
+            items += g
+            nbytes += nb
+        frame_bytes = int(ln.astype(np.int64).sum())
+        res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
+                   rx_burst_ms=round(t_rx / K * 1e3, 3), app_recv_ms=round(t_dr / K * 1e3, 3),
+                   rx_burst_mpps=round(B * K / t_rx / 1e6, 3),
+                   payload_gb_per_s=round(nbytes / (t_rx + t_dr) / 1e9, 3),
+                   frame_gb_per_s=round(frame_bytes * K / (t_rx + t_dr) / 1e9, 3),
+                   received_per_burst=items // K, udp_delivered_per_burst=delivered // K,
+                   dropped=int(ns.stat(1)))
+    finally:
+        ns.fini()
+    if with_cpu:  # the reference's path on one core: oracle/ref_stack.c
+        O = _oracle()
+        st = O.Stack()
+        if name == "cfg2":
+            for u in udp:
+                fd = st.socket(2)
+                st.bind(fd, int(u["localip"]), int(u["localport"]))
+        else:
+            fd = st.socket(1)
+            st.bind(fd, R.ip_raw(L), R.port_raw(9999))
+            st.listen(fd)
+            for k in (0, 1):
+                for s in setup:
+                    st.rx(s[k])
+        rbuf = np.zeros(65536, np.uint8)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            st.rx_burst(pk, off, ln, ul)
+            st.drain_all(rbuf)
+            done += B
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = dict(mpps=round(done / el / 1e6, 3), unit="Mpps", cores=1,
+                                   kind="port", frames=done, seconds=round(el, 2),
+                                   sample=f"the same {B}-frame burst, cycled: oracle/ref_stack.c "
+                                          f"oracle_rx per frame + every socket read; host "
+                                          f"{cores['model']}")
+        res["vs_cpu"] = round(res["mpps"] / max(res["cpu_baseline"]["mpps"], 1e-9), 2)
+    del keep
+    return res
+
+
 def hbm_copy_peak(dev, nbytes=4 << 30, reps=10):
     """device-to-device copy rate on this box (read + write bytes / s): the
     measured ceiling beside the 8 TB/s spec"""
@@ -869,6 +977,8 @@ def main():
     ap.add_argument("--backend", default="gloo", help="torch.distributed backend of the control "
                     "plane (rendezvous, barriers, max-over-ranks timing)")
     ap.add_argument("--e2e", action="store_true", help="also measure the PCIe-inclusive rate")
+    ap.add_argument("--no-sockrate", action="store_true",
+                    help="skip the socket-API rate (nstack_rx_burst + nrecvfrom/nrecv)")
     ap.add_argument("--sweep-variants", default="", help="';'-separated g,p,fpg,pipe list")
     ap.add_argument("--ramp-ms", type=float, default=200.0,
                     help="untimed clock ramp per workload before the warmup steps (ms of wall time)")
@@ -962,6 +1072,16 @@ def main():
     if rank == 0 and world == 1 and not a.no_cfg1:
         cfg1 = run_cfg1(local, dev, a.steps, a.warmup, 0 if a.no_cpu else a.cpu_budget / 2, cores)
         log("cfg1", json.dumps(cfg1))
+    sock = {}
+    if rank == 0 and world == 1 and not a.no_sockrate:
+        for nm in ("cfg2", "cfg3"):
+            try:
+                sock[nm] = socket_api(local, nm, 0 if a.no_cpu else a.cpu_budget / 2, cores,
+                                      with_cpu=not a.no_cpu)
+                log("socket_api", json.dumps(sock[nm]))
+            except Exception as e:  # reported in the line, never silent
+                sock[nm] = dict(error=repr(e))
+                log(f"socket_api {nm} failed: {e!r}")
     copy_peak = hbm_copy_peak(dev) if rank == 0 and world == 1 else None
 
     if a.e2e and rank == 0:
@@ -1017,6 +1137,8 @@ def main():
             line["pcie_peaks"] = head["pcie_peaks"]
         if cfg1:
             line["cfg1"] = cfg1
+        if sock:
+            line["socket_api"] = sock
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}

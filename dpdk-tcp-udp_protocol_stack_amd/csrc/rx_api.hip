@@ -40,6 +40,11 @@ hipError_t rx_gather_launch(const uint8_t *pkts, const uint32_t *off, const uint
                             uint64_t cap, uint32_t *dst_off, uint16_t *dst_len, void *ws,
                             hipStream_t s);
 int rx_group_allreduce_u64(rxg_group *g, void *d, uint32_t n, hipStream_t s);
+size_t rx_compact_ws_bytes(uint32_t n, uint32_t nflows);
+hipError_t rx_compact_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                             uint32_t n, uint32_t unit_log2, const uint4 *verd, uint32_t nflows,
+                             rxg_dgram *dg, uint32_t *first, uint8_t *payload, uint64_t cap,
+                             uint32_t *totals, void *ws, hipStream_t s);
 
 static thread_local std::string g_last_hip;
 
@@ -211,6 +216,14 @@ struct rxg_ctx {
         uint64_t ticket = 0;          // last burst submitted to this slot (0 = none)
     } slots[RXG_PIPE_DEPTH];
     uint64_t next_ticket = 1;
+    // UDP compaction results of the host-buffer path (rxg_process_mbufs_udp):
+    // device buffers and their pinned host copies, sized by max_pkts / max_bytes
+    rxg_dgram *d_cp_dg = nullptr, *h_cp_dg = nullptr;
+    uint32_t *d_cp_first = nullptr, *h_cp_first = nullptr;
+    uint8_t *d_cp_payload = nullptr, *h_cp_payload = nullptr;
+    uint32_t *d_cp_totals = nullptr, *h_cp_totals = nullptr;
+    void *d_cp_ws = nullptr;
+    size_t d_cp_ws_cap = 0;
 };
 
 static int ensure_dev(void **p, size_t *cap, size_t bytes) {
@@ -609,6 +622,15 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_counts_base);
     (void)hipFree(c->d_ws);
     (void)hipFree(c->d_aux);
+    (void)hipFree(c->d_cp_dg);
+    (void)hipFree(c->d_cp_first);
+    (void)hipFree(c->d_cp_payload);
+    (void)hipFree(c->d_cp_totals);
+    (void)hipFree(c->d_cp_ws);
+    if (c->h_cp_dg) (void)hipHostFree(c->h_cp_dg);
+    if (c->h_cp_first) (void)hipHostFree(c->h_cp_first);
+    if (c->h_cp_payload) (void)hipHostFree(c->h_cp_payload);
+    if (c->h_cp_totals) (void)hipHostFree(c->h_cp_totals);
     for (rxg_ctx::ws_use &u : c->wu)
         if (u.ev) (void)hipEventDestroy(u.ev);
     for (rx_track &t : c->trk)
@@ -1179,17 +1201,11 @@ int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uin
     return rxg_classify_span(c, pkts, span, off, len, n, off_unit_log2, out);
 }
 
-int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out) {
-    if (!c) return RXG_EINVAL;
-    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (n == 0) return RXG_OK;
-    if (!m || !out) return RXG_EINVAL;
-    if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
-    DEVGUARD(c);
-    const uint64_t t = c->next_ticket++;
-    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+// frames of an mbuf burst into slot sl's pinned staging at 64-B aligned
+// places (buf_addr + data_off, data_len bytes); *span = bytes used
+static int gather_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n,
+                        uint64_t *span) {
     if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_stage
-    // gather frames (buf_addr + data_off, data_len bytes) at 64-B aligned slots
     uint64_t pos = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
@@ -1202,8 +1218,117 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
         sl.h_len[i] = (uint16_t)l;
         pos += step;
     }
-    int rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    *span = pos;
+    return RXG_OK;
+}
+
+int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n == 0) return RXG_OK;
+    if (!m || !out) return RXG_EINVAL;
+    if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
+    DEVGUARD(c);
+    const uint64_t t = c->next_ticket++;
+    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+    uint64_t pos = 0;
+    int rc = gather_mbufs(c, sl, m, n, &pos);
+    if (rc) return rc;
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
     return rc ? rc : rxg_wait(c, t);
+}
+
+static int compact_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        const uint4 *d_v, rxg_dgram *d_dg, uint32_t *d_first, uint8_t *d_payload,
+                        uint64_t cap, uint32_t *d_totals, hipStream_t s) {
+    const uint32_t nf = c->fs.udp.id_space();
+    if (nf == 0 || nf > RXG_COMPACT_MAX_FLOWS) return nf ? RXG_ERANGE : RXG_OK;
+    const size_t ws = rx_compact_ws_bytes(n, nf);
+    if (ws > c->d_cp_ws_cap) {
+        HIPCHK(hipStreamSynchronize(s)); // (a grown workspace: the last use is on s)
+        int rc = ensure_dev(&c->d_cp_ws, &c->d_cp_ws_cap, ws);
+        if (rc) return rc;
+    }
+    HIPCHK(rx_compact_launch(d_pkts, d_off, d_len, n, off_unit_log2, d_v, nf, d_dg, d_first,
+                             d_payload, cap, d_totals, c->d_cp_ws, s));
+    return RXG_OK;
+}
+
+int rxg_udp_compact_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        const rxg_verdict *d_v, rxg_dgram *d_dgram, uint32_t *d_first,
+                        uint8_t *d_payload, uint64_t payload_cap, uint32_t *d_totals, void *stream) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (!d_first || !d_totals || (n && (!d_pkts || !d_off || !d_len || !d_v || !d_dgram ||
+                                        !d_payload)))
+        return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    DEVGUARD(c);
+    if (c->fs.udp.id_space() > RXG_COMPACT_MAX_FLOWS) return RXG_ERANGE;
+    return compact_impl(c, d_pkts, d_off, d_len, n, off_unit_log2,
+                        reinterpret_cast<const uint4 *>(d_v), d_dgram, d_first, d_payload,
+                        payload_cap, d_totals, (hipStream_t)stream);
+}
+
+int rxg_process_mbufs_udp(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                          const rxg_dgram **dgram, const uint32_t **first, const uint8_t **payload,
+                          uint32_t *ndgram, uint64_t *nbytes) {
+    if (!c || !dgram || !first || !payload || !ndgram || !nbytes) return RXG_EINVAL;
+    *ndgram = 0;
+    *nbytes = 0;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n && (!m || !out)) return RXG_EINVAL;
+    if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
+    const uint32_t nf = c->fs.udp.id_space();
+    if (nf > RXG_COMPACT_MAX_FLOWS) return RXG_ERANGE;
+    DEVGUARD(c);
+    if (!c->d_cp_dg) { // first use: results sized for a full staging slot
+        HIPCHK(hipMalloc(&c->d_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram)));
+        HIPCHK(hipMalloc(&c->d_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&c->d_cp_payload, c->max_bytes));
+        HIPCHK(hipMalloc(&c->d_cp_totals, 4 * sizeof(uint32_t)));
+        HIPCHK(hipHostMalloc((void **)&c->h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
+        HIPCHK(hipHostMalloc((void **)&c->h_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
+        HIPCHK(hipHostMalloc((void **)&c->h_cp_payload, c->max_bytes, 0));
+        HIPCHK(hipHostMalloc((void **)&c->h_cp_totals, 4 * sizeof(uint32_t), 0));
+    }
+    *dgram = c->h_cp_dg;
+    *first = c->h_cp_first;
+    *payload = c->h_cp_payload;
+    memset(c->h_cp_first, 0, (nf + 1) * sizeof(uint32_t));
+    if (n == 0) return RXG_OK;
+    const uint64_t t = c->next_ticket++;
+    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+    uint64_t pos = 0;
+    int rc = gather_mbufs(c, sl, m, n, &pos);
+    if (rc) return rc;
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    if (rc) return rc;
+    // the compaction follows the classify on the context's stream (its inputs:
+    // the staged frames and the device verdicts of this slot)
+    rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_cp_dg, c->d_cp_first,
+                      c->d_cp_payload, c->max_bytes, c->d_cp_totals, c->stream);
+    if (rc) return rc;
+    if (nf) {
+        HIPCHK(hipMemcpyAsync(c->h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_cp_totals[2]) return RXG_ERANGE; // (not reached: staging bounds the payloads)
+        *ndgram = c->h_cp_totals[0];
+        *nbytes = c->h_cp_totals[1];
+        HIPCHK(hipMemcpyAsync(c->h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        if (*ndgram)
+            HIPCHK(hipMemcpyAsync(c->h_cp_dg, c->d_cp_dg, (size_t)*ndgram * sizeof(rxg_dgram),
+                                  hipMemcpyDeviceToHost, c->stream));
+        if (*nbytes)
+            HIPCHK(hipMemcpyAsync(c->h_cp_payload, c->d_cp_payload, *nbytes, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return rxg_wait(c, t);
 }
 
 int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const uint16_t *d_len,

@@ -98,15 +98,43 @@ struct localhost {
     pthread_cond_t cond;
     pthread_mutex_t mutex;
     uint32_t flow_id; /* stable id in the GPU flow tables (verdict flow_id) */
+    uint32_t queued;  /* datagrams in rcvbuf (a batch item holds several) */
 };
 
+struct dgram_batch;
 struct offload {
     uint32_t sip, dip;
     uint16_t sport, dport;
     int protocol;
     unsigned char *data;
     uint16_t length;
+    struct dgram_batch *batch; /* non-NULL: this ring item is a burst's datagrams for
+                                  the socket, delivered with one copy (GPU compaction) */
 };
+
+/* The datagrams of one burst for one socket, in burst order, as the GPU's
+ * compaction (rxg_process_mbufs_udp) hands them over: one allocation, one
+ * memcpy of the socket's payload slice.  Each datagram reads as the offload
+ * udp_process would have enqueued for it (udp.c:31-46): length = dgram_len,
+ * the captured payload then zeros. */
+struct dgram_meta {
+    uint32_t sip, off; /* source address; payload offset in data */
+    uint16_t sport, len, ncopy; /* source port; payload bytes (dgram_len - 8); captured ones */
+};
+struct dgram_batch {
+    uint32_t n, next; /* datagrams; the next one to read */
+    struct dgram_meta *meta;
+    unsigned char *data;
+};
+
+static void offload_free(struct offload *o) {
+    if (!o) return;
+    if (o->batch)
+        free(o->batch); /* (meta and data live in the batch's allocation) */
+    else
+        free(o->data);
+    free(o);
+}
 
 struct tcp_stream {
     int fd;
@@ -177,6 +205,7 @@ static uint32_t g_local_ip;
 static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
+static int g_udp_done;          /* this burst's UDP datagrams went out as batches */
 
 /* the control block of each stable flow id (NULL: free id).  Blocks are
  * registered with the GPU flow tables as they are created, changed and freed
@@ -362,10 +391,7 @@ void nstack_fini(void) {
         struct localhost *h = g_pstHost;
         LL_REMOVE(h, g_pstHost);
         void *p;
-        while (ring_dequeue(h->rcvbuf, &p) == 0) {
-            free(((struct offload *)p)->data);
-            free(p);
-        }
+        while (ring_dequeue(h->rcvbuf, &p) == 0) offload_free(p);
         while (ring_dequeue(h->sndbuf, &p) == 0) {
             free(((struct offload *)p)->data);
             free(p);
@@ -588,12 +614,18 @@ ssize_t nsend(int sockfd, const void *buf, size_t len, int flags) { /* :418-460 
     return n;
 }
 
+static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags);
+
 ssize_t nrecv(int sockfd, void *buf, size_t len, int flags) { /* :462-515 */
     pthread_mutex_lock(&g_lock);
     struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
     pthread_mutex_unlock(&g_lock);
     if (!s) return -1;
     if (s->protocol != IPPROTO_TCP) return 0;
+    return nrecv_tcb(s, buf, len, flags);
+}
+
+static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags) {
     struct tcp_fragment *f = NULL;
     pthread_mutex_lock(&s->mutex);
     while (ring_dequeue(s->rcvbuf, (void **)&f) < 0) {
@@ -634,7 +666,7 @@ ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr 
     if (!h) return -1;
     struct offload *o = NULL;
     pthread_mutex_lock(&h->mutex);
-    while (ring_dequeue(h->rcvbuf, (void **)&o) < 0) {
+    while (ring_peek(h->rcvbuf, (void **)&o) < 0) {
         if (flags & MSG_DONTWAIT) {
             pthread_mutex_unlock(&h->mutex);
             errno = EAGAIN;
@@ -642,6 +674,47 @@ ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr 
         }
         pthread_cond_wait(&h->cond, &h->mutex);
     }
+    if (o->batch) { /* the next datagram of a batch, read like its own offload */
+        struct dgram_batch *b = o->batch;
+        const struct dgram_meta *d = &b->meta[b->next++];
+        struct offload *spent = NULL; /* the batch, once its last datagram is read */
+        if (b->next == b->n) ring_dequeue(h->rcvbuf, (void **)&spent);
+        if (src_addr) {
+            struct sockaddr_in *a = (struct sockaddr_in *)src_addr;
+            a->sin_family = AF_INET;
+            a->sin_port = d->sport;
+            memcpy(&a->sin_addr.s_addr, &d->sip, 4);
+        }
+        const uint32_t length = (uint32_t)d->len + 8u; /* offload.length = dgram_len (udp.c:37) */
+        if (len < length) { /* :542-556: len bytes out, the rest to the TAIL of the ring */
+            struct offload *r = calloc(1, sizeof(*r));
+            unsigned char *rest = r ? calloc(1, length - len) : NULL;
+            if (rest) {
+                if (d->ncopy > len) memcpy(rest, b->data + d->off + len, d->ncopy - len);
+                r->sip = d->sip;
+                r->sport = d->sport;
+                r->protocol = IPPROTO_UDP;
+                r->data = rest;
+                r->length = (uint16_t)(length - len);
+                if (ring_enqueue(h->rcvbuf, r)) offload_free(r), h->queued--;
+            } else {
+                free(r);
+                h->queued--;
+            }
+            memset(buf, 0, len);
+            memcpy(buf, b->data + d->off, d->ncopy < len ? d->ncopy : len);
+            offload_free(spent);
+            pthread_mutex_unlock(&h->mutex);
+            return (ssize_t)len;
+        }
+        memcpy(buf, b->data + d->off, d->ncopy); /* :558-564: payload, then zeros */
+        memset((unsigned char *)buf + d->ncopy, 0, length - d->ncopy);
+        h->queued--;
+        offload_free(spent);
+        pthread_mutex_unlock(&h->mutex);
+        return (ssize_t)length;
+    }
+    ring_dequeue(h->rcvbuf, (void **)&o);
     if (src_addr) {
         struct sockaddr_in *a = (struct sockaddr_in *)src_addr;
         a->sin_family = AF_INET;
@@ -656,11 +729,11 @@ ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr 
         pthread_mutex_unlock(&h->mutex);
         return (ssize_t)len;
     }
+    h->queued--;
     pthread_mutex_unlock(&h->mutex);
     ssize_t n = o->length; /* :558-564 */
     memcpy(buf, o->data, o->length);
-    free(o->data);
-    free(o);
+    offload_free(o);
     return n;
 }
 
@@ -708,10 +781,7 @@ int nclose(int fd) { /* :609-666 */
         unreg_udp(h);
         LL_REMOVE(h, g_pstHost);
         void *p;
-        while (ring_dequeue(h->rcvbuf, &p) == 0) {
-            free(((struct offload *)p)->data);
-            free(p);
-        }
+        while (ring_dequeue(h->rcvbuf, &p) == 0) offload_free(p);
         while (ring_dequeue(h->sndbuf, &p) == 0) {
             free(((struct offload *)p)->data);
             free(p);
@@ -978,6 +1048,7 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v, int *rc) {
         g_stat[3]++;
         return 0;
     }
+    if (g_udp_done) return 0;
     const uint8_t *f = (const uint8_t *)m->buf_addr + m->data_off;
     const uint32_t cap = m->data_len;
     struct localhost *h;
@@ -1007,8 +1078,8 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v, int *rc) {
     uint32_t ncopy = v->payload_len < avail ? v->payload_len : avail;
     memcpy(o->data, f + v->payload_off, ncopy); /* udp.c:46 */
     pthread_mutex_lock(&h->mutex);
-    int e = ring_enqueue(h->rcvbuf, o); /* udp.c:48 */
-    if (!e) pthread_cond_signal(&h->cond); /* udp.c:50-52 */
+    int e = h->queued >= D_RING_SIZE ? -ENOBUFS : ring_enqueue(h->rcvbuf, o); /* udp.c:48 */
+    if (!e) h->queued++, pthread_cond_signal(&h->cond); /* udp.c:50-52 */
     pthread_mutex_unlock(&h->mutex);
     if (e) {
         free(o->data);
@@ -1078,17 +1149,98 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
     return rc == RXG_OK ? delivered : rc;
 }
 
+/* UDP delivery of a whole burst from the GPU's compaction (g_lock held):
+ * socket by socket, its datagrams (burst order) in one batch item, their
+ * captured payloads in one memcpy; a full ring keeps the first datagrams and
+ * drops the rest, as successive enqueues would (udp.c:48) */
+static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const uint32_t *first,
+                               const uint8_t *payload, uint32_t nf) {
+    int delivered = 0;
+    for (uint32_t f = 0; f < nf; f++) {
+        const uint32_t a = first[f], k = first[f + 1] - a;
+        if (!k) continue;
+        struct localhost *h = f < s_udp_cap ? s_udp_cb[f] : NULL;
+        if (!h) continue; /* (not reached: verdicts name live sockets) */
+        pthread_mutex_lock(&h->mutex);
+        const uint32_t room = h->queued < D_RING_SIZE ? D_RING_SIZE - h->queued : 0;
+        const uint32_t take = k < room ? k : room;
+        g_stat[1] += k - take;
+        if (!take) {
+            pthread_mutex_unlock(&h->mutex);
+            continue;
+        }
+        const rxg_dgram *d0 = &dg[a], *dl = &dg[a + take - 1];
+        const uint32_t lastc = (uint32_t)dl->len < (m[dl->frame]->data_len > 42u
+                                                        ? m[dl->frame]->data_len - 42u : 0u)
+                                   ? dl->len : (m[dl->frame]->data_len > 42u
+                                                    ? m[dl->frame]->data_len - 42u : 0u);
+        const size_t bytes = (size_t)(dl->offset - d0->offset) + lastc;
+        struct offload *o = calloc(1, sizeof(*o));
+        struct dgram_batch *b = o ? malloc(sizeof(*b) + take * sizeof(struct dgram_meta) + bytes + 1)
+                                  : NULL;
+        if (!b) {
+            free(o);
+            g_stat[1] += take;
+            pthread_mutex_unlock(&h->mutex);
+            continue;
+        }
+        b->n = take;
+        b->next = 0;
+        b->meta = (struct dgram_meta *)(b + 1);
+        b->data = (unsigned char *)(b->meta + take);
+        memcpy(b->data, payload + d0->offset, bytes); /* the socket's slice, once */
+        for (uint32_t j = 0; j < take; j++) {
+            const rxg_dgram *d = &dg[a + j];
+            const uint32_t cap = m[d->frame]->data_len;
+            const uint32_t avail = cap > 42u ? cap - 42u : 0u;
+            b->meta[j].sip = d->sip;
+            b->meta[j].sport = d->sport;
+            b->meta[j].len = d->len;
+            b->meta[j].ncopy = (uint16_t)(d->len < avail ? d->len : avail);
+            b->meta[j].off = d->offset - d0->offset;
+        }
+        o->batch = b;
+        o->protocol = IPPROTO_UDP;
+        if (ring_enqueue(h->rcvbuf, o)) { /* (the item ring holds >= D_RING_SIZE) */
+            offload_free(o);
+            g_stat[1] += take;
+        } else {
+            h->queued += take;
+            g_stat[0] += take;
+            delivered += (int)take;
+            pthread_cond_signal(&h->cond); /* udp.c:50-52 */
+        }
+        pthread_mutex_unlock(&h->mutex);
+    }
+    return delivered;
+}
+
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
-    if (rc == RXG_OK) rc = rxg_process_mbufs(g_ctx, m, n, s_v);
+    const rxg_dgram *dg = NULL;
+    const uint32_t *first = NULL;
+    const uint8_t *payload = NULL;
+    uint32_t ndg = 0;
+    uint64_t nbytes = 0;
+    /* UDP payloads grouped per socket on the GPU (<= RXG_COMPACT_MAX_FLOWS ids:
+     * always, with the reference's 1024 descriptors) */
+    const int compact = rxg_num_udp_ids(g_ctx) <= RXG_COMPACT_MAX_FLOWS;
+    if (rc == RXG_OK)
+        rc = compact ? rxg_process_mbufs_udp(g_ctx, m, n, s_v, &dg, &first, &payload, &ndg, &nbytes)
+                     : rxg_process_mbufs(g_ctx, m, n, s_v);
     int delivered = 0;
     if (rc == RXG_OK) {
         if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
-        delivered = deliver_burst(m, n, s_v, rc_out);
+        if (compact) {
+            delivered = deliver_udp_batches(m, dg, first, payload, rxg_num_udp_ids(g_ctx));
+            g_udp_done = 1; /* the per-frame loop leaves UDP alone */
+        }
+        delivered += deliver_burst(m, n, s_v, rc_out);
+        g_udp_done = 0;
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
@@ -1174,6 +1326,50 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
     }
     pthread_mutex_unlock(&g_lock);
     return rc;
+}
+
+int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
+    uint64_t got = 0, nb = 0;
+    pthread_mutex_lock(&g_lock);
+    int nfd = 0;
+    int *fds = NULL;
+    struct tcp_stream **tcbs = NULL;
+    uint32_t nt = 0;
+    for (struct localhost *h = g_pstHost; h; h = h->next) nfd++;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) nt++;
+    fds = malloc((size_t)(nfd ? nfd : 1) * sizeof(int));
+    tcbs = malloc((size_t)(nt ? nt : 1) * sizeof(*tcbs));
+    if (!fds || !tcbs) {
+        pthread_mutex_unlock(&g_lock);
+        free(fds), free(tcbs);
+        return RXG_ENOMEM;
+    }
+    nfd = 0, nt = 0;
+    for (struct localhost *h = g_pstHost; h; h = h->next) fds[nfd++] = h->fd;
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) tcbs[nt++] = s;
+    pthread_mutex_unlock(&g_lock);
+    for (int k = 0; k < nfd; k++) { /* the application's nrecvfrom loop */
+        ssize_t r;
+        struct sockaddr_in a;
+        socklen_t al = sizeof(a);
+        while ((r = nrecvfrom(fds[k], buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a, &al)) >= 0)
+            got++, nb += (uint64_t)r;
+    }
+    for (uint32_t k = 0; k < nt; k++) { /* nrecv on every tcb, its queued ACKs sent */
+        struct tcp_stream *s = tcbs[k];
+        ssize_t r;
+        while ((r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT)) > 0) got++, nb += (uint64_t)r;
+        void *p;
+        pthread_mutex_lock(&s->mutex);
+        while (ring_dequeue(s->sndbuf, &p) == 0) {
+            free(((struct tcp_fragment *)p)->data);
+            free(p);
+        }
+        pthread_mutex_unlock(&s->mutex);
+    }
+    free(fds), free(tcbs);
+    if (bytes) *bytes = nb;
+    return (int64_t)got;
 }
 
 int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t) {

@@ -77,6 +77,10 @@ UDP_SOCK_DTYPE = np.dtype([("localip", "<u4"), ("localport", "<u2"), ("protocol"
                            ("_pad", "u1")])
 TCB_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
                       ("status", "<u4")])
+DGRAM_DTYPE = np.dtype([("frame", "<u4"), ("offset", "<u4"), ("sip", "<u4"), ("sport", "<u2"),
+                        ("len", "<u2")])
+assert DGRAM_DTYPE.itemsize == 16
+COMPACT_MAX_FLOWS = 1024
 
 
 class GenCfg(C.Structure):
@@ -121,6 +125,8 @@ _flows_update_udp = _sig("rxg_flows_update_udp", _i32, _vp, _u32, _vp)
 _flows_update_tcb = _sig("rxg_flows_update_tcb", _i32, _vp, _u32, _vp)
 _flows_commit = _sig("rxg_flows_commit", _i32, _vp, _vp)
 _num_udp_ids = _sig("rxg_num_udp_ids", _u32, _vp)
+_udp_compact_dev = _sig("rxg_udp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp,
+                        _vp, _u64, _vp, _vp)
 _flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
@@ -173,7 +179,8 @@ GROUP_ID_BYTES = 128
 
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
-            "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds",
+            "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
+            "rxg_process_mbufs_udp",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
@@ -368,6 +375,16 @@ class Context:
             _check(_classify_dev_cs(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2,
                                     len_hint, p(d_out), p(d_counts), stream, count_stream),
                    "rxg_classify_dev_cs")
+
+    def udp_compact_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, d_v, d_dgram,
+                        d_first, d_payload, payload_cap: int, d_totals, stream=None):
+        """K3: a classified burst's delivered datagrams grouped by socket and
+        their payloads gathered (rxg_udp_compact_dev), async on stream"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        _check(_udp_compact_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, p(d_v),
+                                p(d_dgram), p(d_first), p(d_payload), payload_cap, p(d_totals),
+                                stream), "rxg_udp_compact_dev")
 
     def tx_cksum(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
                  off_unit_log2: int) -> np.ndarray:
@@ -594,6 +611,7 @@ class NStack:
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
                    ("nstack_flow_ids", _i32, [_vp, _u32, _vp, _u32]),
+                   ("nstack_drain_all", C.c_int64, [_vp, C.c_size_t, _vp]),
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
                    ("nstack_tcb_count", _u32, []),
@@ -741,6 +759,34 @@ class NStack:
         if r < 0:
             _check(r, "nstack_rx_burst")
         return r, rcs, v
+
+    @staticmethod
+    def mbufs_over(pkts: np.ndarray, off: np.ndarray, lens: np.ndarray, off_unit_log2: int):
+        """rte_mbuf-shaped descriptors over a packed burst (no copies; keep
+        pkts alive while they are used): (array, n)"""
+        n = len(off)
+        ms = (Mbuf * n)()
+        base = pkts.ctypes.data
+        for i in range(n):
+            ms[i].buf_addr = base + (int(off[i]) << off_unit_log2)
+            ms[i].data_len = int(lens[i])
+        arr = (C.POINTER(Mbuf) * n)(*[C.pointer(ms[i]) for i in range(n)])
+        return arr, ms
+
+    def rx_burst_mbufs(self, arr, n: int, rcs: np.ndarray | None = None) -> int:
+        """nstack_rx_burst over prebuilt descriptors (mbufs_over)"""
+        r = self.lib.nstack_rx_burst(C.cast(arr, _vp), n, _ptr(rcs), None)
+        if r < 0:
+            _check(r, "nstack_rx_burst")
+        return r
+
+    def drain_all(self, buf: np.ndarray):
+        """nstack_drain_all: (items received, bytes)"""
+        nb = _u64()
+        r = self.lib.nstack_drain_all(_ptr(buf), buf.nbytes, C.byref(nb))
+        if r < 0:
+            _check(int(r), "nstack_drain_all")
+        return int(r), nb.value
 
     def stat(self, which):
         return self.lib.nstack_stat(which)

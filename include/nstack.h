@@ -129,6 +129,14 @@ int nstack_arp_insert(uint32_t ip, const uint8_t mac[6]);
 int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *len,
                     uint32_t max_frames, int cksum, uint64_t *span);
 
+/* The application side of a benchmark, in one call: every UDP socket read
+ * with nrecvfrom until empty, every tcb's receive queue read (nrecv) and its
+ * queued ACKs taken off its send ring (as one tcp_out pass would).  buf/cap =
+ * the receive buffer each call uses.  Returns the datagrams + fragments
+ * received (a negative RXG_E* code on error); *bytes = the bytes the calls
+ * returned. */
+int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
+
 /* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),
  * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,
  * 4 = TCP fragments (payload or EOF) queued for nrecv.  Counter 1 also counts

@@ -248,6 +248,43 @@ int rxg_submit(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, const uin
                uint64_t *ticket);
 int rxg_wait(rxg_ctx *ctx, uint64_t ticket);
 
+/* ---- UDP delivery on the GPU: per-socket payload compaction ------------
+ * The delivery half of udp_process (udp.c:25-52): for every datagram that
+ * found its socket (verdict rc 0) the reference mallocs an offload, copies
+ * dgram_len - 8 payload bytes from udp + 1 and enqueues it on that socket's
+ * ring, frame by frame.  Here one device pass groups a classified burst's
+ * delivered datagrams by socket — inside a socket in burst order, the order
+ * its ring would have — and gathers their captured payload bytes into one
+ * buffer, socket after socket, so the host hands each socket one contiguous
+ * slice.  UDP id spaces up to RXG_COMPACT_MAX_FLOWS (the reference's socket
+ * layer has at most 1024 descriptors, common.h:34). */
+#define RXG_COMPACT_MAX_FLOWS 1024u
+typedef struct rxg_dgram {
+    uint32_t frame;  /* burst index of the datagram's frame */
+    uint32_t offset; /* its payload's first byte in the compacted buffer (16-B aligned) */
+    uint32_t sip;    /* raw source address (offload.sip, udp.c:31) */
+    uint16_t sport;  /* raw source port (offload.sport) */
+    uint16_t len;    /* payload bytes, dgram_len - 8 (udp.c:38); only the captured ones,
+                        min(len, caplen - 42), are in the buffer: the rest read as 0 */
+} rxg_dgram;
+/* Device form, asynchronous on `stream`: d_v = the burst's verdicts; the
+ * datagrams of UDP id f get ranks [d_first[f], d_first[f+1]) of d_dgram (so
+ * d_first has rxg_num_udp_ids() + 1 entries, d_dgram room for n); d_totals =
+ * {datagrams, payload bytes used, 1 if payload_cap was too small (those
+ * payloads are not written)}.  RXG_ERANGE above RXG_COMPACT_MAX_FLOWS ids. */
+int rxg_udp_compact_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        const rxg_verdict *d_v, rxg_dgram *d_dgram, uint32_t *d_first,
+                        uint8_t *d_payload, uint64_t payload_cap, uint32_t *d_totals, void *stream);
+/* rxg_process_mbufs followed by the compaction: verdicts into `out` as there;
+ * the datagram records, the per-id first ranks and the compacted payload stay
+ * in pinned buffers the context owns, valid until its next burst call
+ * (*dgram: *ndgram records; *first: rxg_num_udp_ids() + 1 entries; *payload:
+ * *nbytes bytes).  Synchronous. */
+int rxg_process_mbufs_udp(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                          const rxg_dgram **dgram, const uint32_t **first, const uint8_t **payload,
+                          uint32_t *ndgram, uint64_t *nbytes);
+
 /* TX checksum generation (the send side's per-frame work, udp.c:84-95 and
  * tcp.c:444-463): for every IPv4 frame of the burst, the IPv4 header checksum
  * (rte_ipv4_cksum, rte_ip.h:255-265) is written at frame offset 24, and for

@@ -60,6 +60,9 @@ int oracle_nlisten(oracle_stack *st, int fd);
 int oracle_naccept(oracle_stack *st, int fd, uint32_t *sip, uint16_t *sport);
 int oracle_nclose(oracle_stack *st, int fd);
 int oracle_rx(oracle_stack *st, const uint8_t *frame, uint32_t caplen);
+void oracle_rx_burst(oracle_stack *st, const uint8_t *pkts, const uint32_t *off,
+                     const uint16_t *len, uint32_t n, uint32_t unit_log2, int32_t *rcs);
+long oracle_drain_all(oracle_stack *st, uint8_t *buf, size_t cap, uint64_t *bytes);
 long oracle_nrecvfrom(oracle_stack *st, int fd, uint8_t *buf, size_t len, uint32_t *sip,
                       uint16_t *sport);
 long oracle_nrecv(oracle_stack *st, int fd, uint8_t *buf, size_t len);

@@ -430,6 +430,46 @@ int oracle_rx(oracle_stack *st, const uint8_t *f, uint32_t cap) {
     return tcp_rx(st, f, cap);
 }
 
+/* a burst of frames through oracle_rx in order, as the reference's
+ * pkt_process loop calls udp_process / tcp_process (the socket-API rate's
+ * CPU baseline, bench.py); rcs nullable */
+void oracle_rx_burst(oracle_stack *st, const uint8_t *pkts, const uint32_t *off,
+                     const uint16_t *len, uint32_t n, uint32_t unit_log2, int32_t *rcs) {
+    for (uint32_t i = 0; i < n; i++) {
+        const int r = oracle_rx(st, pkts + ((uint64_t)off[i] << unit_log2), len[i]);
+        if (rcs) rcs[i] = r;
+    }
+}
+
+/* the application side of the same baseline: every socket read until empty
+ * (nrecvfrom / nrecv), every tcb's queued control fragments dropped (sent);
+ * returns the items received, *bytes their returned lengths */
+long oracle_drain_all(oracle_stack *st, uint8_t *buf, size_t cap, uint64_t *bytes) {
+    long got = 0;
+    uint64_t nb = 0;
+    for (o_host *h = st->hosts; h; h = h->next) {
+        long r;
+        while ((r = oracle_nrecvfrom(st, h->fd, buf, cap, NULL, NULL)) >= 0) got++, nb += (uint64_t)r;
+    }
+    for (o_tcb *s = st->tcbs; s; s = s->next) {
+        o_frag *fr;
+        while ((fr = (o_frag *)fifo_get(&s->rcvbuf)) != NULL) {
+            if (fr->length > 0) {
+                memcpy(buf, fr->data, (size_t)fr->length < cap ? (size_t)fr->length : cap);
+                got++, nb += (uint64_t)fr->length;
+            }
+            free(fr->data);
+            free(fr);
+        }
+        while ((fr = (o_frag *)fifo_get(&s->sndbuf)) != NULL) {
+            free(fr->data);
+            free(fr);
+        }
+    }
+    if (bytes) *bytes = nb;
+    return got;
+}
+
 /* nrecvfrom, common.c:517-565 (non-blocking outcome) */
 long oracle_nrecvfrom(oracle_stack *st, int fd, uint8_t *buf, size_t len, uint32_t *sip,
                       uint16_t *sport) {

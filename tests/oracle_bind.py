@@ -137,7 +137,9 @@ def _stack_sigs(l):
             ("oracle_nrecv", lng, [vp, C.c_int, vp, sz]),
             ("oracle_tcb_state", C.c_int, [vp, u32, u32, u16, u16, vp, vp, vp, vp]),
             ("oracle_tcb_sndq", C.c_int, [vp, u32, u32, u16, u16, u32, vp, vp]),
-            ("oracle_tcb_count", u32, [vp])]:
+            ("oracle_tcb_count", u32, [vp]),
+            ("oracle_rx_burst", None, [vp, vp, vp, vp, u32, u32, vp]),
+            ("oracle_drain_all", lng, [vp, vp, sz, vp])]:
         f = getattr(l, name)
         f.restype, f.argtypes = res, args
 
@@ -212,3 +214,13 @@ class Stack:
 
     def tcb_count(self):
         return lib.oracle_tcb_count(self.h)
+
+    def rx_burst(self, pkts, off, lens, off_unit_log2, rcs=None):
+        """frames through oracle_rx in burst order (one C call)"""
+        lib.oracle_rx_burst(self.h, pkts.ctypes.data, off.ctypes.data, lens.ctypes.data, len(off),
+                            off_unit_log2, None if rcs is None else rcs.ctypes.data)
+
+    def drain_all(self, buf):
+        nb = C.c_uint64()
+        r = lib.oracle_drain_all(self.h, buf.ctypes.data, buf.nbytes, C.byref(nb))
+        return r, nb.value
