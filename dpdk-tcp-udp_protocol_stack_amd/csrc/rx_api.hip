@@ -156,6 +156,7 @@ struct rxg_ctx {
     hipEvent_t ev_commit = nullptr; // after the last commit's writes
     uint64_t commit_gen = 0;
     rx_track trk[RX_TRACK];
+    rx_track *cur = nullptr; // the stream of the latest burst (its event not yet recorded)
     uint64_t use_clock = 0;
     uint32_t tune_tables = 0; // rxg_tune_tables flags
     rx_ft_dev ft{};
@@ -283,8 +284,15 @@ static uint32_t random_seed() {
 }
 
 // ---- burst tracking ----------------------------------------------------
-// the tracking entry of stream s (an LRU slot; an evicted stream's last burst
-// is waited for on the host first, so its table reads stay ordered)
+// Table writes (commits, rxg_flows_sync) must follow every burst of this
+// context still reading the tables, on whatever stream it ran — never the
+// device's other work.  An event per burst would do it but costs the burst
+// loop ~1% at cfg2 (0.2361 vs 0.2330 ms, interleaved A/B in one process,
+// profiles/r03a/ab_track.txt), so events are recorded only when needed: on a
+// stream switch, on the stream the context leaves (it was used a moment
+// ago), and lazily on the current stream when a table write comes.  The
+// stream of the context's most recent burst must therefore still exist at
+// the context's next call (rxgpu.h).
 static int track_slot(rxg_ctx *c, hipStream_t s, rx_track **out) {
     rx_track *t = nullptr, *old = &c->trk[0];
     for (rx_track &x : c->trk) {
@@ -293,7 +301,7 @@ static int track_slot(rxg_ctx *c, hipStream_t s, rx_track **out) {
     }
     if (!t) {
         t = old;
-        if (t->used) HIPCHK(hipEventSynchronize(t->ev));
+        if (t->used) HIPCHK(hipEventSynchronize(t->ev)); // (never the current stream: LRU)
         t->s = s;
         t->used = true;
         t->commit_seen = c->commit_gen; // (a new stream: tables already on the device
@@ -303,6 +311,15 @@ static int track_slot(rxg_ctx *c, hipStream_t s, rx_track **out) {
     t->last_use = ++c->use_clock;
     *out = t;
     return RXG_OK;
+}
+
+// the event of tracking entry x marks its stream's last burst: recorded now
+// for the current stream (lazily), already recorded for the others
+static hipError_t track_mark(rxg_ctx *c, rx_track &x) {
+    if (&x != c->cur) return hipSuccess;
+    hipError_t e = hipEventRecord(x.ev, x.s);
+    if (e == hipSuccess) c->cur = nullptr; // (its event now covers all its bursts)
+    return e;
 }
 
 // before a burst on s: the pending table changes, then order s after the last commit
@@ -315,26 +332,21 @@ static int burst_begin(rxg_ctx *c, hipStream_t s) {
     rx_track *t;
     int rc = track_slot(c, s, &t);
     if (rc) return rc;
+    if (c->cur && c->cur != t) HIPCHK(track_mark(c, *c->cur)); // leaving a stream
+    c->cur = t;
     if (t->commit_seen < c->commit_gen) {
         HIPCHK(hipStreamWaitEvent(s, c->ev_commit, 0));
         t->commit_seen = c->commit_gen;
     }
     return RXG_OK;
 }
-// after a burst's launches on s
-static int burst_end(rxg_ctx *c, hipStream_t s) {
-    if (c->tune_tables & RXG_TT_NO_TRACK) return RXG_OK;
-    for (rx_track &x : c->trk)
-        if (x.used && x.s == s) {
-            HIPCHK(hipEventRecord(x.ev, s));
-            return RXG_OK;
-        }
-    return RXG_OK;
-}
 // host wait for every burst of this context (a table rebuild in place)
 static int bursts_drain(rxg_ctx *c) {
     for (rx_track &x : c->trk)
-        if (x.used) HIPCHK(hipEventSynchronize(x.ev));
+        if (x.used) {
+            HIPCHK(track_mark(c, x));
+            HIPCHK(hipEventSynchronize(x.ev));
+        }
     for (rxg_ctx::ws_use &u : c->wu)
         if (u.used) HIPCHK(hipEventSynchronize(u.ev));
     if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
@@ -414,7 +426,10 @@ static int commit_on(rxg_ctx *c, hipStream_t s) {
     }
     rx_flowset &fs = c->fs;
     for (rx_track &x : c->trk)
-        if (x.used && x.s != s) HIPCHK(hipStreamWaitEvent(s, x.ev, 0));
+        if (x.used && x.s != s) {
+            HIPCHK(track_mark(c, x));
+            HIPCHK(hipStreamWaitEvent(s, x.ev, 0));
+        }
     for (rxg_ctx::ws_use &u : c->wu)
         if (u.used && u.st != s) HIPCHK(hipStreamWaitEvent(s, u.ev, 0));
     int rc = counts_layout(c, fs.udp.id_space(), fs.tcp.id_space(), s);
@@ -885,9 +900,7 @@ int rxg_flows_commit(rxg_ctx *c, void *stream) {
     }
     DEVGUARD(c);
     const hipStream_t s = (hipStream_t)stream;
-    int rc = burst_begin(c, s); // commits on s and tracks s
-    if (rc) return rc;
-    return burst_end(c, s);
+    return burst_begin(c, s); // commits on s and tracks s
 }
 
 uint32_t rxg_num_udp_ids(const rxg_ctx *c) { return c ? c->fs.udp.id_space() : 0; }
@@ -932,8 +945,7 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_NO_TRACK)))
-        return RXG_EINVAL;
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B))) return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
     return RXG_OK;
@@ -1055,18 +1067,16 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
     return RXG_OK;
 }
 
-// a burst: pending flow-table changes first (stream-ordered on s), then the
-// launches, then the tracking event that later table writes wait on
+// a burst: pending flow-table changes first (stream-ordered on s), the
+// stream tracked for later table writes, then the launches
 static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
                        uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
                        unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
     int rc = burst_begin(c, s);
     if (rc) return rc;
-    rc = classify_ws_body(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, d_out,
-                          d_counts, s, cs);
-    if (rc) return rc;
-    return burst_end(c, s);
+    return classify_ws_body(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, d_out,
+                            d_counts, s, cs);
 }
 
 static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,

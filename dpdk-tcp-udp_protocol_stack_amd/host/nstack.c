@@ -240,13 +240,25 @@ static int set_fd_frombitmap(int fd) { /* common.c:87-95 */
     return 0;
 }
 
-/* common.c:111-143 (loop advances correctly here) */
+/* common.c:111-143 (loop advances correctly here): the first block with the
+ * fd, UDP list first, each newest first.  The walk's answer per fd is kept
+ * in g_fd_cb and refreshed whenever a block with that fd is created, given
+ * the fd (naccept), or freed, so the socket calls look their descriptor up
+ * in O(1) instead of walking up to 1024 blocks per nrecvfrom. */
+static void *g_fd_cb[D_MAX_FD_COUNT];
+
+static void fd_refresh(int fd) {
+    if (fd < 0 || fd >= D_MAX_FD_COUNT) return;
+    void *cb = NULL;
+    for (struct localhost *h = g_pstHost; h && !cb; h = h->next)
+        if (h->fd == fd) cb = h;
+    for (struct tcp_stream *s = g_tcb_set; s && !cb; s = s->next)
+        if (s->fd == fd) cb = s;
+    g_fd_cb[fd] = cb;
+}
+
 static void *get_hostinfo_fromfd(int fd) {
-    for (struct localhost *h = g_pstHost; h; h = h->next)
-        if (h->fd == fd) return h;
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
-        if (s->fd == fd) return s;
-    return NULL;
+    return fd >= 0 && fd < D_MAX_FD_COUNT ? g_fd_cb[fd] : NULL;
 }
 
 /* common.c:58-70 */
@@ -417,6 +429,7 @@ void nstack_fini(void) {
         free(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
+    memset(g_fd_cb, 0, sizeof(g_fd_cb));
     free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v), free(s_udp_id),
         free(s_tcb_id);
     s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL, s_udp_id = NULL,
@@ -472,6 +485,7 @@ int nsocket(int domain, int type, int protocol) {
             goto fail;
         }
         LL_ADD(h, g_pstHost);
+        fd_refresh(fd);
     } else if (type == SOCK_STREAM) { /* :304-337 */
         struct tcp_stream *s = calloc(1, sizeof(*s));
         if (!s) goto fail;
@@ -495,6 +509,7 @@ int nsocket(int domain, int type, int protocol) {
             goto fail;
         }
         LL_ADD(s, g_tcb_set);
+        fd_refresh(fd);
     }
     pthread_mutex_unlock(&g_lock);
     return fd;
@@ -563,6 +578,7 @@ int naccept(int sockfd, struct sockaddr *addr, socklen_t *addrlen) { /* :388-416
         pthread_cond_wait(&s->accept_cond, &g_lock);
     }
     apt->fd = get_fd_frombitmap();
+    fd_refresh(apt->fd);
     if (addr) {
         struct sockaddr_in *sa = (struct sockaddr_in *)addr;
         sa->sin_family = AF_INET;
@@ -790,6 +806,7 @@ int nclose(int fd) { /* :609-666 */
         ring_free(h->sndbuf);
         free(h);
         set_fd_frombitmap(fd);
+        fd_refresh(fd);
     } else {
         struct tcp_stream *s = info;
         if (s->status != TCP_STATUS_LISTEN) { /* queue FIN, wait for LAST_ACK */
@@ -815,6 +832,7 @@ int nclose(int fd) { /* :609-666 */
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
             free(s);
+            fd_refresh(fd);
             /* the reference leaves the listener's fd set in the bitmap here */
         }
     }
@@ -1001,7 +1019,9 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
             }
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
+            const int sfd = s->fd;
             free(s);
+            fd_refresh(sfd);
             g_burst_mutated = 1;
         }
         break;

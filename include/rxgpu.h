@@ -18,6 +18,9 @@
  * checksum).  Plain pointers and sizes only; no C++ or torch types.
  *
  * Threading: one rxg_ctx per rx thread; a context is not thread-safe.
+ * Streams: bursts may run on any streams; the stream of a context's most
+ * recent burst call must still exist at the context's next call (table
+ * writes are ordered after it by an event recorded then).
  * Every call that touches the device switches the calling thread to the
  * context's device and back: the thread's current device is unchanged.
  * Errors: API calls return 0 or a negative RXG_E* code (rxg_strerror);
@@ -334,9 +337,7 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
  * <= 65536 flows.  Verdicts and counts depend on neither. */
 #define RXG_TT_NO_UDP_PORT 0x1u
 #define RXG_TT_COUNT_4B 0x2u
-/* A/B only, unsafe: no per-burst tracking event (table commits and
- * rxg_flows_sync are then no longer ordered after bursts on other streams) */
-#define RXG_TT_NO_TRACK 0x4u
+
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
