@@ -19,12 +19,20 @@ cp $OUT/pmc_$TAG.json profiles/pmc_$TAG.json || exit 1
 step bench 420 python bench.py --steps $STEPS --warmup 5 --e2e ${BENCH_ARGS:-} || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-    -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu || exit $?
+    -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu --no-sockrate || exit $?
 f=$(find $OUT/prof_$TAG -name '*kernel_trace.csv' | head -1)
 [ -n "$f" ] && python tools/trace_durations.py "$f" > $OUT/trace_durations_$TAG.txt
 # N = 2 rehearsal of the split path: two ranks on this one GPU (gloo carries
 # the counts when the ranks share a GPU; the driver's N-GPU run uses RCCL)
-step n2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 || exit $?
+step n2 400 python bench.py --gpus 2 --steps 5 --warmup 2 || exit $?
 grep '^{' $OUT/n2.log > $OUT/bench_n2_$TAG.json || true
+# CEIL=1: the read ceilings of this box (tools/membw_large: plain streams and
+# the cfg3 access pattern with no per-frame work) right after the bench, and
+# the SQ counters of the cfg3 kernel, for the roofline comparison on one box
+if [ "${CEIL:-0}" = 1 ]; then
+  step membw 300 ./tools/membw_large || exit $?
+  step sq_cfg3 400 python tools/pmc_counters.py $TAG cfg3 "--no-tx --no-sockrate --no-cfg1" \
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+    "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" || exit $?
+fi
 echo ALLDONE
