@@ -774,7 +774,7 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
         const uint32_t x7 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x107, 0xF, 0xF, false));
         if ((lane & 7u) == 0u) {
             const rx_u32x4 w = {v | (x1 << 16), x2 | (x3 << 16), x4 | (x5 << 16), x6 | (x7 << 16)};
-            __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p));
+            st_stream16(reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p), w);
         }
     } else {
         const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x101, 0xF, 0xF, false));
@@ -782,7 +782,7 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
         const uint32_t x3 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x103, 0xF, 0xF, false));
         if ((lane & 3u) == 0u) {
             const rx_u32x4 w = {idx, x1, x2, x3};
-            __builtin_nontemporal_store(w, reinterpret_cast<rx_u32x4 *>(static_cast<uint32_t *>(ft.count_idx) + p));
+            st_stream16(reinterpret_cast<rx_u32x4 *>(static_cast<uint32_t *>(ft.count_idx) + p), w);
         }
     }
 }

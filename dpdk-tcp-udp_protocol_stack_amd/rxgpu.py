@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librxgpu.so")
+# RXGPU_LIB: another build of the same library (A/B of compile-time variants)
+LIB_PATH = os.environ.get("RXGPU_LIB") or os.path.join(_HERE, "librxgpu.so")
 NSTACK_PATH = os.path.join(_HERE, "libnstack.so")
 
 # One HIP runtime per process: PyTorch (the plumbing for device memory, streams
