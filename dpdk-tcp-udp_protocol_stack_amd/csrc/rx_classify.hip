@@ -127,7 +127,7 @@ __device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) 
 // loads of a lane in flight; a pass past a frame's end loads the frame's first
 // chunk again, an L1/L2 hit, and adds nothing), which keeps enough bytes in
 // flight for jumbo frames.
-template <int G, int P, int FPG, bool NTL = true, int RI = 0>
+template <int G, int P, int FPG, bool NTL = true, int RI = 0, bool WT = false>
 __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t gl, uint32_t gbase,
                                               int32_t s0, const rx_ft_dev &ft,
                                               uint4 *__restrict__ out,
@@ -366,7 +366,10 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             v.y = (poff & 0xFFFFu) | (plen << 16);
             v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
             v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
-            stg16(&out[S.pf[f]], v);
+            if constexpr (WT)
+                stg16_wt(&out[S.pf[f]], v);
+            else
+                stg16(&out[S.pf[f]], v);
             const bool counted = rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE;
             const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
             if (counts && counted) {
@@ -383,7 +386,8 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
 // PIPE = 1: trip t+1's descriptors are fetched one trip ahead and its frame
 // bytes are issued before trip t is processed (one extra frame set of
 // registers), so both HBM round trips overlap the previous trip's work.
-template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1>
+// WT: write-through (sc1) verdict stores, which leave the XCD's L2 (A/B, pipe 40)
+template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1, bool WT = false>
 __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -418,13 +422,13 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
         group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         for (; tile * TILE < n; tile += gridDim.x) {
             group_load<G, FPG, P, NTL>(B, s0); // no-op lanes past the end (cap 0)
-            group_process<G, P, FPG, NTL, RI>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             A = B;
             group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         }
     } else {
         for (; tile * TILE < n; tile += gridDim.x) {
-            group_process<G, P, FPG, NTL, RI>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
             group_load<G, FPG, P, NTL>(A, s0);
         }
@@ -439,7 +443,8 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     }
 }
 
-template <int G, int P, int FPG, int PIPE = 0, bool NTL = true, int RI = 0, int MINW = 1>
+template <int G, int P, int FPG, int PIPE = 0, bool NTL = true, int RI = 0, int MINW = 1,
+          bool WT = false>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s, const uint32_t *idx = nullptr,
@@ -449,7 +454,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     // resident blocks: one wave of blocks, equal shares, no tail
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
-        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), 256,
+        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT>), 256,
         lds, &cu, &bpc);
     if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
@@ -458,7 +463,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
@@ -2320,6 +2325,9 @@ static const variant_entry k_variants[] = {
     {4, 1, 2, 0, launch_v<4, 1, 2, 0>},    {4, 1, 2, 1, launch_v<4, 1, 2, 1>},
     {4, 1, 4, 0, launch_v<4, 1, 4, 0>},
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
+    // 40: the cfg3 default with write-through verdict stores (sc1: the lines
+    // leave the L2 instead of staying in it)
+    {8, 2, 2, 40, launch_v<8, 2, 2, 0, true, 0, 1, true>},
     {8, 2, 1, 0, launch_v<8, 2, 1, 0>},    {8, 2, 1, 1, launch_v<8, 2, 1, 1>},
     {16, 2, 2, 0, launch_v<16, 2, 2, 0>},  {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
     {16, 2, 1, 1, launch_v<16, 2, 1, 1>},  {32, 3, 2, 0, launch_v<32, 3, 2, 0>},

@@ -103,6 +103,12 @@ __device__ __forceinline__ void st_stream16(rx_u32x4 *p, rx_u32x4 w) {
 #endif
 }
 
+// a write-through 16-B store (sc1) whatever RX_ST_POLICY says
+__device__ __forceinline__ void stg16_wt(uint4 *p, uint4 v) {
+    const rx_u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+}
+
 __device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
     const rx_u32x4 w = {v.x, v.y, v.z, v.w};
     st_stream16(reinterpret_cast<rx_u32x4 *>(p), w);

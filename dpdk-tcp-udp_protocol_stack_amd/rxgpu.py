@@ -50,7 +50,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (1, 4, 1, 5), (1, 4, 1, 6), (1, 4, 1, 7), (1, 4, 1, 8), (1, 4, 1, 9), (1, 4, 1, 10),
                    (1, 4, 1, 11), (1, 4, 1, 12), (1, 4, 1, 13), (1, 4, 1, 14),
                    (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 1, 3), (4, 1, 2, 2), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
-                   (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
+                   (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 2, 40), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
                    (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
                    (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1),
                    # pipeline 10 + RI: interleaved remainder passes (RI per frame per batch)
