@@ -2397,8 +2397,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 1.3417 ms for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716
         // on another (counts on, interleaved sweeps, profiles/r02ab)
         *g = 0, *p = 0, *fpg = 0, *pipe = 64;
-    } else if (len_hint <= 1536) { // cfg3: 1500 B
-        *g = 8, *p = 2, *fpg = 2, *pipe = 0;
+    } else if (len_hint <= 1536) { // cfg3: 1500 B.  Write-through verdict stores (pipe 40):
+        // 1.0191 vs 1.0322 ms for pipe 0 (interleaved sweep, profiles/r03c/sweep_cfg3_wt.txt),
+        // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt)
+        *g = 8, *p = 2, *fpg = 2, *pipe = 40;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), the
         // IMIX shape: pipe 38 vs 30 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms (r01g, r01j)
         *g = 0, *p = 0, *fpg = 0, *pipe = 38;
