@@ -945,13 +945,9 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_SLAB128 |
-                                   RXG_TT_CIDX_WT)))
-        return RXG_EINVAL;
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B))) return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
-    c->ft.slab128 = (flags & RXG_TT_SLAB128) ? 1u : 0u;
-    c->ft.cidx_wt = (flags & RXG_TT_CIDX_WT) ? 1u : 0u;
     return RXG_OK;
 }
 

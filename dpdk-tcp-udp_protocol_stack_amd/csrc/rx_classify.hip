@@ -779,11 +779,7 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
         const uint32_t x7 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x107, 0xF, 0xF, false));
         if ((lane & 7u) == 0u) {
             const rx_u32x4 w = {v | (x1 << 16), x2 | (x3 << 16), x4 | (x5 << 16), x6 | (x7 << 16)};
-            rx_u32x4 *dst = reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p);
-            if (ft.cidx_wt)
-                stg16_wt(reinterpret_cast<uint4 *>(dst), make_uint4(w.x, w.y, w.z, w.w));
-            else
-                st_stream16(dst, w);
+            st_stream16(reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p), w);
         }
     } else {
         const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x101, 0xF, 0xF, false));
@@ -2137,14 +2133,14 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
 // profiles/r02f/ab_count_paths.txt.)
 __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
                                                                 uint32_t nslabs, uint32_t words,
-                                                                uint32_t nflows, uint32_t rflows,
+                                                                uint32_t nflows,
                                                                 unsigned long long *__restrict__ counts) {
     __shared__ uint4 part[2][16][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    // blockIdx.y = flow range (its slabs, its rflows counts)
+    // blockIdx.y = flow range (its slabs, its 65536 counts)
     slab += (uint64_t)blockIdx.y * nslabs * words;
-    counts += (uint64_t)blockIdx.y * rflows;
-    nflows -= blockIdx.y * rflows;
+    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
+    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
     const uint32_t w = (blockIdx.x * 64 + lane) * 4; // first of this lane's 4 words
     const uint32_t wc = w < words ? w : 0;
     uint4 lo = make_uint4(0, 0, 0, 0), hi = lo;
@@ -2190,10 +2186,10 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *_
 // slab of its range, 8 loads in flight; 256-thread blocks of 1024 pairs
 __global__ __launch_bounds__(256) void rx_count_reduce_few_kernel(
     const uint32_t *__restrict__ slab, uint32_t nslabs, uint32_t words, uint32_t nflows,
-    uint32_t rflows, unsigned long long *__restrict__ counts) {
+    unsigned long long *__restrict__ counts) {
     slab += (uint64_t)blockIdx.y * nslabs * words;
-    counts += (uint64_t)blockIdx.y * rflows;
-    nflows -= blockIdx.y * rflows;
+    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
+    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
     const uint32_t w = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (w >= words) return;
     uint32_t l[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0};
@@ -2226,129 +2222,26 @@ __global__ __launch_bounds__(256) void rx_count_reduce_few_kernel(
     }
 }
 
-// ≤ 65536 flows (2-B indices), the "lite" slab pass: ranges of 16384 flows
-// (blockIdx.y), 256-thread blocks with a 32 KiB LDS histogram and nothing
-// else in LDS.  A block that size fits the slot an SH classify block (32 KiB,
-// 5 per CU) leaves when it retires, so the counts of burst k, on the count
-// stream, run beside the classify of burst k+1 instead of waiting for it to
-// drain (a 128-KiB block needs an empty CU).  Each range's blocks read their
-// whole index segment (4 ranges at 65536 flows: the segment is read 4 times,
-// from the L2 / MALL mostly) and keep the indices of their range.  Same
-// overflow rule as rx_count_slab_kernel; the wrap check's two block sums meet
-// in the first LDS words once every thread holds its bins in registers.
-constexpr uint32_t LITE_FLOWS = 16384;
-
-__device__ __forceinline__ uint32_t wave_add(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
-    return x;
-}
-
-__global__ __launch_bounds__(256) void rx_count_slab_lite_kernel(
-    const uint16_t *__restrict__ cidx, uint32_t n, uint32_t per, uint32_t words, uint32_t nflows,
-    uint32_t *__restrict__ slab, unsigned long long *__restrict__ counts) {
-    constexpr uint32_t W4 = LITE_FLOWS / 8; // 16-B bin groups (4 pairs each)
-    __shared__ __attribute__((aligned(16))) uint32_t bins[LITE_FLOWS / 2]; // 32 KiB, all of it
-    uint4 *b4 = reinterpret_cast<uint4 *>(bins);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t w4 = words / 4; // this slab's bin groups (words: a multiple of 4)
-    for (uint32_t i = tid; i < w4; i += 256) b4[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    const uint32_t f0 = blockIdx.y * LITE_FLOWS;
-    const uint32_t lim = min(nflows - f0, LITE_FLOWS);
-    const uint64_t b0 = (uint64_t)blockIdx.x * per;
-    const uint64_t b1 = min((uint64_t)n, b0 + per);
-    uint32_t mine = 0;
-    auto count = [&](uint32_t x) { // the all-ones index is never counted here (see above)
-        const uint32_t f = x - f0;
-        if (x != 0xFFFFu && f < lim) {
-            atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
-            ++mine;
-        }
-    };
-    // 8 indices per 16-B load, 8 loads in flight per thread
-    uint64_t i = b0 + 8ull * tid;
-    for (; i + 8ull * 7 * 256 + 7 < b1; i += 8ull * 8 * 256) {
-        uint4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + i + (uint64_t)u * 8 * 256));
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                count(w[j] & 0xFFFFu);
-                count(w[j] >> 16);
-            }
-        }
-    }
-    for (; i < b1; i += 8ull * 256)
-        for (uint64_t k = i; k < i + 8 && k < b1; ++k) count(cidx[k]);
-    __syncthreads();
-    uint4 r[W4 / 256];
-    uint32_t part = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < W4 / 256; ++k) {
-        const uint32_t g = k * 256 + tid;
-        r[k] = g < w4 ? b4[g] : make_uint4(0, 0, 0, 0);
-        part += (r[k].x & 0xFFFFu) + (r[k].x >> 16) + (r[k].y & 0xFFFFu) + (r[k].y >> 16) +
-                (r[k].z & 0xFFFFu) + (r[k].z >> 16) + (r[k].w & 0xFFFFu) + (r[k].w >> 16);
-    }
-    part = wave_add(part);
-    mine = wave_add(mine);
-    __syncthreads(); // every bin is in registers: the first 8 words are free
-    if (lane == 0) {
-        bins[wv] = part;
-        bins[4 + wv] = mine;
-    }
-    __syncthreads();
-    const bool wrapped = bins[0] + bins[1] + bins[2] + bins[3] !=
-                         bins[4] + bins[5] + bins[6] + bins[7]; // block-uniform
-    uint4 *dst = reinterpret_cast<uint4 *>(slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words);
-#pragma unroll
-    for (uint32_t k = 0; k < W4 / 256; ++k) {
-        const uint32_t g = k * 256 + tid;
-        if (g < w4) stg16(&dst[g], wrapped ? make_uint4(0, 0, 0, 0) : r[k]);
-    }
-    if (wrapped)
-        for (uint64_t k = b0 + tid; k < b1; k += 256) {
-            const uint32_t x = cidx[k], f = x - f0;
-            if (x != 0xFFFFu && f < lim) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
-        }
-}
-
 // Flows above 65536: the count is split into ranges of 65536 flows
 // (blockIdx.y), each range's blocks scanning every index; up to
 // SLAB_MAX_RANGES ranges, beyond that global atomics in the classify kernel.
 constexpr uint32_t SLAB_MAX_RANGES = 32;
 
-// u16 count indices: the flows fit one range
-static bool cidx16(const rx_ft_dev &ft) { return ft.nu + ft.nt <= SLAB_MAX_FLOWS; }
-
-// the lite slab pass (2-B indices)
-static bool slab_lite(const rx_ft_dev &ft) { return cidx16(ft) && !ft.count_4b && !ft.slab128; }
-
-// flows per range
-static uint32_t slab_rflows(const rx_ft_dev &ft) { return slab_lite(ft) ? LITE_FLOWS : SLAB_MAX_FLOWS; }
-
 static uint32_t slab_ranges(const rx_ft_dev &ft) {
-    return (ft.nu + ft.nt + slab_rflows(ft) - 1) / slab_rflows(ft);
+    return (ft.nu + ft.nt + SLAB_MAX_FLOWS - 1) / SLAB_MAX_FLOWS;
 }
 
 // 16-bit bin pairs per slab (a multiple of 4): all flows for one range, a
 // whole range otherwise
 static uint32_t slab_words(const rx_ft_dev &ft) {
-    return slab_ranges(ft) > 1 ? slab_rflows(ft) / 2 : (((ft.nu + ft.nt + 1) / 2 + 3) & ~3u);
+    return slab_ranges(ft) > 1 ? SLAB_MAX_FLOWS / 2 : (((ft.nu + ft.nt + 1) / 2 + 3) & ~3u);
 }
 
 // slab geometry: about one 1024-thread block per CU in all (256 blocks over
-// the ranges; lite: four 256-thread blocks per CU), >= 16384 frames per slab
-// so the slabs stay small beside the indices, a multiple of 8 frames (aligned
-// 16-B index loads)
-static void slab_geometry(const rx_ft_dev &ft, uint32_t n, uint32_t *nslabs, uint32_t *per) {
-    const uint32_t nranges = slab_ranges(ft);
-    const uint64_t want = std::max<uint64_t>(1, (slab_lite(ft) ? 1024 : 256) / nranges);
+// the ranges), >= 16384 frames per slab so the slabs stay small beside the
+// indices, a multiple of 4 frames (aligned 16-B index loads)
+static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
+    const uint64_t want = std::max<uint64_t>(1, 256 / nranges);
     uint64_t pr = std::max<uint64_t>(((uint64_t)n + want - 1) / want, 16384);
     pr = (pr + 7) & ~7ull;
     const uint64_t nb = ((uint64_t)n + pr - 1) / pr;
@@ -2361,15 +2254,15 @@ static bool use_slab(const rx_ft_dev &ft, bool counts) {
     return counts && nf >= SLAB_MIN_FLOWS && nf <= SLAB_MAX_FLOWS * SLAB_MAX_RANGES;
 }
 
+// u16 count indices: the flows fit one range
+static bool cidx16(const rx_ft_dev &ft) { return ft.nu + ft.nt <= SLAB_MAX_FLOWS; }
+
 static hipError_t launch_count_slab(const void *cidx, uint32_t n, const rx_ft_dev &ft,
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
-    slab_geometry(ft, n, &nslabs, &per);
-    if (slab_lite(ft))
-        hipLaunchKernelGGL(rx_count_slab_lite_kernel, dim3(nslabs, nr), dim3(256), 0, s,
-                           static_cast<const uint16_t *>(cidx), n, per, words, nf, slab, counts);
-    else if (ft.cidx16)
+    slab_geometry(n, nr, &nslabs, &per);
+    if (ft.cidx16)
         hipLaunchKernelGGL(rx_count_slab_kernel<uint16_t>, dim3(nslabs, nr), dim3(1024), 0, s,
                            static_cast<const uint16_t *>(cidx), n, per, words, nf,
                            slab, counts);
@@ -2379,13 +2272,12 @@ static hipError_t launch_count_slab(const void *cidx, uint32_t n, const rx_ft_de
                            slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint32_t rf = slab_rflows(ft);
     if (nslabs <= 64)
         hipLaunchKernelGGL(rx_count_reduce_few_kernel, dim3((words / 4 + 255) / 256, nr), dim3(256),
-                           0, s, slab, nslabs, words, nf, rf, counts);
+                           0, s, slab, nslabs, words, nf, counts);
     else
         hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0,
-                           s, slab, nslabs, words, nf, rf, counts);
+                           s, slab, nslabs, words, nf, counts);
     return hipGetLastError();
 }
 
@@ -2540,7 +2432,7 @@ size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_d
     size_t b = ws_lists_bytes(n, g, pipe);
     if (use_slab(ft, counts)) {
         uint32_t nslabs, per;
-        slab_geometry(ft, n, &nslabs, &per);
+        slab_geometry(n, slab_ranges(ft), &nslabs, &per);
         b += ws_cidx_bytes(n) * std::max(nbuf, 1u) +
              (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
     }

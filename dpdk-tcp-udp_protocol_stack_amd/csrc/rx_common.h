@@ -65,12 +65,6 @@ struct rx_ft_dev {
     // rxg_tune_tables(RXG_TT_COUNT_4B): 4-B count indices whatever the flow
     // count (the round-1 count path, for A/B)
     uint32_t count_4b;
-    // rxg_tune_tables(RXG_TT_SLAB128): the 128-KiB slab pass for <= 65536
-    // flows instead of the lite one (A/B)
-    uint32_t slab128;
-    // rxg_tune_tables(RXG_TT_CIDX_WT): count indices stored write-through
-    // (sc1: the lines leave the L2) instead of non-temporal (A/B)
-    uint32_t cidx_wt;
 };
 
 // rx_classify_launch phases (host side)

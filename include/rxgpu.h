@@ -334,14 +334,9 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
  * RXG_TT_NO_UDP_PORT (applied by the next rxg_flows_sync): no direct UDP port
  * table; every UDP lookup probes the hashed table.  RXG_TT_COUNT_4B (applied
  * at once): the 8193..2M-flow count path keeps 4-B count indices even at
- * <= 65536 flows.  RXG_TT_SLAB128 (applied at once): 8193..65536 flows are
- * counted by the 128-KiB-LDS slab pass instead of the lite one (16384-flow
- * ranges in 32 KiB, which shares a CU with the classify kernel).  Verdicts
- * and counts depend on none of them. */
+ * <= 65536 flows.  Verdicts and counts depend on neither. */
 #define RXG_TT_NO_UDP_PORT 0x1u
 #define RXG_TT_COUNT_4B 0x2u
-#define RXG_TT_SLAB128 0x4u
-#define RXG_TT_CIDX_WT 0x8u /* count indices stored write-through (sc1), A/B */
 
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 

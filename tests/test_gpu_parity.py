@@ -323,17 +323,13 @@ def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     assert np.array_equal(cnt, wcnt)
 
 
-@pytest.mark.parametrize("tables", [0, R.TT_SLAB128])
 @pytest.mark.parametrize("nu,nt", [(4000, 4191), (4096, 4096), (12000, 8000), (32768, 32767),
                                    (40000, 30000), (40000, 120000)])
-def test_count_paths_accumulate(ctx, torch_dev, nu, nt, tables):
+def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
     """per-flow counts on each side of the LDS-histogram / slab / global-atomic
-    thresholds (8192 and 65536 flows incl. the listener; up to 65536 the lite
-    slab pass runs per 16384-flow range — one, two partial, four — or, with
-    RXG_TT_SLAB128, the 128-KiB pass; above 65536 the slab count runs per
-    65536-flow range), accumulated over two bursts"""
+    thresholds (8192 and 65536 flows incl. the listener; above 65536 the slab
+    count runs per 65536-flow range), accumulated over two bursts"""
     torch, dev = torch_dev
-    ctx.tune_tables(tables)
     cfg = rxdist.gen_cfg("cfg4", n_udp=nu, n_tcp=nt)
     n = 50000 if nu + nt < 100000 else 15000  # the oracle's list scans are O(flows)
     pk, off, ln = R.gen_host(cfg, 99, n, 6)
@@ -352,7 +348,6 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt, tables):
         torch.cuda.synchronize(dev)
         got = d_out.cpu().numpy().view(R.VERDICT_DTYPE)
         assert got.tobytes() == want.tobytes(), _mismatch_report(got, want)
-    ctx.tune_tables(0)
     assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 2 * wcnt)
 
 

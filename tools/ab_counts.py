@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """A/B of the per-flow count passes above 8192 flows, interleaved in one
 process (GPU): the bench's step loop (classify on the main stream, the count
-passes of burst k on a second stream beside burst k+1's classify) with the
-lite slab pass (default) and the 128-KiB one (RXG_TT_SLAB128), against the
-classify kernel alone without counts.  Median and min over rounds; the counts
+passes of burst k on a second stream beside burst k+1's classify) and the
+same with every pass on one stream, against the classify kernel alone
+without counts.  Median and min over rounds; the counts
 of each mode are checked against the verdicts.  "K1" is the classify
 dispatch alone (a HIP event pair around each launch on the main stream, the
 count passes on the count stream), summed over the steps.
@@ -21,10 +21,11 @@ import torch  # noqa: E402
 import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
-MODES = [("no counts", None, 0), ("lite, count stream", True, 0),
-         ("slab128, count stream", True, R.TT_SLAB128),
-         ("slab128 + wt idx, cs", True, R.TT_SLAB128 | R.TT_CIDX_WT),
-         ("lite + wt idx, cs", True, R.TT_CIDX_WT)]
+# (name, count stream?, rxg_tune_tables flags).  profiles/r03d/ also holds a
+# run with two count variants since removed: a "lite" slab pass (16384-flow
+# ranges in 32 KiB of LDS, to share CUs with the classify kernel) and count
+# indices stored write-through; neither was faster
+MODES = [("no counts", None, 0), ("count stream", True, 0), ("one stream", False, 0)]
 
 
 def main():

@@ -35,4 +35,8 @@ if [ "${CEIL:-0}" = 1 ]; then
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
     "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" || exit $?
 fi
+# PROBE=1: L2 hits of the flow-table probes at cfg4 (with vs without the probe)
+if [ "${PROBE:-0}" = 1 ]; then
+  step probe_hits 400 python tools/pmc_probe_hits.py cfg4 $TAG || exit $?
+fi
 echo ALLDONE
