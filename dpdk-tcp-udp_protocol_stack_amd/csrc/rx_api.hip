@@ -962,6 +962,36 @@ uint32_t rxg_num_flows(const rxg_ctx *c) {
     return c ? c->fs.udp.id_space() + c->fs.tcp.id_space() : 0;
 }
 
+// diagnostics: the device image of a flow table next to the host one
+int rxg_ft_dump(rxg_ctx *c, uint32_t which, int device_copy, void *dst, uint64_t bytes,
+                uint32_t info[8]) {
+    if (!c || (!dst && bytes)) return RXG_EINVAL;
+    const rx_flowset &fs = c->fs;
+    const void *h = nullptr;
+    const void *d = nullptr;
+    uint64_t n = 0;
+    if (which == 0) h = fs.udp.tab.slots.data(), d = c->d_udp, n = fs.udp.tab.slots.size() * 16ull;
+    else if (which == 1) h = fs.tcp.tab.slots.data(), d = c->d_tcp, n = fs.tcp.tab.slots.size() * 16ull;
+    else if (which == 2) h = fs.listen.data(), d = c->d_listen, n = 65536 * 4ull;
+    else return RXG_EINVAL;
+    if (info) {
+        info[0] = c->ft.tcp_mask, info[1] = c->ft.tcp_probe, info[2] = c->ft.hseed;
+        info[3] = fs.tcp.tab.mask, info[4] = fs.tcp.tab.probe, info[5] = fs.seed;
+        info[6] = c->dirty ? 1u : 0u, info[7] = (uint32_t)(n / 16);
+    }
+    n = std::min(n, bytes);
+    if (n == 0) return RXG_OK;
+    if (!device_copy || c->device == RXG_HOST_ONLY) {
+        memcpy(dst, h, n);
+        return RXG_OK;
+    }
+    DEVGUARD(c);
+    int rc = bursts_drain(c);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(dst, d, n, hipMemcpyDeviceToHost));
+    return RXG_OK;
+}
+
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *c, uint32_t dip, uint16_t dport) {
     if (!c) return RXG_FLOW_NONE;
     const rx_flowset &fs = c->fs;
@@ -1073,8 +1103,14 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
                        uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
                        unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
+    // the context's own counts move when the commit burst_begin makes grows
+    // the id space (counts_layout frees the old vector, stream-ordered, and
+    // the same commit may allocate a table in its place): take the pointer
+    // after the commit, never before
+    const bool own = d_counts != nullptr && d_counts == c->d_counts;
     int rc = burst_begin(c, s);
     if (rc) return rc;
+    if (own) d_counts = c->d_counts;
     return classify_ws_body(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, d_out,
                             d_counts, s, cs);
 }

@@ -1404,6 +1404,22 @@ int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t
     return rc;
 }
 
+rxg_ctx *nstack_ctx(void) { return g_ctx; }
+
+uint32_t nstack_lookup_udp(uint32_t dip, uint16_t dport) {
+    pthread_mutex_lock(&g_lock);
+    const uint32_t f = g_ctx ? rxg_ft_lookup_udp(g_ctx, dip, dport) : RXG_FLOW_NONE;
+    pthread_mutex_unlock(&g_lock);
+    return f;
+}
+
+uint32_t nstack_lookup_tcp(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport) {
+    pthread_mutex_lock(&g_lock);
+    const uint32_t f = g_ctx ? rxg_ft_lookup_tcp(g_ctx, sip, dip, sport, dport) : RXG_FLOW_NONE;
+    pthread_mutex_unlock(&g_lock);
+    return f;
+}
+
 /* ---- TX: one udp_out + tcp_out pass of the protocol loop (netfamily.c:205-206) */
 static inline void wr16be(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)(v >> 8);

@@ -148,6 +148,7 @@ TT_COUNT_4B = 0x2
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)
+_ft_dump = _sig("rxg_ft_dump", _i32, _vp, _u32, _i32, _vp, _u64, _vp)
 _rss = _sig("rxg_rss_hash", _u32, _u32, _u32, _u16, _u16)
 _gen_flows = _sig("rxg_gen_flows", _i32, C.POINTER(GenCfg), _vp, _vp)
 _gen_host = _sig("rxg_gen_host", _i32, C.POINTER(GenCfg), _u64, _u32, _vp, _vp, _vp, _u32)
@@ -182,7 +183,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum", "rxg_rss_split",
@@ -588,6 +589,16 @@ def sockaddr(ip: str, port: int) -> SockaddrIn:
     return SockaddrIn(AF_INET, port_raw(port), ip_raw(ip))
 
 
+def ft_dump(h, which: int, device: bool):
+    """rxg_ft_dump of context handle h: (uint32 array of the table, info[8])"""
+    info = np.zeros(8, np.uint32)
+    _check(_ft_dump(h, which, int(device), None, 0, _ptr(info)), "rxg_ft_dump")  # sizes
+    words = int(info[7]) * 4 if which < 2 else 65536
+    buf = np.zeros(words, np.uint32)
+    _check(_ft_dump(h, which, int(device), _ptr(buf), buf.nbytes, _ptr(info)), "rxg_ft_dump")
+    return buf, info
+
+
 class NStack:
     """Process-wide socket layer (one per process, like the reference's globals)."""
     _lib = None
@@ -615,6 +626,9 @@ class NStack:
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
                    ("nstack_tcb_count", _u32, []),
+                   ("nstack_lookup_udp", _u32, [_u32, _u16]),
+                   ("nstack_lookup_tcp", _u32, [_u32, _u32, _u16, _u16]),
+                   ("nstack_ctx", _vp, []),
                    ("nstack_stat", _u64, [_i32]),
                    ("nstack_set_local", _i32, [_u32, _vp]),
                    ("nstack_arp_insert", _i32, [_u32, _vp]),
@@ -691,6 +705,18 @@ class NStack:
             m = (v["cls"] == cls) & (v["flow_id"] != FLOW_NONE)
             v["flow_id"][m] = ids[v["flow_id"][m]]
         return v
+
+    def lookup_udp(self, dip: int, dport: int) -> int:
+        """the flow id the library's tables give a UDP key (raw network order)"""
+        return self.lib.nstack_lookup_udp(dip, dport)
+
+    def lookup_tcp(self, sip: int, dip: int, sport: int, dport: int) -> int:
+        """the flow id the library's tables give a TCP 4-tuple (raw), listener included"""
+        return self.lib.nstack_lookup_tcp(sip, dip, sport, dport)
+
+    def ft_dump(self, which: int, device: bool):
+        """diagnostics: (table, info) of the socket layer's context (rxg_ft_dump)"""
+        return ft_dump(self.lib.nstack_ctx(), which, device)
 
     def flows(self, with_gen: bool = False):
         """the lists in creation order (and, with_gen, their generation for deliver)"""

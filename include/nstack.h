@@ -99,6 +99,14 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
  * nstack_flows arrays, in the same order. */
 int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t);
 
+/* Diagnostics (tests): the flow id the library's flow tables (the host image
+ * of what the device probes) give a key — UDP (dst ip, dst port), TCP (the
+ * exact 4-tuple, else the listener on dport); RXG_FLOW_NONE if none. */
+uint32_t nstack_lookup_udp(uint32_t dip, uint16_t dport);
+/* the library context the socket layer classifies with (diagnostics) */
+rxg_ctx *nstack_ctx(void);
+uint32_t nstack_lookup_tcp(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);
+
 /* Diagnostics (tests): the tcb with this exact 4-tuple (raw network order):
  * status, rcv_nxt, snd_nxt, fd; and the k-th fragment queued in its send
  * ring (TCP flags, acknum).  0 = found, -1 = none.  nstack_tcb_count = tcbs

@@ -345,6 +345,13 @@ int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);
 uint32_t rxg_num_flows(const rxg_ctx *ctx);
 
+/* Diagnostics: flow table `which` (0 UDP slots, 1 TCP slots, 2 listeners) as
+ * the device holds it (device_copy != 0; after this context's bursts drain)
+ * or as the host image is, up to `bytes`; info (nullable) = {device tcp_mask,
+ * tcp_probe, hseed, host tcp mask, probe, seed, changes pending, slots}. */
+int rxg_ft_dump(rxg_ctx *ctx, uint32_t which, int device_copy, void *dst, uint64_t bytes,
+                uint32_t info[8]);
+
 /* Host-side lookups through the built flow table (same code path as the
  * device probe, for control-plane use and tests). */
 uint32_t rxg_ft_lookup_udp(const rxg_ctx *ctx, uint32_t dip, uint16_t dport);

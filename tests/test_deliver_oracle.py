@@ -148,15 +148,37 @@ class Pair:
             assert self.ns.listen(a) == self.os.listen(a) == 0
             self.listen_fds[port] = a
 
+    def check_tables(self, frames, v):
+        """the library's host table images (what the device probes) give every
+        frame's key the flow of the oracle's list walk (verdicts v, stable ids)"""
+        for f, x in zip(frames, v):
+            if len(f) < 38 or x["cls"] not in (R.CLS_UDP, R.CLS_TCP):
+                continue
+            sip, dip = int.from_bytes(f[26:30], "little"), int.from_bytes(f[30:34], "little")
+            sport, dport = int.from_bytes(f[34:36], "little"), int.from_bytes(f[36:38], "little")
+            if x["cls"] == R.CLS_UDP:
+                assert self.ns.lookup_udp(dip, dport) == x["flow_id"], (f.hex(), x)
+            elif x["cksum_ok"]:
+                assert self.ns.lookup_tcp(sip, dip, sport, dport) == x["flow_id"], (f.hex(), x)
+
     def burst(self, frames):
         want = [self.os.rx(f) for f in frames]
         rcs = np.zeros(len(frames), np.int32)
         if self.deliver_mode == "gpu":
-            _, rcs, _ = self.ns.rx_burst(frames)
+            # the verdicts the GPU must hand the delivery: the oracle's front
+            # end over the lists as they stand before the burst, in stable ids
+            u, t = self.ns.flows()
+            buf, off, lens = F.pack_frames(frames)
+            vw = self.ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))
+            self.check_tables(frames, vw)
+            _, rcs, vg = self.ns.rx_burst(frames)
+            assert vg.tobytes() == vw.tobytes(), [(i, vg[i], vw[i]) for i in range(len(frames))
+                                                  if vg[i].tobytes() != vw[i].tobytes()]
         else:
             u, t, gen = self.ns.flows(with_gen=True)
             buf, off, lens = F.pack_frames(frames)
             v = self.ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))
+            self.check_tables(frames, v)
             self.ns.deliver(frames, v, rcs, gen)
         assert list(rcs) == want, (list(rcs), want)
 

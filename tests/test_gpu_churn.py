@@ -324,3 +324,44 @@ def test_udp_churn_small_socket_set(torch_dev):
         want["flow_id"][m] = np.array(order, np.uint32)[want["flow_id"][m]]
         assert got.tobytes() == want.tobytes(), step
     ctx.close()
+
+
+def test_counts_move_with_the_id_space_tables_intact(torch_dev):
+    """every rxg_flows_add grows the TCP id space, so the context's own count
+    vector moves (counts_layout) in the commit of the next burst; that burst's
+    kernel must count into the new vector.  Regression: the pointer was taken
+    before the commit, so the kernel added into the freed vector, whose memory
+    the same commit could hand to the grown TCP table (seen as +1 words in the
+    device table and tcbs found as their listener).  After each burst: the
+    device table equals the host image word for word, the verdicts equal the
+    model's, and the counts equal the delivered frames per flow"""
+    ctx = R.Context(0, max_pkts=4096, max_bytes=1 << 20)
+    lis = np.zeros(1, R.TCB_DTYPE)
+    lis[0] = (0, L, 0, P9999, R.TCP_STATUS_LISTEN)
+    ctx.flows_sync(None, lis)
+    want_counts = {0: 0}
+    keys = []
+    for k in range(40):
+        t = np.zeros(1, R.TCB_DTYPE)
+        cip = f"10.0.{k // 200}.{1 + k % 200}"
+        t[0] = (R.ip_raw(cip), L, R.port_raw(40000 + k), P9999, 4)
+        _, tid, _ = ctx.flows_add(None, t)
+        keys.append((cip, 40000 + k, int(tid[0])))
+        frames, ids = [], []
+        for cip_, cport, fid in keys:
+            frames.append(F.tcp_frame(cip_, cport, "192.168.100.77", 9999, b"x" * 10))
+            ids.append(fid)
+        frames.append(F.tcp_frame("10.9.9.9", 1234, "192.168.100.77", 9999, b"", flags=0x02))
+        ids.append(0)  # no tcb: the listener
+        buf, off, lens = F.pack_frames(frames, 6)
+        got = ctx.classify(buf, off, lens, 6)
+        assert list(got["flow_id"]) == ids and np.all(got["rc"] == 0), k
+        for fid in ids:
+            want_counts[fid] = want_counts.get(fid, 0) + 1
+        hd, hi = R.ft_dump(ctx._h, 1, False)
+        dd, di = R.ft_dump(ctx._h, 1, True)
+        assert np.array_equal(hd, dd), (k, np.nonzero(hd != dd)[0][:8])
+        c = ctx.flow_counts()
+        nu = ctx.num_udp_ids
+        assert all(int(c[nu + fid]) == n for fid, n in want_counts.items()), k
+    ctx.close()
