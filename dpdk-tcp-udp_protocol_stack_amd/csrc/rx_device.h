@@ -97,16 +97,19 @@ __device__ __forceinline__ uint4 ld_slot(const uint4 *p) {
 #endif
 __device__ __forceinline__ void st_stream16(rx_u32x4 *p, rx_u32x4 w) {
 #if RX_ST_POLICY == 1
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
 #else
     __builtin_nontemporal_store(w, p);
 #endif
 }
 
-// a write-through 16-B store (sc1) whatever RX_ST_POLICY says
+// a write-through 16-B store (sc1) whatever RX_ST_POLICY says.  The s_nop is
+// the one wait state a store of more than 8 bytes needs before a VALU may
+// overwrite its data registers: the compiler inserts it after its own stores,
+// but cannot see inside inline asm
 __device__ __forceinline__ void stg16_wt(uint4 *p, uint4 v) {
     const rx_u32x4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
 }
 
 __device__ __forceinline__ void stg16(uint4 *p, uint4 v) {
