@@ -116,6 +116,7 @@ COUNTS = True
 # on a second stream (rxg_classify_dev_cs) they overlap the next step's classify
 COUNT_STREAM = True
 TX = True
+V8 = True  # also time the steps with 8-B verdicts (rxg_classify_dev8)
 RAMP_MS = 200.0
 JSON_OUT = sys.stdout
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
@@ -305,6 +306,9 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     res["digest"]["seconds"] = round(time.perf_counter() - t_dg, 2)
     if res["digest"]["digest_ok"] is False:
         log(f"DIGEST MISMATCH {name}: {res['digest']}")
+    if V8 and world == 1:
+        res["verdict8"] = verdict8_leg(name, ctx, pk, off, ln, n, ul, w["len_hint"], out, nflows,
+                                       steps, warmup, dev, stream, csh, frame_bytes)
     if TX and world == 1:  # K2 (TX checksum fill) over the same burst, in place
         tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for _ in range(warmup):
@@ -323,6 +327,43 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
+
+
+def verdict8_leg(name, ctx, pk, off, ln, n, ul, len_hint, out16, nflows, steps, warmup, dev,
+                 stream, csh, frame_bytes):
+    """the same steps writing compact 8-B verdicts (rxg_classify_dev8): time,
+    rate, and every verdict against the projection of this run's 16-B
+    verdicts (pinned by the digests above) and the golden verdict8_sha256"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import digest as D  # parity leg only
+    sh = stream.cuda_stream
+    out8 = torch.empty(max(n, 1) * 8, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(max(nflows, 1), dtype=torch.int64, device=dev) if COUNTS else None
+    for _ in range(warmup):
+        ctx.classify_dev8(pk, off, ln, n, ul, len_hint, out8, cnt, stream=sh, count_stream=csh)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    torch.cuda.synchronize(dev)
+    ev[0].record(stream)
+    for _ in range(steps):
+        ctx.classify_dev8(pk, off, ln, n, ul, len_hint, out8, cnt, stream=sh, count_stream=csh)
+    if csh is not None:
+        stream.wait_stream(torch.cuda.ExternalStream(csh, device=dev))
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / max(steps, 1)
+    same = bool(torch.equal(out8[:n * 8], D.verdict8_torch(out16[:n * 16])))
+    sha = D.sha256_bytes(out8[:n * 8].cpu().numpy())
+    try:
+        gold = D.load_golden().get(name, {}).get("verdict8_sha256")
+    except OSError:
+        gold = None
+    alg = frame_bytes + 14 * n
+    r = dict(ms_per_step=round(ms, 4), mpps=round(n / ms / 1e3, 1),
+             alg_bytes_per_launch=alg, gb_per_s=round(alg / ms / 1e6, 1),
+             frac=round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), equals_projection=same,
+             verdict8_sha256=sha, digest_ok=(sha == gold) if gold else None)
+    del out8, cnt
+    return r
 
 
 def burst_digest(name, out, n, gidx, counts, total_steps, rank, world):
@@ -971,6 +1012,8 @@ def main():
                     help="per-flow counts on the classify stream (rxg_classify_dev), not "
                          "overlapped with the next step (A/B)")
     ap.add_argument("--no-tx", action="store_true", help="skip timing the TX checksum kernel")
+    ap.add_argument("--no-v8", action="store_true",
+                    help="skip the steps with 8-B verdicts (rxg_classify_dev8)")
     ap.add_argument("--collective", default="rxg", choices=["rxg", "torch"],
                     help="N > 1 count all-reduce: rxg = RCCL through librxgpu's C ABI "
                          "(rxg_group); torch = torch.distributed's nccl (RCCL) backend")
@@ -1040,7 +1083,8 @@ def main():
     ctx = R.Context(local)
     if a.flow_load:
         ctx.tune_flow_load(a.flow_load)
-    global COUNTS, TX, RAMP_MS, COUNT_STREAM
+    global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8
+    V8 = not a.no_v8
     RAMP_MS = a.ramp_ms
     COUNT_STREAM = not a.no_count_stream
     COUNTS = not a.no_counts
@@ -1095,7 +1139,9 @@ def main():
 
     parity_bad = sum(r["parity"]["mismatches"] for r in results.values()) + \
         (cfg1["parity"]["mismatches"] if cfg1 else 0) + \
-        sum(r["digest"]["digest_ok"] is False for r in results.values())
+        sum(r["digest"]["digest_ok"] is False for r in results.values()) + \
+        sum(("verdict8" in r and (not r["verdict8"]["equals_projection"]
+                                  or r["verdict8"]["digest_ok"] is False)) for r in results.values())
     if rank == 0:
         line = {
             "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
@@ -1130,6 +1176,8 @@ def main():
             line["allreduce_ms"] = head["allreduce_ms"]
             line["allreduce_bytes"] = head["allreduce_bytes"]
             line["per_rank"] = head["per_rank"]
+        if "verdict8" in head:
+            line["verdict8"] = head["verdict8"]
         if "tx_cksum" in head:
             line["tx_cksum"] = head["tx_cksum"]
         if "e2e_pcie" in head:

@@ -23,6 +23,13 @@ hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const ui
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
                               unsigned long long *counts, hipStream_t s, uint32_t *ws,
                               uint32_t phase, uint32_t buf, uint32_t nbuf);
+// the same kernels writing 8-B verdicts (rx_classify.hip built with RX_V8=1)
+hipError_t rx_classify_launch8(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
+                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
+                               unsigned long long *counts, hipStream_t s, uint32_t *ws,
+                               uint32_t phase, uint32_t buf, uint32_t nbuf);
+void rx_set_bpc_cap8(uint32_t cap);
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts, uint32_t nbuf);
 bool rx_count_uses_slabs(const rx_ft_dev &ft, bool counts);
@@ -1062,8 +1069,11 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
         return RXG_OK;
     };
     rx_set_bpc_cap(c->tune_bpc);
+    rx_set_bpc_cap8(c->tune_bpc);
+    // the verdict format of this burst (rxg_classify_dev8: c->ft.v8)
+    const auto k1 = c->ft.v8 ? rx_classify_launch8 : rx_classify_launch;
     if (!ws) {
-        HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+        HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
                                   d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
         return join_cs();
     }
@@ -1076,7 +1086,7 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
     if (!split) {
         HIPCHK(ws_wait(c, WS_BUF0, s));
         HIPCHK(ws_wait(c, WS_SLAB, s));
-        HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+        HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
                                   d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
         HIPCHK(ws_mark(c, WS_BUF0, s));
         HIPCHK(ws_mark(c, WS_SLAB, s));
@@ -1085,12 +1095,12 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
     const uint32_t b = c->ws_flip;
     c->ws_flip ^= 1u;
     HIPCHK(ws_wait(c, b, s)); // the count that last read this index buffer
-    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+    HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
                               d_out, d_counts, s, c->d_ws, RX_PH_CLASSIFY, b, 2));
     HIPCHK(hipEventRecord(c->ev_k1, s));
     HIPCHK(hipStreamWaitEvent(cs, c->ev_k1, 0));
     HIPCHK(ws_wait(c, WS_SLAB, cs));
-    HIPCHK(rx_classify_launch(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
+    HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
                               d_out, d_counts, cs, c->d_ws, RX_PH_COUNT, b, 2));
     HIPCHK(ws_mark(c, b, cs)); // covers the classify too (cs waited on it)
     HIPCHK(ws_mark(c, WS_SLAB, cs));
@@ -1117,8 +1127,8 @@ static int classify_ws(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
 
 static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                              const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
-                             uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
-                             hipStream_t s, hipStream_t cs) {
+                             uint32_t len_hint, void *d_out, uint64_t *d_counts, hipStream_t s,
+                             hipStream_t cs, uint32_t v8 = 0) {
     if (!c) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
     if (n == 0) return RXG_OK;
@@ -1127,9 +1137,12 @@ static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *
     DEVGUARD(c);
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
     if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
-    return classify_ws(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe,
-                       reinterpret_cast<uint4 *>(d_out),
-                       reinterpret_cast<unsigned long long *>(d_counts), s, cs);
+    c->ft.v8 = v8; // read by this burst's launches only (they copy c->ft)
+    const int rc = classify_ws(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe,
+                               static_cast<uint4 *>(d_out),
+                               reinterpret_cast<unsigned long long *>(d_counts), s, cs);
+    c->ft.v8 = 0;
+    return rc;
 }
 
 int rxg_classify_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
@@ -1145,6 +1158,15 @@ int rxg_classify_dev_cs(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off
                         void *count_stream) {
     return classify_dev_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, len_hint, d_out,
                              d_counts, (hipStream_t)stream, (hipStream_t)count_stream);
+}
+
+int rxg_classify_dev8(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                      const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t len_hint,
+                      rxg_verdict8 *d_out, uint64_t *d_counts, void *stream, void *count_stream) {
+    static_assert(sizeof(rxg_verdict8) == 8, "rxg_verdict8 is 8 bytes");
+    if (d_out && (reinterpret_cast<uintptr_t>(d_out) & 7u)) return RXG_EINVAL;
+    return classify_dev_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, len_hint, d_out,
+                             d_counts, (hipStream_t)stream, (hipStream_t)count_stream, 1u);
 }
 
 // Frames of a host burst into a slot: exactly `span` bytes cross PCIe (the

@@ -59,6 +59,20 @@
 #include "rx_common.h"
 #include "rx_device.h"
 
+// This file is compiled twice (Makefile): RX_V8 = 0 writes the 16-B
+// rxg_verdict, RX_V8 = 1 the 8-B rxg_verdict8 (rxg_classify_dev8).  The
+// second build exports only rx_classify_launch8 and rx_set_bpc_cap8, so the
+// format is a compile-time choice in every kernel: no branch on either path
+// (a run-time switch measured 0.2-0.6% slower on the 16-B path, r03e).
+#ifndef RX_V8
+#define RX_V8 0
+#endif
+#if RX_V8
+#define RX_K1_NAME(x) x##8
+#else
+#define RX_K1_NAME(x) x
+#endif
+
 namespace {
 
 // resident blocks per CU the launchers use: min(occupancy, cap); 0 = no cap
@@ -78,6 +92,40 @@ __device__ __forceinline__ void count_ffff(const rx_ft_dev &ft, uint32_t idx) {
 __device__ __forceinline__ void put_count_idx(const rx_ft_dev &ft, uint64_t p, uint32_t idx) {
     if (ft.count_ffff) count_ffff(ft, idx);
     rx_put_count_idx(ft, p, idx);
+}
+
+// The verdict store.  RX_V8: the compact 8-B verdict
+// (rxg_verdict8, include/rxgpu.h) packed from the 16-B one: flow id; then
+// payload_len | payload_off (7 bits) + TCP_NEGLEN << 7 | cls | rc (3-bit
+// two's complement) << 3 | cksum_ok << 6 | TRUNC << 7.  Everything the
+// reference decides per frame; only the two checksum values (l4_cksum,
+// stored_cksum: cksum_ok is their comparison) stay in the 16-B form.
+__device__ __forceinline__ uint64_t verdict8_of(uint4 v) {
+    const uint32_t hi = (v.y >> 16) | ((v.y & 0x7Fu) << 16) | ((v.w & 0x200u) << 14) |
+                        (((v.z >> 16) & 7u) << 24) | (((v.z >> 24) & 7u) << 27) |
+                        ((v.w & 1u) << 30) | ((v.w & 0x100u) << 23);
+    return (uint64_t)v.x | ((uint64_t)hi << 32);
+}
+// WT: write-through (sc1) stores; PLAIN: ordinary stores; else non-temporal
+template <bool WT = false, bool PLAIN = false>
+__device__ __forceinline__ void st_verdict(const rx_ft_dev &ft, uint4 *__restrict__ out, uint64_t p,
+                                           uint4 v) {
+    if constexpr (RX_V8) {
+        uint64_t *o = reinterpret_cast<uint64_t *>(out) + p;
+        const uint64_t w = verdict8_of(v);
+        if constexpr (WT)
+            asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(o), "v"(w) : "memory");
+        else if constexpr (PLAIN)
+            *o = w;
+        else
+            __builtin_nontemporal_store(w, o);
+    } else if constexpr (WT) {
+        stg16_wt(&out[p], v);
+    } else if constexpr (PLAIN) {
+        out[p] = v;
+    } else {
+        stg16(&out[p], v);
+    }
 }
 
 template <int FPG, int P>
@@ -366,10 +414,7 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             v.y = (poff & 0xFFFFu) | (plen << 16);
             v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
             v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
-            if constexpr (WT)
-                stg16_wt(&out[S.pf[f]], v);
-            else
-                stg16(&out[S.pf[f]], v);
+            st_verdict<WT>(ft, out, S.pf[f], v);
             const bool counted = rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE;
             const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
             if (counts && counted) {
@@ -793,11 +838,9 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
 }
 
 template <bool ST_NT>
-__device__ __forceinline__ void lane_store(uint4 *__restrict__ out, uint64_t p, uint4 v) {
-    if constexpr (ST_NT)
-        stg16(&out[p], v);
-    else
-        out[p] = v;
+__device__ __forceinline__ void lane_store(const rx_ft_dev &ft, uint4 *__restrict__ out, uint64_t p,
+                                           uint4 v) {
+    st_verdict<false, !ST_NT>(ft, out, p, v);
 }
 
 // the original one-shot form: verdict, store, count
@@ -813,7 +856,7 @@ __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
         if (ABL & 4)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
         else
-            lane_store<ST_NT>(out, L.p, v);
+            lane_store<ST_NT>(ft, out, L.p, v);
         lane_count(idx, counts, hist, lds_bins);
         if (ft.count_idx) put_count_idx(ft, L.p, idx);
     }
@@ -869,7 +912,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             const uint64_t nq = nvalid ? np : 0;
             const uint32_t noff = off[nq];
             const uint16_t nlen = len[nq];
-            if (pend_valid) lane_store<ST_NT>(out, pend_p, pend);
+            if (pend_valid) lane_store<ST_NT>(ft, out, pend_p, pend);
             uint32_t idx;
             pend = lane_verdict<ABL, NTL>(L, nullptr, ft, &idx);
             pend_p = L.p;
@@ -881,7 +924,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             L.fb = pkts + ((uint64_t)noff << unit_log2);
             L.cap = nvalid ? (int32_t)nlen : 0;
         }
-        if (pend_valid) lane_store<ST_NT>(out, pend_p, pend);
+        if (pend_valid) lane_store<ST_NT>(ft, out, pend_p, pend);
     } else if constexpr (PIPE == 0) {
         for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += stride, p += stride) {
             lane_frame L;
@@ -1620,7 +1663,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             vd.y = vy;
             vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
             vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-            stg16(&out[p], vd);
+            st_verdict(ft, out, p, vd);
             lane_count(cidx, counts, hist, lds_bins);
         }
         put_count_idx_wave(ft, p, cidx, lane);
@@ -2004,7 +2047,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         vd.y = (poff & 0xFFFFu) | (plen << 16);
         vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
-        stg16(&out[p], vd);
+        st_verdict(ft, out, p, vd);
         lane_count(cidx, counts, hist, lds_bins);
     }
     put_count_idx_wave(ft, p, cidx, lane);
@@ -2384,6 +2427,7 @@ static const variant_entry k_variants[] = {
 // bench.py --sweep, interleaved rounds).  Any frame length works
 // with any variant (frames longer than P passes take the remainder loop); the
 // choice only moves speed.
+#if !RX_V8
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b),
@@ -2407,7 +2451,11 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
     }
 }
 
-void rx_set_bpc_cap(uint32_t cap) { g_bpc_cap = cap; }
+#endif
+
+void RX_K1_NAME(rx_set_bpc_cap)(uint32_t cap) { g_bpc_cap = cap; }
+
+#if !RX_V8
 
 // a compiled variant with this lanes-per-frame and pipeline id (rxg_tune)
 bool rx_variant_exists(uint32_t g, uint32_t pipe) {
@@ -2415,6 +2463,8 @@ bool rx_variant_exists(uint32_t g, uint32_t pipe) {
         if (v.g == g && v.pipe == pipe) return true;
     return false;
 }
+#endif
+
 
 // workspace bytes one launch needs: the binned path's lists (16 B + 8 B per
 // frame), then nbuf count-index buffers (room for 4 B per frame each: two when
@@ -2425,6 +2475,7 @@ static size_t ws_lists_bytes(uint32_t n, uint32_t g, uint32_t pipe) {
 }
 static size_t ws_cidx_bytes(uint32_t n) { return ((size_t)n * 4 + 255) & ~(size_t)255; }
 
+#if !RX_V8
 bool rx_count_uses_slabs(const rx_ft_dev &ft, bool counts) { return use_slab(ft, counts); }
 
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
@@ -2445,7 +2496,9 @@ size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_d
 // caller orders it after the RX_PH_CLASSIFY launch that filled the buffer).
 // Without the slab path (few flows, or no counts) RX_PH_COUNT does nothing and
 // the other two count inside the classify kernel.
-hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+#endif
+
+hipError_t RX_K1_NAME(rx_classify_launch)(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft_in, uint4 *out,
                               unsigned long long *counts, hipStream_t s, uint32_t *ws,

@@ -74,6 +74,25 @@ VERDICT_DTYPE = np.dtype([
     ("cls", "u1"), ("rc", "i1"), ("cksum_ok", "u1"), ("flags", "u1"), ("stored_cksum", "<u2"),
 ])
 assert VERDICT_DTYPE.itemsize == 16
+# rxg_verdict8 (rxg_classify_dev8): off_neg = payload_off | TCP_NEGLEN << 7,
+# status = cls | (rc & 7) << 3 | cksum_ok << 6 | TRUNC << 7
+VERDICT8_DTYPE = np.dtype([("flow_id", "<u4"), ("payload_len", "<u2"), ("off_neg", "u1"),
+                           ("status", "u1")])
+assert VERDICT8_DTYPE.itemsize == 8
+
+
+def verdict8_of(v: np.ndarray) -> np.ndarray:
+    """the 8-B verdicts of 16-B ones (rxg_verdict8_of in include/rxgpu.h)"""
+    v = np.ascontiguousarray(v).view(VERDICT_DTYPE)
+    r = np.empty(v.shape, VERDICT8_DTYPE)
+    r["flow_id"] = v["flow_id"]
+    r["payload_len"] = v["payload_len"]
+    r["off_neg"] = (v["payload_off"] & 0x7F) | np.where(v["flags"] & 0x02, 0x80, 0)
+    r["status"] = ((v["cls"] & 7) | ((v["rc"].view(np.uint8) & 7) << 3) | ((v["cksum_ok"] & 1) << 6)
+                   | np.where(v["flags"] & 0x01, 0x80, 0)).astype(np.uint8)
+    return r
+
+
 UDP_SOCK_DTYPE = np.dtype([("localip", "<u4"), ("localport", "<u2"), ("protocol", "u1"),
                            ("_pad", "u1")])
 TCB_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
@@ -132,6 +151,9 @@ _flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
                         _vp, _vp)
+# (older builds, e.g. an A/B against a previous library, lack it: classify_dev8 then raises)
+_classify_dev8 = (_sig("rxg_classify_dev8", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
+                       _vp, _vp) if hasattr(_lib, "rxg_classify_dev8") else None)
 _classify = _sig("rxg_classify", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp)
 _classify_span = _sig("rxg_classify_span", _i32, _vp, _vp, _u64, _vp, _vp, _u32, _u32, _vp)
 _process_mbufs = _sig("rxg_process_mbufs", _i32, _vp, _vp, _u32, _vp)
@@ -182,7 +204,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp",
-            "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
+            "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
@@ -376,6 +398,17 @@ class Context:
             _check(_classify_dev_cs(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2,
                                     len_hint, p(d_out), p(d_counts), stream, count_stream),
                    "rxg_classify_dev_cs")
+
+    def classify_dev8(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, len_hint: int,
+                      d_out, d_counts=None, stream=None, count_stream=None):
+        """classify_dev writing 8-B verdicts (VERDICT8_DTYPE, rxg_classify_dev8)
+        into d_out (n x 8 bytes)"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        if _classify_dev8 is None:
+            raise RuntimeError(f"{LIB_PATH} has no rxg_classify_dev8 (an older build)")
+        _check(_classify_dev8(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, len_hint,
+                              p(d_out), p(d_counts), stream, count_stream), "rxg_classify_dev8")
 
     def udp_compact_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, d_v, d_dgram,
                         d_first, d_payload, payload_cap: int, d_totals, stream=None):

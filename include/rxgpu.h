@@ -85,6 +85,41 @@ typedef struct rxg_verdict {
     uint16_t stored_cksum; /* the L4 checksum field as stored in the frame (LE u16) */
 } rxg_verdict;
 
+/* Compact 8-byte verdict (rxg_classify_dev8): the same decision in half the
+ * bytes, for the device-resident burst loop, where the verdict array is a
+ * quarter of the HBM traffic at 64-B frames.  It carries everything the
+ * reference decides per frame (return code, matched block, payload window,
+ * checksum pass/fail, class, flags); only the two checksum VALUES of the
+ * 16-byte form (l4_cksum, stored_cksum) are left out — cksum_ok is their
+ * comparison.  Field for field it equals rxg_verdict8_of(the 16-byte verdict). */
+typedef struct rxg_verdict8 {
+    uint32_t flow_id;     /* = rxg_verdict.flow_id */
+    uint16_t payload_len; /* = rxg_verdict.payload_len */
+    uint8_t off_neg;      /* bits 0-6: payload_off (0, 42 or 34 + 4*hl <= 94);
+                             bit 7: RXG_F_TCP_NEGLEN */
+    uint8_t status;       /* bits 0-2: cls; bits 3-5: rc (3-bit two's complement);
+                             bit 6: cksum_ok; bit 7: RXG_F_TRUNC */
+} rxg_verdict8;
+
+#define RXG_V8_PAYLOAD_OFF(v) ((uint32_t)((v).off_neg & 0x7Fu))
+#define RXG_V8_CLS(v) ((uint32_t)((v).status & 7u))
+#define RXG_V8_RC(v) ((int32_t)(((v).status >> 3) & 7u) - (int32_t)((((v).status >> 3) & 4u) << 1))
+#define RXG_V8_CKSUM_OK(v) ((uint32_t)(((v).status >> 6) & 1u))
+/* RXG_F_* of the 16-byte form (UDP_SHORT: a UDP frame with payload_len 0) */
+#define RXG_V8_FLAGS(v)                                                                 \
+    ((uint32_t)((v).status >> 7) | ((uint32_t)((v).off_neg >> 7) << 1) |              \
+     ((RXG_V8_CLS(v) == RXG_CLS_UDP && (v).payload_len == 0) ? (uint32_t)RXG_F_UDP_SHORT : 0u))
+
+static inline rxg_verdict8 rxg_verdict8_of(const rxg_verdict *v) {
+    rxg_verdict8 r;
+    r.flow_id = v->flow_id;
+    r.payload_len = v->payload_len;
+    r.off_neg = (uint8_t)((v->payload_off & 0x7Fu) | ((v->flags & RXG_F_TCP_NEGLEN) ? 0x80u : 0u));
+    r.status = (uint8_t)((v->cls & 7u) | (((uint32_t)(uint8_t)v->rc & 7u) << 3) |
+                         ((v->cksum_ok & 1u) << 6) | ((v->flags & RXG_F_TRUNC) ? 0x80u : 0u));
+    return r;
+}
+
 /* ---- control-block snapshot (flow table source) ---------------------- */
 
 /* One UDP socket = one `struct localhost` of the reference (udp.h:10-29).
@@ -221,6 +256,13 @@ int rxg_classify_dev_cs(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_o
                         const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
                         uint32_t len_hint, rxg_verdict *d_out, uint64_t *d_counts,
                         void *stream, void *count_stream);
+
+/* rxg_classify_dev_cs writing compact 8-byte verdicts (d_out: n x 8 bytes,
+ * 8-byte aligned); kernels, counts and streams exactly as there. */
+int rxg_classify_dev8(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                      const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                      uint32_t len_hint, rxg_verdict8 *d_out, uint64_t *d_counts, void *stream,
+                      void *count_stream);
 
 /* Host-buffer burst (PCIe-inclusive): copies frames + descriptors to the
  * device, classifies, copies verdicts back, accumulates the context's own

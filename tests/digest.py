@@ -74,6 +74,17 @@ def frame_digest_torch(idx, verdicts) -> int:
     return int(h.sum().item()) & _M64  # int64 sum wraps like u64
 
 
+def verdict8_torch(verdicts):
+    """rxgpu.verdict8_of on the device: a uint8 tensor of n x 16 verdict bytes
+    -> n x 8 bytes (rxg_verdict8)"""
+    import torch
+    v = verdicts.reshape(-1, 16).view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    x, y, z, w = v[:, 0], v[:, 1], v[:, 2], v[:, 3]
+    hi = ((y >> 16) | ((y & 0x7F) << 16) | ((w & 0x200) << 14) | (((z >> 16) & 7) << 24)
+          | (((z >> 24) & 7) << 27) | ((w & 1) << 30) | ((w & 0x100) << 23))
+    return (x | (hi << 32)).contiguous().view(torch.uint8)
+
+
 def sha256_bytes(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()
 

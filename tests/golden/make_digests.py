@@ -8,6 +8,9 @@ reference's list-scan lookups and DPDK checksum, test infrastructure) on
 `--threads` host threads, and reduced to:
 
   verdict_sha256  SHA-256 of the n x 16 verdict bytes in frame order
+  verdict8_sha256 SHA-256 of the n x 8 compact verdicts (rxg_verdict8: the
+                  16-B verdicts projected by rxgpu.verdict8_of, as
+                  rxg_classify_dev8 writes them)
   frame_digest    sum over frames of H(i, verdict_i) mod 2**64 (tests/digest.py)
   counts_sha256   SHA-256 of the burst's per-flow histogram (u64 LE, UDP then TCP)
   rc / cls        verdict histograms (for reading)
@@ -64,6 +67,7 @@ def digest_config(name: str, threads: int, n: int | None = None) -> dict:
         return v, cnt
 
     sha = hashlib.sha256()
+    sha8 = hashlib.sha256()
     fd = 0
     counts = np.zeros(max(nflows, 1), np.uint64)[:nflows]
     rc = {}
@@ -73,6 +77,7 @@ def digest_config(name: str, threads: int, n: int | None = None) -> dict:
     with cf.ThreadPoolExecutor(threads) as ex:
         for s, (v, cnt) in zip(starts, ex.map(work, starts)):  # results in frame order
             sha.update(v.tobytes())
+            sha8.update(R.verdict8_of(v).tobytes())
             fd = (fd + D.frame_digest_np(np.arange(s, s + len(v), dtype=np.uint64), v)) & D._M64
             counts += cnt
             for key, hist in (("rc", rc), ("cls", cls)):
@@ -85,7 +90,7 @@ def digest_config(name: str, threads: int, n: int | None = None) -> dict:
                 print(f"{name}: {done}/{n} frames, {el:.0f} s", file=sys.stderr, flush=True)
     el = time.perf_counter() - t0
     return dict(workload=name, desc=w["desc"], frames=n, flows=nflows,
-                verdict_sha256=sha.hexdigest(), frame_digest=f"{fd:016x}",
+                verdict_sha256=sha.hexdigest(), verdict8_sha256=sha8.hexdigest(), frame_digest=f"{fd:016x}",
                 counts_sha256=D.counts_sha256(counts), counted=int(counts.sum()),
                 rc=rc, cls=cls, seconds=round(el, 1), threads=threads,
                 host=platform.processor() or platform.machine(),

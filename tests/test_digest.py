@@ -80,3 +80,38 @@ def test_gpu_whole_burst_matches_golden_digest(name):
         assert D.counts_sha256(c) == g["counts_sha256"], name
         del d_pk, out
         torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+def test_gpu_whole_burst_v8_matches_golden_digest(name):
+    """rxg_classify_dev8 (8-B verdicts, counts on a second stream above 8192
+    flows): every verdict of the full burst hashes to the oracle's projected
+    digest, and the per-flow counts to the oracle's histogram"""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a GPU (no fallback path exists)")
+    dev = torch.device("cuda", 0)
+    w = rxdist.WORKLOADS[name]
+    cfg = rxdist.gen_cfg(name)
+    n, ul = w["n"], w["unit_log2"]
+    udp, tcb = R.gen_flows(cfg)
+    g = GOLD[name]
+    with R.Context(0) as ctx:
+        ctx.flows_sync(udp, tcb)
+        d_pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
+        d_off = torch.empty(n, dtype=torch.int32, device=dev)
+        d_ln = torch.empty(n, dtype=torch.int16, device=dev)
+        st = torch.cuda.current_stream(dev)
+        cs = torch.cuda.Stream(dev)
+        R.gen_dev(cfg, 0, n, d_pk, d_off, d_ln, ul, stream=st.cuda_stream)
+        out = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(max(ctx.num_flows, 1), dtype=torch.int64, device=dev)
+        ctx.classify_dev8(d_pk, d_off, d_ln, n, ul, w["len_hint"], out, cnt, stream=st.cuda_stream,
+                          count_stream=cs.cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert D.sha256_bytes(out.cpu().numpy()) == g["verdict8_sha256"], name
+        c = cnt.cpu().numpy().view(np.uint64)[:ctx.num_flows]
+        assert D.counts_sha256(c) == g["counts_sha256"], name
+        del d_pk, out
+        torch.cuda.empty_cache()

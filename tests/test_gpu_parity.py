@@ -31,18 +31,24 @@ def ctx(torch_dev):
     c.close()
 
 
-def _dev_classify(torch_dev, ctx, buf, off, lens, unit_log2, len_hint, counts=False):
+def _dev_classify(torch_dev, ctx, buf, off, lens, unit_log2, len_hint, counts=False, v8=False):
+    """device burst through rxg_classify_dev (16-B verdicts) or, v8,
+    rxg_classify_dev8 (8-B verdicts, compared with R.verdict8_of(oracle))"""
     torch, dev = torch_dev
     n = len(off)
     d_pk = torch.from_numpy(np.concatenate([buf, np.zeros(64, np.uint8)])).to(dev)
     d_off = torch.from_numpy(off.view(np.int32)).to(dev)
     d_ln = torch.from_numpy(lens.view(np.int16)).to(dev)
-    d_out = torch.full((n * 16,), 0xAB, dtype=torch.uint8, device=dev)
+    vb = 8 if v8 else 16
+    d_out = torch.full((n * vb + 8,), 0xAB, dtype=torch.uint8, device=dev)
     d_cnt = torch.zeros(max(ctx.num_flows, 1), dtype=torch.int64, device=dev) if counts else None
-    ctx.classify_dev(d_pk, d_off, d_ln, n, unit_log2, len_hint, d_out, d_cnt,
-                     stream=torch.cuda.current_stream(dev).cuda_stream)
+    fn = ctx.classify_dev8 if v8 else ctx.classify_dev
+    fn(d_pk, d_off, d_ln, n, unit_log2, len_hint, d_out, d_cnt,
+       stream=torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    v = d_out.cpu().numpy().view(R.VERDICT_DTYPE)
+    o = d_out.cpu().numpy()
+    assert (o[n * vb:] == 0xAB).all(), "store past the burst's verdicts"
+    v = o[:n * vb].view(R.VERDICT8_DTYPE if v8 else R.VERDICT_DTYPE)
     if counts:
         return v, d_cnt.cpu().numpy().view(np.uint64)[:ctx.num_flows]
     return v
@@ -61,9 +67,12 @@ def test_edge_fixture(ctx, torch_dev):
     want = np.load(os.path.join(GOLD, "edge_verdicts.npy"))
     got = ctx.classify(buf, off, lens, 6)              # host-buffer path
     assert got.tobytes() == want.tobytes(), _mismatch_report(got, want)
+    want8 = R.verdict8_of(want)
     for hint in (64, 300, 600, 1500, 9000):             # every lanes-per-frame variant
         got = _dev_classify(torch_dev, ctx, buf, off, lens, 6, hint)
         assert got.tobytes() == want.tobytes(), (hint, _mismatch_report(got, want))
+        got = _dev_classify(torch_dev, ctx, buf, off, lens, 6, hint, v8=True)
+        assert got.tobytes() == want8.tobytes(), (hint, _mismatch_report(got, want8))
 
 
 def test_survey_frame_kats(ctx):
@@ -134,6 +143,11 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
         got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, w["unit_log2"], hint, counts=True)
         assert got.tobytes() == want.tobytes(), (name, hint, _mismatch_report(got, want))
         assert np.array_equal(cnt, wcnt), (name, hint)
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, w["unit_log2"], hint, counts=True,
+                                 v8=True)
+        want8 = R.verdict8_of(want)
+        assert got.tobytes() == want8.tobytes(), (name, hint, _mismatch_report(got, want8))
+        assert np.array_equal(cnt, wcnt), (name, hint, "v8")
 
 
 @pytest.mark.parametrize("variant", R.KERNEL_VARIANTS, ids=lambda v: "v" + "-".join(map(str, v)))
@@ -154,9 +168,12 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     ctx.tune(*variant)
     try:
         got = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 0)
+        got8 = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 0, v8=True)
     finally:
         ctx.tune(0)
     assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
+    want8 = R.verdict8_of(want)
+    assert got8.tobytes() == want8.tobytes(), (variant, "v8", _mismatch_report(got8, want8))
 
 
 @pytest.mark.parametrize("variant", [(1, 4, 1, 12), (1, 4, 1, 14)])

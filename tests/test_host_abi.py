@@ -21,6 +21,7 @@ def _declared(header_path):
     src = open(header_path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"#define[^\n]*", "", src)
+    src = re.sub(r"^static inline[^{]*\{.*?^\}", "", src, flags=re.S | re.M)  # header-only helpers
     names = re.findall(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", src, flags=re.M)
     return sorted(set(n for n in names if n not in ("if", "while", "sizeof")))
 

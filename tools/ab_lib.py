@@ -20,7 +20,7 @@ for r in range(rounds):
         if lib:
             env["RXGPU_LIB"] = lib
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wls, "--no-cpu",
-               "--no-cfg1", "--no-sockrate", "--no-tx", "--parity-sample", "256", "--steps", "50"]
+               "--no-cfg1", "--no-sockrate", "--no-tx", "--no-v8", "--parity-sample", "256", "--steps", "50"]
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         if p.returncode != 0:
             print(p.stderr[-3000:])

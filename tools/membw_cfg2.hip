@@ -22,7 +22,8 @@
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int MODE, int U> // MODE 0 = R, 1 = RD, 2 = RDW (nt store), 3 = RDW (plain store)
+template <int MODE, int U> // MODE 0 = R, 1 = RD, 2 = RDW (nt store), 3 = RDW (plain store),
+                           // 4 = RDW8 (8-B nt store), 5 = RDW4 (4-B nt store)
 __global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
                                               const unsigned *__restrict__ off,
                                               const unsigned short *__restrict__ len, size_t n,
@@ -56,6 +57,11 @@ __global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
             if (MODE >= 2 && f < n) {
                 if (MODE == 2)
                     __builtin_nontemporal_store(r, out + f);
+                else if (MODE == 4)
+                    __builtin_nontemporal_store((unsigned long long)r.x | ((unsigned long long)r.y << 32),
+                                                reinterpret_cast<unsigned long long *>(out) + f);
+                else if (MODE == 5)
+                    __builtin_nontemporal_store(r.x ^ r.z, reinterpret_cast<unsigned *>(out) + f);
                 else
                     out[f] = r;
             } else {
@@ -113,6 +119,10 @@ int main() {
         run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
         run<2, 4>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
         run<3, 2>("RDWp", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+        run<4, 1>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
+        run<4, 2>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
+        run<5, 1>("RDW4", fr, off, len, n, out, sink, cu, bpc, r + d + w / 4);
+        run<5, 2>("RDW4", fr, off, len, n, out, sink, cu, bpc, r + d + w / 4);
     }
     printf("(cfg2 algorithmic bytes per launch: %.3f GB)\n", (r + d + w) / 1e9);
     return 0;
