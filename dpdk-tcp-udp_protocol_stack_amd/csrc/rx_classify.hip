@@ -1704,14 +1704,22 @@ hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_
 // chunk reads as thread 255's, whose k is then out of range or past its
 // capture, masked).  A frame's
 // tail sum is the prefix difference at two chunk boundaries known from the
-// descriptors: [64, caplen & ~15).  After the stream the owner parses its head
-// from LDS, probes the flow table and writes the verdict.  Exact, with
-// fallbacks that are rare in real bursts:
+// descriptors: [64, caplen & ~15).  The partial last chunk of a frame (caplen
+// not a multiple of 16) is captured from the stream as well: its owner marks
+// it in the map, and the streaming lane writes it to slot 0 of the owner's
+// head slots, whose chunk 0 is not kept (the parse needs only its ether type,
+// which that lane publishes as a 2-bit class).  So nothing is loaded per frame
+// at the block start (a 16-B load there fetched a line that the L2 had evicted
+// again before the stream reached it: 3.6M extra L2 misses and 5% of the cfg4
+// time, pipe 264 ablation, profiles/r03e).  After the stream the owner parses
+// its head from LDS, sums its partial chunk, probes the flow table and writes
+// the verdict.  Exact, with fallbacks that are rare in real bursts:
 //  - the L4 sum ends before the capture (14 + total_length < caplen, e.g.
 //    Ethernet padding): the owner re-sums [64, end) from HBM;
-//  - frames sharing head chunks (overlapping descriptors): the losers of the
-//    map write read their heads from HBM after the stream (checked after the
-//    map barrier);
+//  - frames sharing head or partial chunks (overlapping descriptors): the
+//    losers of the map write read those from HBM after the stream (checked
+//    after the map barrier), as do captures under 14 bytes (a class cannot
+//    mask an ether type cut by the capture);
 //  - a span of scattered frames or one larger than the map (SH_MAPC chunks):
 //    per-thread head loads and tail loops.
 // LDS 31.9 KiB per block (map 7.25, heads 16, prefixes 8): 5 blocks per CU.
@@ -1766,8 +1774,9 @@ __device__ __forceinline__ sh_head sh_parse(const uint4 (&c)[4], int32_t cp) {
     return h;
 }
 
-// ABL (diagnostic builds, pipe 160): 1 = no flow-table probe (flow id from the
-// port: wrong verdicts by construction).  PW: slots of the first probe window
+// ABL (diagnostic builds, pipes 160 / 264): 1 = no flow-table probe (flow id
+// from the port; wrong verdicts by construction), 2 = every partial last
+// chunk loaded from HBM after the stream (no partial marks).  PW: slots of the first probe window
 // (1, 2 or 4 consecutive slots of the hashed table loaded together; the table
 // mirrors its first slots past its end), so a displaced key costs no dependent
 // second round trip at the end of the block (pipes 60 / 63 / 64).
@@ -1787,8 +1796,9 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     __shared__ __attribute__((aligned(16))) uint8_t s_map[MAPC];
     __shared__ __attribute__((aligned(16))) uint4 s_hd[256 * 4];
     __shared__ uint16_t s_rel[256]; // each frame's first chunk in the span
+    __shared__ uint32_t s_et[16];   // each frame's ether-type class, 2 bits (1 IPv4, 2 ARP)
     __shared__ unsigned long long s_lo, s_hi;
-    __shared__ uint32_t s_tail;
+    __shared__ uint32_t s_tail, s_pk255; // thread 255's partial chunk (an unmarked chunk reads as 255)
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
@@ -1796,7 +1806,9 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         s_lo = ~0ull;
         s_hi = 0;
         s_tail = 0;
+        s_pk255 = ~0u;
     }
+    if (tid < 16) s_et[tid] = 0;
     {
         uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
         for (uint32_t i = tid; i < MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -1810,8 +1822,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     const uint64_t fc = fpos >> 4;                  // first chunk (absolute)
     const uint32_t nch = ((uint32_t)cp + 15u) >> 4; // chunks of the capture
     const int32_t cf = cp & ~15;                    // full chunks: [0, cf)
-    // the partial last chunk past the head (descriptor-derived), used after the stream
-    const uint4 pcv = ldg16<false>(fb + (cf < cp && cf >= 64 ? cf : 0));
+    const bool part = cf >= 64 && cf < cp;          // a partial last chunk past the head
     __syncthreads(); // s_lo/s_hi/s_tail and the map initialised
     span_add(cp > 0, fc, fc + nch, &s_lo, &s_hi, &s_tail, lane);
     __syncthreads();
@@ -1834,12 +1845,23 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     if (streamed) {
         for (uint32_t k = 0; k < nh; ++k) s_map[rel + k] = (uint8_t)tid;
         s_rel[tid] = (uint16_t)rel;
+        if (part && !(ABL & 2)) {
+            s_map[rel + ((uint32_t)cf >> 4)] = (uint8_t)tid;
+            if (tid == 255) s_pk255 = (uint32_t)cf >> 4;
+        }
     }
     __syncthreads(); // map complete
-    bool direct = !streamed && cp > 0;
-    if (streamed)
+    const uint32_t pk255 = __builtin_amdgcn_readfirstlane(s_pk255);
+    // heads from HBM after the stream: not streamed, a shared head chunk, or
+    // an ether type cut by the capture; the partial chunk from HBM: not
+    // streamed is summed from HBM anyway, a lost mark
+    bool direct = cp > 0 && (!streamed || cp < 14);
+    bool plost = false;
+    if (streamed) {
         for (uint32_t k = 0; k < nh; ++k)
             if (s_map[rel + k] != (uint8_t)tid) direct = true; // shared head chunk
+        plost = part && ((ABL & 2) || s_map[rel + ((uint32_t)cf >> 4)] != (uint8_t)tid);
+    }
 
     // ---- flow probe loads: the port entry (UDP: the direct port table; TCP:
     // the listener) and the hashed table's home slot, issued once per frame
@@ -1863,9 +1885,13 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
 #pragma unroll
         for (int w = 0; w < PW; ++w) sw[w] = ld_slot(sp0 + (hash0 ? w : 0));
     };
+    // chunk 0 stands in by its ether type (the class the stream published);
+    // slot 0 holds the partial last chunk
     auto head_of = [&](uint4 (&c)[4]) {
+        const uint32_t ec = (s_et[tid >> 4] >> (2u * (tid & 15u))) & 3u;
+        c[0] = make_uint4(0, 0, 0, ec == 1u ? 0x0008u : (ec == 2u ? 0x0608u : 0u));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = chunk_below(s_hd[tid * 4u + k], 16 * k, cp);
+        for (int k = 1; k < 4; ++k) c[k] = chunk_below(s_hd[tid * 4u + k], 16 * k, cp);
     };
 
     // ---- stream: tile prefixes, head capture, boundary pickup ---------------
@@ -1880,9 +1906,17 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
             const uint32_t k = c0 + j * 256 + tid;
             sj[j] = k < span ? chunk_sum(v[j]) : 0u;
             xj[j] = sj[j];
-            if (k < span) { // (0xFF is thread 255 or no head: the k range tells)
+            if (k < span) { // (0xFF is thread 255 or no mark: the k range tells)
                 const uint32_t m = s_map[k], hk = k - s_rel[m];
-                if (hk < 4u) s_hd[m * 4u + hk] = v[j];
+                if (hk == 0u) { // chunk 0: its ether type, as a class
+                    const uint32_t et = v[j].w & 0xFFFFu;
+                    const uint32_t ec = et == 0x0008u ? 1u : (et == 0x0608u ? 2u : 0u);
+                    if (ec) atomicOr(&s_et[m >> 4], ec << (2u * (m & 15u)));
+                } else if (hk < 4u || m != 255u || hk == pk255) {
+                    // head chunks 1..3, or the owner's partial chunk (the only
+                    // other chunk it marks) into slot 0
+                    s_hd[m * 4u + (hk < 4u ? hk : 0u)] = v[j];
+                }
             }
         }
         wave_incl_scan_n<LPT>(xj);
@@ -1932,16 +1966,16 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     }
 
     // ---- head: parse, checksum, probe, verdict ------------------------------------
+    uint4 c[4];
+    head_of(c);
     if (__ballot(direct) != 0ull) { // rare (wave-uniform branch): heads from HBM
         uint4 hd[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) hd[k] = ldg16<false>(direct && 16 * k < cp ? fb + 16 * k : pkts);
         if (direct)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) s_hd[tid * 4u + k] = hd[k];
+            for (int k = 0; k < 4; ++k) c[k] = chunk_below(hd[k], 16 * k, cp);
     }
-    uint4 c[4];
-    head_of(c);
     issue_probe(c);
     const sh_head h = sh_parse(c, cp);
     uint4 h1 = c[1], h2 = c[2], h3 = c[3];
@@ -1956,11 +1990,18 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     acc = lane_chunk_sum(acc, h3, 48, e);
     if (h.do_sum) acc += (h.proto << 8) + rx_bswap16(h.l4n); // pseudo-header words
     // the sum ends where the capture does (the common case): tail from the
-    // stream prefixes, the partial chunk from pcv; otherwise re-sum from HBM
+    // stream prefixes, the partial chunk from its slot; otherwise re-sum from HBM
     if (h.do_sum && e > 64) {
         if (streamed && e == cp) {
             if (tailf) acc += ee - es;
-            if (cf < cp && cf >= 64) acc = lane_chunk_sum(acc, pcv, cf, e);
+            if (part) {
+                uint4 pv = s_hd[tid * 4u];
+                if (__ballot(plost) != 0ull) { // rare (wave-uniform branch): lost mark
+                    const uint4 ph = ldg16<false>(plost ? fb + cf : pkts);
+                    if (plost) pv = ph;
+                }
+                acc = lane_chunk_sum(acc, pv, cf, e);
+            }
         } else {
             for (int32_t s = 64; s < e; s += 16) acc = lane_chunk_sum(acc, ldg16<false>(fb + s), s, e);
         }
@@ -2419,6 +2460,9 @@ static const variant_entry k_variants[] = {
     // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
     {0, 1, 1, 63, launch_sh<0, 2>}, {0, 1, 1, 64, launch_sh<0, 4>},
+    // 264: 64 with every partial last chunk loaded from HBM after the stream
+    // (no partial marks; diagnostic)
+    {0, 1, 1, 264, launch_sh<2, 4>},
 };
 
 } // namespace

@@ -369,14 +369,20 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
 
 
 @pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 54)])
-@pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix"])
+@pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix", "dirty_gaps", "reversed",
+                                  "empty"])
 def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
     """the SH stream kernel's exact fallbacks, against the oracle: frames whose
     L4 sum ends before the capture (random bytes after the IP datagram, as
     Ethernet padding), descriptors sharing or overlapping head chunks
-    (duplicates, and starts 16 B into another frame), and blocks whose span
-    exceeds the head map (jumbo frames among IMIX ones)"""
-    rng = np.random.default_rng({"padded": 1, "overlap": 2, "jumbo_mix": 3}[case])
+    (duplicates, and starts 16 B into another frame), blocks whose span
+    exceeds the head map (jumbo frames among IMIX ones); and the partial last
+    chunk summed inside the stream: random bytes in every gap between frames
+    (64-B slots, so the masked bytes of a partial chunk and whole unowned
+    chunks are garbage), frames in decreasing buffer order and empty frames
+    (blocks that are not in increasing order load the partial chunk instead)"""
+    rng = np.random.default_rng({"padded": 1, "overlap": 2, "jumbo_mix": 3, "dirty_gaps": 4,
+                                 "reversed": 5, "empty": 6}[case])
     cfg = rxdist.gen_cfg("cfg4", n_udp=400, n_tcp=400)
     udp, tcb = R.gen_flows(cfg)
     pk, off, ln = R.gen_host(cfg, 77, 3000, 6)
@@ -391,7 +397,18 @@ def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
         for k, j in enumerate(jumbo):  # 40 jumbo frames over the first blocks
             frames.insert(37 * k + 5, j)
         tcb = np.concatenate([tcb, R.gen_flows(jcfg)[1]])
-    buf, off, lens = F.pack_frames(frames, 4)
+    elif case == "empty":
+        frames = [b"" if rng.random() < 0.02 else f for f in frames]
+    ul = 6 if case == "dirty_gaps" else 4
+    buf, off, lens = F.pack_frames(frames[::-1] if case == "reversed" else frames, ul)
+    if case == "reversed":  # frame i is the i-th from the end of the buffer
+        off, lens = off[::-1].copy(), lens[::-1].copy()
+    if case == "dirty_gaps":
+        own = np.zeros(len(buf), bool)
+        for o, l in zip(off, lens):
+            own[(int(o) << ul):(int(o) << ul) + int(l)] = True
+        buf = buf.copy()
+        buf[~own] = rng.integers(0, 256, int((~own).sum()), np.uint8)
     if case == "overlap":
         off, lens = off.copy(), lens.copy()
         for i in range(1, len(off), 7):
@@ -401,14 +418,16 @@ def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
                 off[i] = off[i - 1] + 1
                 lens[i] = max(int(lens[i - 1]) - 16, 0)
     ctx.flows_sync(udp, tcb)
-    want, wcnt = O.Tables(udp, tcb).classify(buf, off, lens, 4, counts=True)
+    want, wcnt = O.Tables(udp, tcb).classify(buf, off, lens, ul, counts=True)
     ctx.tune(*variant)
     try:
-        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 354, counts=True)
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, ul, 354, counts=True)
+        got8 = _dev_classify(torch_dev, ctx, buf, off, lens, ul, 354, v8=True)
     finally:
         ctx.tune(0)
     assert got.tobytes() == want.tobytes(), (variant, case, _mismatch_report(got, want))
     assert np.array_equal(cnt, wcnt), (variant, case)
+    assert got8.tobytes() == R.verdict8_of(want).tobytes(), (variant, case, "v8")
 
 
 def test_fuzzed_frames_match_oracle(ctx, torch_dev):

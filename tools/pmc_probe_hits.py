@@ -4,7 +4,8 @@ counters of the classify kernel with the probe (SH, pipe 64) and without it
 (the no-probe ablation, pipe 160: the flow id from the port, wrong verdicts
 by construction), one rocprofv3 --pmc pass each, nothing else collected.
 The differences are the probes' own requests, hits and misses.
-Run on the GPU box:  python tools/pmc_probe_hits.py [workload] [tag]"""
+Run on the GPU box:  python tools/pmc_probe_hits.py [workload] [tag] [ablation pipe]
+(ablation pipe 264: without the partial-last-chunk load instead of the probe)"""
 import csv
 import glob
 import json
@@ -25,7 +26,7 @@ def collect(workload, variant, outdir):
     r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, TMPDIR="/tmp"), capture_output=True,
                        text=True, timeout=240)
     # the ablation's verdicts are wrong by construction: bench.py exits 3 on them
-    if r.returncode not in ((0, 3) if variant.endswith(",160") else (0,)):
+    if r.returncode not in ((0, 3) if int(variant.split(",")[-1]) >= 100 else (0,)):
         sys.stderr.write(r.stdout[-3000:] + r.stderr[-3000:])
         raise SystemExit(r.returncode)
     vals = {c: [] for c in COUNTERS}
@@ -44,7 +45,8 @@ def main():
     tag = sys.argv[2] if len(sys.argv) > 2 else "r03"
     outdir = os.path.join(ROOT, "gpurun_out")
     res = {"workload": w, "counters": COUNTERS, "per_dispatch_median": {}}
-    for name, v in (("probe", "0,1,1,64"), ("no_probe", "0,1,1,160")):
+    abl = sys.argv[3] if len(sys.argv) > 3 else "160"
+    for name, v in (("probe", "0,1,1,64"), ("no_probe", "0,1,1," + abl)):
         res["per_dispatch_median"][name] = collect(w, v, outdir)
         print(name, res["per_dispatch_median"][name], flush=True)
     a, b = res["per_dispatch_median"]["probe"], res["per_dispatch_median"]["no_probe"]
@@ -54,7 +56,8 @@ def main():
     res["probe_hit_rate"] = dhit / dreq if dreq > 0 else None
     res["kernel_hit_rate"] = a["TCC_HIT_sum"] / max(a["TCC_REQ_sum"], 1.0)
     print(json.dumps(res), flush=True)
-    with open(os.path.join(outdir, f"pmc_probe_hits_{w}_{tag}.json"), "w") as fh:
+    res["ablation_pipe"] = int(abl)
+    with open(os.path.join(outdir, f"pmc_probe_hits_{w}_{tag}_{abl}.json"), "w") as fh:
         json.dump(res, fh, indent=1)
 
 
