@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
         const bool tail = ef > 64;
         const uint64_t cs_abs = (fpos + 64) >> 4, ce_abs = (fpos + (uint32_t)ef) >> 4;
         // the last partial chunk (consumed after the stream) and the first probe slot
-        const uint4 pc = ldg16<false>(fb + (part ? ef : 0));
+        const uint4 pc = (ABL & 8) ? make_uint4(0, 0, 0, 0) : ldg16<false>(fb + (part ? ef : 0));
         const bool probe = valid && l4;
         const uint32_t ka = is_udp ? dip : sip;
         const uint32_t kb = is_udp ? dport : dip;
@@ -2088,10 +2088,11 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         vd.y = (poff & 0xFFFFu) | (plen << 16);
         vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
+        if constexpr ((ABL & 32) != 0) put_count_idx_wave(ft, p, cidx, lane); // (diagnostic order)
         st_verdict(ft, out, p, vd);
         lane_count(cidx, counts, hist, lds_bins);
     }
-    put_count_idx_wave(ft, p, cidx, lane);
+    if constexpr ((ABL & 48) == 0) put_count_idx_wave(ft, p, cidx, lane);
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -2456,6 +2457,10 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
     {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, true>},
+    // ablations of pipe 38 (the jumbo default): no head loads (438), no
+    // partial-chunk load (838), neither (1238)
+    {0, 1, 1, 438, launch_stream<true, 4, 3, 1, true>}, {0, 1, 1, 838, launch_stream<true, 8, 3, 1, true>},
+    {0, 1, 1, 1238, launch_stream<true, 12, 3, 1, true>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
@@ -2463,6 +2468,9 @@ static const variant_entry k_variants[] = {
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
     {0, 1, 1, 264, launch_sh<2, 4>},
+    // 1064: 64 without the count-index store; 2064: 64 with the count index
+    // stored before the verdict (diagnostics; the counts of 1064 are wrong)
+    {0, 1, 1, 1064, launch_sh<16, 4>}, {0, 1, 1, 2064, launch_sh<32, 4>},
 };
 
 } // namespace
