@@ -14,12 +14,13 @@ step() { local name=$1 t=$2; shift 2; echo "== $name: $*"; date +%T; timeout -k 
 step pytest_gpu 420 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread || exit $?
 step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 export TMPDIR=/tmp
+timeout -k 10 60 tools/membw_cfg2 > $OUT/membw_cfg2.log 2>&1 && grep "RDW   U=2 bpc=2" $OUT/membw_cfg2.log
 step pmc 900 python tools/pmc_traffic.py $TAG cfg2,cfg3,cfg4,cfg5 || exit $?
 cp $OUT/pmc_$TAG.json profiles/pmc_$TAG.json || exit 1
 step bench 420 python bench.py --steps $STEPS --warmup 5 --e2e ${BENCH_ARGS:-} || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench_$TAG.json || true
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-    -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu --no-sockrate || exit $?
+    -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu --no-sockrate --no-v8 || exit $?
 f=$(find $OUT/prof_$TAG -name '*kernel_trace.csv' | head -1)
 [ -n "$f" ] && python tools/trace_durations.py "$f" > $OUT/trace_durations_$TAG.txt
 # N = 2 rehearsal of the split path: two ranks on this one GPU (gloo carries
@@ -31,7 +32,7 @@ grep '^{' $OUT/n2.log > $OUT/bench_n2_$TAG.json || true
 # the SQ counters of the cfg3 kernel, for the roofline comparison on one box
 if [ "${CEIL:-0}" = 1 ]; then
   step membw 300 ./tools/membw_large || exit $?
-  step sq_cfg3 400 python tools/pmc_counters.py $TAG cfg3 "--no-tx --no-sockrate --no-cfg1" \
+  step sq_cfg3 400 python tools/pmc_counters.py $TAG cfg3 "--no-tx --no-sockrate --no-cfg1 --no-v8" \
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
     "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" || exit $?
 fi

@@ -21,7 +21,7 @@ def collect(workload, variant, outdir):
     d = os.path.join(outdir, f"pmc_hits_{workload}_{variant.replace(',', '-')}")
     cmd = ["rocprofv3", "--pmc", *COUNTERS, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "3",
-           "--warmup", "1", "--no-cpu", "--no-cfg1", "--no-sockrate", "--no-tx",
+           "--warmup", "1", "--no-cpu", "--no-cfg1", "--no-sockrate", "--no-tx", "--no-v8",
            "--parity-sample", "0", "--variant", variant]
     r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, TMPDIR="/tmp"), capture_output=True,
                        text=True, timeout=240)

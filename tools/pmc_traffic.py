@@ -24,7 +24,7 @@ def collect(workload, counter, outdir, variant=""):
     d = os.path.join(outdir, f"pmc_{workload}_{counter}{'_' + variant.replace(',', '-') if variant else ''}")
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "3",
-           "--warmup", "1", "--no-cpu", "--no-cfg1", "--no-sockrate", "--parity-sample", "0"]
+           "--warmup", "1", "--no-cpu", "--no-cfg1", "--no-sockrate", "--no-v8", "--parity-sample", "0"]
     if variant:  # a forced kernel variant (tuning comparisons)
         cmd += ["--variant", variant]
     env = dict(os.environ, TMPDIR="/tmp")
