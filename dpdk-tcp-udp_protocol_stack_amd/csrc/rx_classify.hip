@@ -810,7 +810,7 @@ __device__ __forceinline__ void lane_count(uint32_t idx, unsigned long long *__r
 // indices past n never, so the last wave's pieces may cover frames >= n (the
 // index buffer has room for 4 B per frame, rounded to 256 B).
 __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t p, uint32_t idx,
-                                                   uint32_t lane) {
+                                                   uint32_t lane, uint32_t lim = 64) {
     if (!ft.count_idx) return;
     if (ft.count_ffff) count_ffff(ft, idx);
     if (ft.cidx16) {
@@ -822,7 +822,7 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
         const uint32_t x5 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x105, 0xF, 0xF, false));
         const uint32_t x6 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x106, 0xF, 0xF, false));
         const uint32_t x7 = pin(__builtin_amdgcn_update_dpp(0u, v, 0x107, 0xF, 0xF, false));
-        if ((lane & 7u) == 0u) {
+        if ((lane & 7u) == 0u && lane < lim) {
             const rx_u32x4 w = {v | (x1 << 16), x2 | (x3 << 16), x4 | (x5 << 16), x6 | (x7 << 16)};
             st_stream16(reinterpret_cast<rx_u32x4 *>(static_cast<uint16_t *>(ft.count_idx) + p), w);
         }
@@ -830,7 +830,7 @@ __device__ __forceinline__ void put_count_idx_wave(const rx_ft_dev &ft, uint64_t
         const uint32_t x1 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x101, 0xF, 0xF, false));
         const uint32_t x2 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x102, 0xF, 0xF, false));
         const uint32_t x3 = pin(__builtin_amdgcn_update_dpp(0u, idx, 0x103, 0xF, 0xF, false));
-        if ((lane & 3u) == 0u) {
+        if ((lane & 3u) == 0u && lane < lim) {
             const rx_u32x4 w = {idx, x1, x2, x3};
             st_stream16(reinterpret_cast<rx_u32x4 *>(static_cast<uint32_t *>(ft.count_idx) + p), w);
         }
@@ -1317,8 +1317,11 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
+// FPB: frames per block (256, or 128 / 64 / 32 with the other threads streaming
+// only: shorter blocks for jumbo frames, whose 256-frame blocks stream 2.3 MB
+// each and leave the last round of blocks a fraction of the chip)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false>
+          bool HG = false, uint32_t FPB = 256>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1350,8 +1353,9 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     // frame: PMC r02g.)
     {
         const uint64_t tile = blockIdx.x;
-        const uint64_t p = tile * 256 + tid;
-        const bool valid = p < n;
+        static_assert(FPB == 256 || FPB == 128 || FPB == 64 || FPB == 32, "frames per block");
+        const uint64_t p = tile * FPB + tid;
+        const bool valid = tid < FPB && p < n;
         const uint64_t q = valid ? p : 0;
         const uint64_t fpos = (uint64_t)off[q] << unit_log2;
         const uint8_t *fb = pkts + fpos;
@@ -1666,7 +1670,8 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             st_verdict(ft, out, p, vd);
             lane_count(cidx, counts, hist, lds_bins);
         }
-        put_count_idx_wave(ft, p, cidx, lane);
+        // (FPB 32: the first half of wave 0; its other lanes' pieces are the next block's)
+        if (FPB >= 256 || wv * 64 < FPB) put_count_idx_wave(ft, p, cidx, lane, FPB < 64 ? FPB : 64);
     } // tile
     if (lds_bins) {
         __syncthreads();
@@ -1678,14 +1683,14 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
 }
 
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false>
+          bool HG = false, uint32_t FPB = 256>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
-    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    const uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG, FPB>), dim3((uint32_t)blocks),
                        dim3(256), (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out,
                        counts, lds_bins);
     return hipGetLastError();
@@ -2461,6 +2466,10 @@ static const variant_entry k_variants[] = {
     // partial-chunk load (838), neither (1238)
     {0, 1, 1, 438, launch_stream<true, 4, 3, 1, true>}, {0, 1, 1, 838, launch_stream<true, 8, 3, 1, true>},
     {0, 1, 1, 1238, launch_stream<true, 12, 3, 1, true>},
+    // 338 / 538: pipe 38 with 128 / 64 frames per block
+    {0, 1, 1, 338, launch_stream<true, 0, 3, 1, true, false, false, 128>},
+    {0, 1, 1, 538, launch_stream<true, 0, 3, 1, true, false, false, 64>},
+    {0, 1, 1, 738, launch_stream<true, 0, 3, 1, true, false, false, 32>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
@@ -2497,9 +2506,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 1.0191 vs 1.0322 ms for pipe 0 (interleaved sweep, profiles/r03c/sweep_cfg3_wt.txt),
         // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt)
         *g = 8, *p = 2, *fpg = 2, *pipe = 40;
-    } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), the
-        // IMIX shape: pipe 38 vs 30 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms (r01g, r01j)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 38;
+    } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), pipe 38
+        // (vs 30: 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms, r01g, r01j) with 32 frames per block:
+        // 1.6746 vs 1.7833 ms for 256 (64: 1.6810, 128: 1.7139; profiles/r03f/sweep_cfg5_fpb.txt)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 738;
     }
 }
 

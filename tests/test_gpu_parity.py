@@ -302,7 +302,8 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
-                                     (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (4, 1, 2, 0)])
+                                     (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (4, 1, 2, 0),
+                                     (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
     frames shuffled inside each 256-frame block (streamed, unordered
@@ -359,13 +360,14 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
     d_ln = torch.from_numpy(ln.view(np.int16)).to(dev)
     d_cnt = torch.zeros(ctx.num_flows, dtype=torch.int64, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
-    for hint in (354, 1500):
+    hints = (354, 1500, 9000)  # the SH, group and jumbo stream kernels
+    for hint in hints:
         d_out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
         ctx.classify_dev(d_pk, d_off, d_ln, n, 6, hint, d_out, d_cnt, stream=sh)
         torch.cuda.synchronize(dev)
         got = d_out.cpu().numpy().view(R.VERDICT_DTYPE)
-        assert got.tobytes() == want.tobytes(), _mismatch_report(got, want)
-    assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 2 * wcnt)
+        assert got.tobytes() == want.tobytes(), (hint, _mismatch_report(got, want))
+    assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), len(hints) * wcnt)
 
 
 @pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 54)])
