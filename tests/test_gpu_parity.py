@@ -150,6 +150,32 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
         assert np.array_equal(cnt, wcnt), (name, hint, "v8")
 
 
+@pytest.mark.parametrize("shift", [0, 8])
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 4097, 40001])
+def test_verdict8_lane_pairs(ctx, torch_dev, n, shift):
+    """64-B frames (lane kernel, pipe 14) into 8-B verdicts: lane pairs store
+    16 B when the output is 16-B aligned (shift 0), one 8 B per frame when
+    it is only 8-B aligned (shift 8); odd bursts end on an unpaired frame.
+    Nothing is written outside [shift, shift + 8n)."""
+    torch, dev = torch_dev
+    cfg = rxdist.gen_cfg("cfg2")
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    pk, off, ln = R.gen_host(cfg, 777, n, 6)
+    want8 = R.verdict8_of(O.Tables(udp, tcb).classify(pk, off, ln, 6))
+    d_pk = torch.from_numpy(np.concatenate([pk, np.zeros(64, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_ln = torch.from_numpy(ln.view(np.int16)).to(dev)
+    d_out = torch.full((n * 8 + 32,), 0xAB, dtype=torch.uint8, device=dev)
+    ctx.classify_dev8(d_pk, d_off, d_ln, n, 6, 64, d_out.data_ptr() + shift, None,
+                      stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    o = d_out.cpu().numpy()
+    assert (o[:shift] == 0xAB).all() and (o[shift + n * 8:] == 0xAB).all(), "store outside the burst"
+    got = o[shift:shift + n * 8].view(R.VERDICT8_DTYPE)
+    assert got.tobytes() == want8.tobytes(), (n, shift, _mismatch_report(got, want8))
+
+
 @pytest.mark.parametrize("variant", R.KERNEL_VARIANTS, ids=lambda v: "v" + "-".join(map(str, v)))
 def test_every_kernel_variant(ctx, torch_dev, variant):
     """each compiled (lanes, passes, frames-per-group) variant, on mixed sizes"""
