@@ -1317,9 +1317,9 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // tile's barrier, which already orders them after their writes; s_pre and
 // s_wt are double-buffered, so the next writes to a buffer come a barrier
 // after its last reads)
-// FPB: frames per block (256, or 128 / 64 / 32 with the other threads streaming
-// only: shorter blocks for jumbo frames, whose 256-frame blocks stream 2.3 MB
-// each and leave the last round of blocks a fraction of the chip)
+// FPB: frames per block (256, or 128 / 64 / 32 / 16 with the other threads
+// streaming only: shorter blocks for jumbo frames, whose 256-frame blocks
+// stream 2.3 MB each and leave the last round of blocks a fraction of the chip)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
           bool HG = false, uint32_t FPB = 256>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
@@ -1353,7 +1353,8 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
     // frame: PMC r02g.)
     {
         const uint64_t tile = blockIdx.x;
-        static_assert(FPB == 256 || FPB == 128 || FPB == 64 || FPB == 32, "frames per block");
+        static_assert(FPB == 256 || FPB == 128 || FPB == 64 || FPB == 32 || FPB == 16,
+                      "frames per block");
         const uint64_t p = tile * FPB + tid;
         const bool valid = tid < FPB && p < n;
         const uint64_t q = valid ? p : 0;
@@ -1670,7 +1671,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             st_verdict(ft, out, p, vd);
             lane_count(cidx, counts, hist, lds_bins);
         }
-        // (FPB 32: the first half of wave 0; its other lanes' pieces are the next block's)
+        // (FPB < 64: the first FPB lanes of wave 0; its other lanes' pieces are the next block's)
         if (FPB >= 256 || wv * 64 < FPB) put_count_idx_wave(ft, p, cidx, lane, FPB < 64 ? FPB : 64);
     } // tile
     if (lds_bins) {
@@ -2470,6 +2471,10 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 338, launch_stream<true, 0, 3, 1, true, false, false, 128>},
     {0, 1, 1, 538, launch_stream<true, 0, 3, 1, true, false, false, 64>},
     {0, 1, 1, 738, launch_stream<true, 0, 3, 1, true, false, false, 32>},
+    // 938: 738 with 16 frames per block; 739: pipe 39 (probe consumed before the
+    // stream) with 32
+    {0, 1, 1, 938, launch_stream<true, 0, 3, 1, true, false, false, 16>},
+    {0, 1, 1, 739, launch_stream<true, 0, 0, 1, true, false, false, 32>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
@@ -2507,9 +2512,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt)
         *g = 8, *p = 2, *fpg = 2, *pipe = 40;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), pipe 38
-        // (vs 30: 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms, r01g, r01j) with 32 frames per block:
-        // 1.6746 vs 1.7833 ms for 256 (64: 1.6810, 128: 1.7139; profiles/r03f/sweep_cfg5_fpb.txt)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 738;
+        // (vs 30: 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms, r01g, r01j) with 16 frames per block:
+        // 32 frames 1.6746 vs 1.7833 ms for 256 (64: 1.6810, 128: 1.7139; profiles/r03f/sweep_cfg5_fpb.txt),
+        // 16 frames 1.6521-1.6595 vs 1.6735-1.6805 for 32 (8: 1.7300; profiles/r03j)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 938;
     }
 }
 

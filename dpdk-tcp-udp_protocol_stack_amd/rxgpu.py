@@ -64,7 +64,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
                    (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
                    (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
-                   (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738),  # 38: 128 / 64 / 32 frames per block
+                   (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),  # 38: 128 / 64 / 32 / 16 frames per block
+                   (0, 0, 0, 739),  # 39 with 32 frames per block
                    (0, 0, 0, 46),  # 38 with the span from the descriptors
                    (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
                    (0, 0, 0, 60),  # heads taken out of the block stream

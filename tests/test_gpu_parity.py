@@ -152,11 +152,12 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
 
 @pytest.mark.parametrize("shift", [0, 8])
 @pytest.mark.parametrize("n", [1, 2, 63, 65, 4097, 40001])
-def test_verdict8_lane_pairs(ctx, torch_dev, n, shift):
-    """64-B frames (lane kernel, pipe 14) into 8-B verdicts: lane pairs store
-    16 B when the output is 16-B aligned (shift 0), one 8 B per frame when
-    it is only 8-B aligned (shift 8); odd bursts end on an unpaired frame.
-    Nothing is written outside [shift, shift + 8n)."""
+def test_verdict8_odd_and_unaligned(ctx, torch_dev, n, shift):
+    """64-B frames (lane kernel, pipe 14) into 8-B verdicts, the output 16-B
+    aligned (shift 0) or only 8-B aligned as rxgpu.h allows (shift 8), bursts
+    of odd lengths (a lane-pair store variant was measured and dropped:
+    DESIGN.md, compact verdicts).  Nothing is written outside
+    [shift, shift + 8n)."""
     torch, dev = torch_dev
     cfg = rxdist.gen_cfg("cfg2")
     udp, tcb = R.gen_flows(cfg)
@@ -329,7 +330,8 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
                                      (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (4, 1, 2, 0),
-                                     (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738)])
+                                     (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),
+                                     (0, 0, 0, 739)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
     frames shuffled inside each 256-frame block (streamed, unordered
