@@ -1352,14 +1352,20 @@ int rxg_process_mbufs_udp(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdic
     const uint32_t nf = c->fs.udp.id_space();
     if (nf > RXG_COMPACT_MAX_FLOWS) return RXG_ERANGE;
     DEVGUARD(c);
-    if (!c->d_cp_dg) { // first use: results sized for a full staging slot
-        HIPCHK(hipMalloc(&c->d_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram)));
-        HIPCHK(hipMalloc(&c->d_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t)));
-        HIPCHK(hipMalloc(&c->d_cp_payload, c->max_bytes));
-        HIPCHK(hipMalloc(&c->d_cp_totals, 4 * sizeof(uint32_t)));
-        HIPCHK(hipHostMalloc((void **)&c->h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
-        HIPCHK(hipHostMalloc((void **)&c->h_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
-        HIPCHK(hipHostMalloc((void **)&c->h_cp_payload, c->max_bytes, 0));
+    if (!c->h_cp_totals) { // first use: results sized for a full staging slot
+        // (h_cp_totals is set last: a failed allocation leaves the set
+        // incomplete and the next call retries the missing pieces)
+        if (!c->d_cp_dg) HIPCHK(hipMalloc(&c->d_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram)));
+        if (!c->d_cp_first)
+            HIPCHK(hipMalloc(&c->d_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t)));
+        if (!c->d_cp_payload) HIPCHK(hipMalloc(&c->d_cp_payload, c->max_bytes));
+        if (!c->d_cp_totals) HIPCHK(hipMalloc(&c->d_cp_totals, 4 * sizeof(uint32_t)));
+        if (!c->h_cp_dg)
+            HIPCHK(hipHostMalloc((void **)&c->h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
+        if (!c->h_cp_first)
+            HIPCHK(hipHostMalloc((void **)&c->h_cp_first,
+                                 (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
+        if (!c->h_cp_payload) HIPCHK(hipHostMalloc((void **)&c->h_cp_payload, c->max_bytes, 0));
         HIPCHK(hipHostMalloc((void **)&c->h_cp_totals, 4 * sizeof(uint32_t), 0));
     }
     *dgram = c->h_cp_dg;
