@@ -928,14 +928,16 @@ static void tcp_enqueue_rcv(struct tcp_stream *s, const uint8_t *f, uint32_t cap
     fr->sport = ntohs(cap >= 36 ? rd16(f + 34) : 0);
     const int plen = tcplen - (int)hl * 4;
     if (plen > 0) {
-        fr->data = calloc(1, (size_t)plen + 1);
+        fr->data = malloc((size_t)plen + 1);
         if (!fr->data) {
             free(fr);
             return;
         }
         const uint32_t from = 34 + hl * 4;
         const uint32_t avail = cap > from ? cap - from : 0;
-        memcpy(fr->data, f + from, (uint32_t)plen < avail ? (uint32_t)plen : avail);
+        const uint32_t ncopy = (uint32_t)plen < avail ? (uint32_t)plen : avail;
+        memcpy(fr->data, f + from, ncopy);
+        memset(fr->data + ncopy, 0, (size_t)plen + 1 - ncopy); /* past the capture, and a NUL */
         fr->length = (uint32_t)plen;
     }
     pthread_mutex_lock(&s->mutex);
