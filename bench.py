@@ -53,6 +53,37 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _deadline_arg(argv):
+    """--deadline S (seconds) from the command line; default from the
+    workload list: 120 s + 120 s per workload (a healthy N-rank run of the
+    default four workloads takes a few minutes at most)"""
+    wl = "cfg2,cfg3,cfg4,cfg5"
+    for k, a in enumerate(argv):
+        if a == "--deadline" and k + 1 < len(argv):
+            return float(argv[k + 1])
+        if a.startswith("--deadline="):
+            return float(a.split("=", 1)[1])
+        if a == "--workload" and k + 1 < len(argv):
+            wl = argv[k + 1]
+        elif a.startswith("--workload="):
+            wl = a.split("=", 1)[1]
+    return 120.0 + 120.0 * len([w for w in wl.split(",") if w.strip()])
+
+
+def stage(rank, what):
+    """this rank's progress: a line on stderr, and (under launch_ranks) the
+    rank's stage file, which the launcher prints if the run outlives its
+    deadline, so a hang names the stage it stopped in"""
+    print(f"bench: rank {rank}: stage {what}", file=sys.stderr, flush=True)
+    d = os.environ.get("BENCH_STAGE_DIR")
+    if d:
+        try:
+            with open(os.path.join(d, f"rank{rank}"), "w") as f:
+                f.write(what)
+        except OSError:
+            pass
+
+
 def launch_ranks(n: int, argv) -> int:
     """`bench.py --gpus N` with no launcher: start N rank processes of this
     script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set), as
@@ -60,14 +91,22 @@ def launch_ranks(n: int, argv) -> int:
     before torch or librxgpu is imported, so this process never touches the
     GPU (children are started, never exec'd).  Rank 0 prints the JSON line on
     the inherited stdout.  When a rank fails, the others get 60 s to finish
-    and are then terminated (a peer stuck in a barrier would wait forever)."""
+    and are then terminated (a peer stuck in a barrier would wait forever).
+    The whole run has a wall-clock deadline (--deadline, default from the
+    workload list): past it every rank still running is terminated (killed
+    10 s later), each rank's last stage is printed, and the exit code is 124."""
+    import shutil
     import subprocess
+    import tempfile
     import time as _t
+    deadline_s = _deadline_arg(argv)
+    stage_dir = tempfile.mkdtemp(prefix="bench_stage_")
     env0 = dict(os.environ)
     env0.setdefault("MASTER_ADDR", "127.0.0.1")
     env0.setdefault("MASTER_PORT", str(_free_port()))
     env0["WORLD_SIZE"] = str(n)
     env0["LOCAL_WORLD_SIZE"] = str(n)
+    env0["BENCH_STAGE_DIR"] = stage_dir
     env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     procs = []
     for r in range(n):
@@ -75,22 +114,47 @@ def launch_ranks(n: int, argv) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                                       env=env))
     print(f"bench: launched {n} ranks (pids {[p.pid for p in procs]}, "
-          f"MASTER {env0['MASTER_ADDR']}:{env0['MASTER_PORT']})", file=sys.stderr, flush=True)
-    deadline = None
+          f"MASTER {env0['MASTER_ADDR']}:{env0['MASTER_PORT']}, deadline {deadline_s:.0f} s)",
+          file=sys.stderr, flush=True)
+    t_end = _t.monotonic() + deadline_s
+    grace = None    # a rank failed: the others' time to finish
+    kill_at = None  # terminated: SIGKILL for whoever is left at this time
+    timed_out = False
     while True:
         rcs = [p.poll() for p in procs]
         if all(rc is not None for rc in rcs):
             break
-        if deadline is None and any(rc not in (None, 0) for rc in rcs):
-            deadline = _t.monotonic() + 60.0
-        if deadline is not None and _t.monotonic() > deadline:
+        now = _t.monotonic()
+        if not timed_out and now > t_end:
+            timed_out = True
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    try:
+                        with open(os.path.join(stage_dir, f"rank{r}")) as f:
+                            st = f.read()
+                    except OSError:
+                        st = "(none reported: before the rendezvous)"
+                    print(f"bench: deadline {deadline_s:.0f} s passed; rank {r} (pid {p.pid}) "
+                          f"still running, last stage: {st}", file=sys.stderr, flush=True)
+            grace = now  # terminate at once
+        if grace is None and any(rc not in (None, 0) for rc in rcs):
+            grace = now + 60.0
+        if grace is not None and kill_at is None and now >= grace:
             for p in procs:
                 if p.poll() is None:
                     p.terminate()
-            deadline = _t.monotonic() + 1e9
+            kill_at = now + 10.0
+        if kill_at is not None and now > kill_at:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            kill_at = float("inf")
         _t.sleep(0.2)
+    shutil.rmtree(stage_dir, ignore_errors=True)
     rcs = [p.returncode for p in procs]
     print(f"bench: rank exit codes {rcs}", file=sys.stderr, flush=True)
+    if timed_out:
+        return 124
     bad = [rc for rc in rcs if rc != 0]
     return 0 if not bad else (bad[0] if bad[0] > 0 else 128 - bad[0])
 
@@ -140,7 +204,7 @@ def collective_fn(group, nccl_group, nflows):
 
 
 def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_sample=4096,
-                 oracle_threads=1):
+                 oracle_threads=1, shard_mode="direct"):
     w = rxdist.WORKLOADS[name]
     cfg = rxdist.gen_cfg(name)
     ul = w["unit_log2"]
@@ -150,7 +214,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     t_setup = time.perf_counter()
-    pk, off, ln, n, gidx = rxdist.build_shard(ctx, name, rank, world, dev, stream)
+    pk, off, ln, n, gidx, gcfg = rxdist.build_shard(ctx, name, rank, world, dev, stream,
+                                                    shard_mode)
     t_setup = time.perf_counter() - t_setup
     out = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=dev)
     counts = torch.zeros(max(nflows, 1), dtype=torch.int64, device=dev)
@@ -209,6 +274,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     # timed steps (back-to-back launches).  Per-step event pairs cost ~3 us of
     # GPU idle each between bursts (0.2583 vs 0.2516 ms per step at cfg2, r02j)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    stage(rank, f"{name}: timed steps")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -251,6 +317,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         t = torch.tensor([el], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
+    kdisp = kernel_dispatches(ctx, pk, off, ln, n, ul, w["len_hint"], out, counts, stream, csh,
+                              dev, alg_bytes)
     # counts: every delivered verdict counted once per step, on every rank
     # after the all-reduce (the global histogram)
     v = out[:n * 16].view(n, 16)
@@ -263,6 +331,18 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         torch.distributed.all_reduce(t)
         n_ok_all = int(t.item())
     expect = n_ok_all * total_steps if COUNTS else None
+    # the count vector flow by flow: (all-reduced) counts == total_steps x the
+    # sum over ranks of each rank's histogram of its own delivered verdicts
+    # (UDP flow k -> k, TCP flow k -> nu + k), exchanged over the control plane
+    counts_match = None
+    if COUNTS:
+        ok = v[:, 11].view(torch.int8) == 0
+        fid = v[:, 0:4].contiguous().view(torch.int32).flatten().to(torch.int64)
+        cidx = torch.where(v[:, 10] == R.CLS_UDP, fid, fid + len(udp))[ok]
+        hist = torch.bincount(cidx, minlength=nflows)[:nflows].cpu()
+        if world > 1:
+            torch.distributed.all_reduce(hist)
+        counts_match = bool(torch.equal(counts.cpu(), hist * total_steps))
     kavg = float(np.mean(kms))
     n_all, alg_all = n, alg_bytes
     if world > 1:  # the whole job: frames and algorithmic bytes of every rank
@@ -276,7 +356,9 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         kernel_ms_avg=kavg,
         alg_bytes_per_launch=alg_bytes, frame_bytes=frame_bytes,
         rc0_frac=n_ok / max(n, 1), counts_ok=(expect is None or counted == expect),
+        counts_match=counts_match,
         setup_s=round(t_setup, 2), count_stream=bool(COUNTS and csh is not None),
+        shard_mode=shard_mode if world > 1 else None,
     )
     if world > 1:
         res["allreduce_ms"] = round(ar_ms, 4)
@@ -285,10 +367,12 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     achieved = alg_bytes / (kavg * 1e-3) / 1e9  # this rank's kernel (HIP events)
     res["roofline"] = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                            unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                           traffic=pmc_traffic(name) if world == 1 else None)
+                           traffic=pmc_traffic(name) if world == 1 else None,
+                           kernel=kdisp)
     # parity of this run: a seeded sample of the verdicts regenerated on the CPU
+    stage(rank, f"{name}: parity")
     t_par = time.perf_counter()
-    checked, bad, first_bad = parity_check(name, cfg, udp, tcb, out, n, gidx, ul,
+    checked, bad, first_bad = parity_check(name, gcfg, udp, tcb, out, n, gidx, ul,
                                            parity_sample, seed=1000 + rank,
                                            threads=oracle_threads)
     if world > 1:
@@ -302,7 +386,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     if first_bad:
         log(f"PARITY FAILURE {name}: {first_bad}")
     t_dg = time.perf_counter()
-    res["digest"] = burst_digest(name, out, n, gidx, counts, warmup + steps, rank, world)
+    res["digest"] = burst_digest(name, out, n, gidx, counts, warmup + steps, rank, world,
+                                 shard_mode)
     res["digest"]["seconds"] = round(time.perf_counter() - t_dg, 2)
     if res["digest"]["digest_ok"] is False:
         log(f"DIGEST MISMATCH {name}: {res['digest']}")
@@ -327,6 +412,40 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
+
+
+KDISP = 20  # dispatches of the per-dispatch pass (roofline.kernel)
+
+
+def kernel_dispatches(ctx, pk, off, ln, n, ul, len_hint, out, counts, stream, csh, dev, alg_bytes):
+    """roofline.kernel: the dominant kernel dispatch by dispatch, so that a
+    kernel trace of the same run (rocprofv3 --kernel-trace) can confirm it.
+    KDISP untimed classify dispatches after the timed steps, each between its
+    own HIP event pair on the kernel's stream, counts on (into a scratch
+    vector: the run's counts stay exact).  A dispatch measured alone includes
+    its ramp-up and drain, which back-to-back steps overlap with the next
+    dispatch, so its mean can exceed ms_per_step."""
+    name, variant = ctx.kernel_variant(len_hint)
+    scratch = torch.zeros_like(counts) if COUNTS else None
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(KDISP)]
+    torch.cuda.synchronize(dev)
+    for a, b in evs:
+        a.record(stream)
+        ctx.classify_dev(pk, off, ln, n, ul, len_hint, out, scratch, stream=stream.cuda_stream,
+                         count_stream=csh)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    t = sorted(a.elapsed_time(b) for a, b in evs)
+    mean = float(np.mean(t))
+    med = t[len(t) // 2]
+    del scratch
+    return dict(name=name, variant=variant, dispatches=KDISP, mean_ms=round(mean, 4),
+                median_ms=round(med, 4), min_ms=round(t[0], 4), max_ms=round(t[-1], 4),
+                achieved=round(alg_bytes / (mean * 1e-3) / 1e9, 1),
+                frac=round(alg_bytes / (mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                timing="per dispatch: one HIP event pair each on the kernel's stream, "
+                       "untimed pass after the steps")
 
 
 def verdict8_leg(name, ctx, pk, off, ln, n, ul, len_hint, out16, nflows, steps, warmup, dev,
@@ -366,7 +485,7 @@ def verdict8_leg(name, ctx, pk, off, ln, n, ul, len_hint, out16, nflows, steps, 
     return r
 
 
-def burst_digest(name, out, n, gidx, counts, total_steps, rank, world):
+def burst_digest(name, out, n, gidx, counts, total_steps, rank, world, shard_mode="direct"):
     """the whole burst against tests/golden/digests.json (the oracle's verdicts
     of every frame of the workload's burst, computed offline by
     tests/golden/make_digests.py): N = 1, the SHA-256 of all n x 16 verdict
@@ -380,9 +499,16 @@ def burst_digest(name, out, n, gidx, counts, total_steps, rank, world):
         gold = D.load_golden().get(name)
     except OSError:
         gold = None
-    r = dict(golden=gold is not None)
     dev = out.device
     v = out[:n * 16]
+    if world > 1 and shard_mode == "direct":
+        # each rank's frames are its own shard stream, not frames of the
+        # golden burst: the per-rank oracle sample and the count check
+        # (counts_match) are the parity evidence at N > 1
+        return dict(golden=False, digest_ok=None,
+                    scope="N > 1, shards generated per rank: no golden burst; see parity "
+                          "(oracle sample per rank) and counts_match")
+    r = dict(golden=gold is not None)
     if world == 1:
         idx = torch.arange(n, dtype=torch.int64, device=dev)
         r["frames"] = n
@@ -1028,6 +1154,14 @@ def main():
     ap.add_argument("--flow-load", type=int, default=0,
                     help="flow tables at load <= 2**-N (rxg_tune_flow_load; 0 = default)")
     ap.add_argument("--sweep-counts", action="store_true", help="sweep with per-flow counts on")
+    ap.add_argument("--shard-gen", default="direct", choices=["direct", "split"],
+                    help="N > 1: each rank generates its RSS shard directly (direct) or every "
+                         "rank generates the global burst, splits it and gathers its shard "
+                         "(split: the shards partition one burst; golden digest of its first n "
+                         "frames)")
+    ap.add_argument("--deadline", type=float, default=0.0,
+                    help="N > 1 without a launcher: wall-clock limit of the whole run in seconds "
+                         "(0 = 120 + 120 per workload); past it every rank is stopped")
     ap.add_argument("--sweep", default="", help="time every kernel variant on these workloads "
                     "(tuning; prints to stderr, no JSON line)")
     a = ap.parse_args()
@@ -1044,11 +1178,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     log(f"bench: rank {rank} of {world} (local {local}, pid {os.getpid()}, {ndev} GPU(s) visible)")
+    hang = os.environ.get("BENCH_TEST_HANG_RANK")  # test hook: this rank blocks forever
+    if hang is not None and int(hang) == rank:
+        stage(rank, "rendezvous (BENCH_TEST_HANG_RANK: blocked on purpose)")
+        while True:
+            time.sleep(60)
     if ndev == 0:
         # no GPU: the rank set and the rendezvous are still checked (gloo),
         # then every rank fails loudly; nothing is measured without the device
         if world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            stage(rank, "rendezvous")
             torch.distributed.init_process_group("gloo")
             t = torch.ones(1)
             torch.distributed.all_reduce(t)
@@ -1063,11 +1203,13 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
+        stage(rank, "rendezvous")
         torch.distributed.init_process_group(a.backend)
         if a.collective == "rxg" and ndev >= world:
             try:  # rank 0 makes the RCCL id, gloo hands it to every rank
                 obj = [R.group_id() if rank == 0 else None]
                 torch.distributed.broadcast_object_list(obj, src=0)
+                stage(rank, "rxg_group_open (RCCL communicator)")
                 group = R.Group(local, world, rank, obj[0])
                 collective = "rccl (rxg_group_open / rxg_counts_allreduce, C ABI)"
             except Exception as e:  # reported in the line, never silent
@@ -1099,12 +1241,13 @@ def main():
     names = [s.strip() for s in a.workload.split(",") if s.strip()]
     results = {}
     for nm in names:
+        stage(rank, f"{nm}: setup")
         coll = None
         if world > 1:
             u, t = R.gen_flows(rxdist.gen_cfg(nm))
             coll = collective_fn(group, nccl_group, len(u) + len(t))
         results[nm] = run_workload(nm, ctx, rank, world, a.steps, a.warmup, dev, coll,
-                                   a.parity_sample, oracle_threads)
+                                   a.parity_sample, oracle_threads, a.shard_gen)
         log(nm, json.dumps({k: v for k, v in results[nm].items() if k != "desc"}))
     head = results[names[0]]
 
@@ -1138,6 +1281,7 @@ def main():
             results[nm]["e2e_pcie"] = r
 
     parity_bad = sum(r["parity"]["mismatches"] for r in results.values()) + \
+        sum(r["counts_match"] is False for r in results.values()) + \
         (cfg1["parity"]["mismatches"] if cfg1 else 0) + \
         sum(r["digest"]["digest_ok"] is False for r in results.values()) + \
         sum(("verdict8" in r and (not r["verdict8"]["equals_projection"]
@@ -1169,6 +1313,7 @@ def main():
             "digest": head["digest"],
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
+            "counts_match": head["counts_match"],
             "hbm_copy_peak_gbs": copy_peak,
             "librxgpu_sha256": lib_sha256()[:16],
         }

@@ -16,8 +16,8 @@
 #include "rx_flows.h"
 
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
-void rx_set_bpc_cap(uint32_t cap);
 bool rx_variant_exists(uint32_t g, uint32_t pipe);
+const char *rx_variant_kernel(uint32_t g, uint32_t pipe);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
                               uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
@@ -29,7 +29,6 @@ hipError_t rx_classify_launch8(const uint8_t *pkts, const uint32_t *off, const u
                                uint32_t pipe, const rx_ft_dev &ft, uint4 *out,
                                unsigned long long *counts, hipStream_t s, uint32_t *ws,
                                uint32_t phase, uint32_t buf, uint32_t nbuf);
-void rx_set_bpc_cap8(uint32_t cap);
 size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_dev &ft,
                             bool counts, uint32_t nbuf);
 bool rx_count_uses_slabs(const rx_ft_dev &ft, bool counts);
@@ -102,16 +101,22 @@ hipError_t rx_occupancy(const void *fn, uint32_t threads, size_t lds, int *cu, i
 
 // one incremental table write (rxg_flows_commit): rx_delta_kernel stores v
 // at element idx of table `which`
-enum { RX_D_UDP = 0, RX_D_TCP = 1, RX_D_LISTEN = 2, RX_D_PORT = 3, RX_D_UDPC = 4, RX_D_UDPW = 5 };
+// (RX_D_CZERO: count index idx of a removed block, zeroed in both of the
+// context's count vectors before its id can name a new block)
+enum { RX_D_UDP = 0, RX_D_TCP = 1, RX_D_LISTEN = 2, RX_D_PORT = 3, RX_D_UDPC = 4, RX_D_UDPW = 5,
+       RX_D_CZERO = 6 };
 struct rx_delta {
     uint32_t which, idx, _r0, _r1;
     uint4 v;
 };
 #define RX_DELTA_CAP 65536u // records per commit; more: whole arrays are uploaded
+#define RX_DELTA_ROOM (RX_DELTA_CAP + 2048u) // staging records (the small tables ride on top)
 
 __global__ __launch_bounds__(256) void rx_delta_kernel(const rx_delta *__restrict__ d, uint32_t n,
                                                        uint4 *udp, uint4 *tcp, uint32_t *listen,
-                                                       uint32_t *port, uint4 *udpc, uint4 *udpw) {
+                                                       uint32_t *port, uint4 *udpc, uint4 *udpw,
+                                                       unsigned long long *cnt,
+                                                       unsigned long long *cnt_base) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const rx_delta r = d[i];
@@ -121,6 +126,7 @@ __global__ __launch_bounds__(256) void rx_delta_kernel(const rx_delta *__restric
     case RX_D_LISTEN: listen[r.idx] = r.v.x; break;
     case RX_D_PORT: port[r.idx] = r.v.x; break;
     case RX_D_UDPC: udpc[r.idx] = r.v; break;
+    case RX_D_CZERO: cnt[r.idx] = 0ull, cnt_base[r.idx] = 0ull; break;
     default: udpw[r.idx] = r.v; break;
     }
 }
@@ -203,6 +209,9 @@ struct rxg_ctx {
     // rxg_ctx_counts_allreduce, d_counts_base the all-reduced total before it
     unsigned long long *d_counts = nullptr, *d_counts_base = nullptr;
     uint32_t counts_cap = 0;
+    // ids removed since the last commit: their counts are zeroed by that
+    // commit (RX_D_CZERO), so a reused id starts from 0
+    std::vector<uint32_t> czero_udp, czero_tcp;
     // host-buffer path: a ring of RXG_PIPE_DEPTH staging slots; burst t uses
     // slot t % depth.  Copies in run on s_h2d, kernels on `stream`, verdict
     // copies out on s_d2h, chained by events, so burst t+1's frames cross PCIe
@@ -233,16 +242,6 @@ struct rxg_ctx {
     void *d_cp_ws = nullptr;
     size_t d_cp_ws_cap = 0;
 };
-
-static int ensure_dev(void **p, size_t *cap, size_t bytes) {
-    if (*cap >= bytes && *p) return RXG_OK;
-    if (*p) HIPCHK(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    HIPCHK(hipMalloc(p, bytes));
-    *cap = bytes;
-    return RXG_OK;
-}
 
 // a flow-table array of at least `bytes`, stream-ordered on s (hipMallocAsync /
 // hipFreeAsync: neither synchronises the device, unlike hipFree)
@@ -500,13 +499,36 @@ static int commit_on(rxg_ctx *c, hipStream_t s) {
     fs.tcp.tab.dirty.clear();
     fs.listen_dirty.clear();
     fs.port_dirty.clear();
-    if (n) {
+    // the staged records to the device and the scatter kernel; a full staging
+    // buffer (more removed ids than it holds) is flushed and refilled after
+    // its copy has left
+    auto flush = [&]() -> int {
+        if (!n) return RXG_OK;
         HIPCHK(hipMemcpyAsync(c->d_delta, c->h_delta, n * sizeof(rx_delta), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(rx_delta_kernel, dim3((n + 255) / 256), dim3(256), 0, s, c->d_delta, n,
                            c->d_udp, c->d_tcp, c->d_listen, c->d_udp_port,
-                           reinterpret_cast<uint4 *>(c->d_udpc), reinterpret_cast<uint4 *>(c->d_udpw));
+                           reinterpret_cast<uint4 *>(c->d_udpc), reinterpret_cast<uint4 *>(c->d_udpw),
+                           c->d_counts, c->d_counts_base);
         HIPCHK(hipGetLastError());
-    }
+        n = 0;
+        return RXG_OK;
+    };
+    // counts of removed ids (in the layout counts_layout just made: TCP at nu + id)
+    const uint32_t nf = c->ft.nu + c->ft.nt;
+    for (int k = 0; k < 2; ++k)
+        for (uint32_t id : k ? c->czero_tcp : c->czero_udp) {
+            const uint32_t idx = k ? c->ft.nu + id : id;
+            if (idx >= nf || (!k && id >= c->ft.nu)) continue;
+            if (n == RX_DELTA_ROOM) {
+                if ((rc = flush())) return rc;
+                HIPCHK(hipEventRecord(c->ev_commit, s));
+                HIPCHK(hipEventSynchronize(c->ev_commit)); // (the staging copy has left)
+            }
+            put(RX_D_CZERO, idx, make_uint4(0, 0, 0, 0));
+        }
+    c->czero_udp.clear();
+    c->czero_tcp.clear();
+    if ((rc = flush())) return rc;
     HIPCHK(hipEventRecord(c->ev_commit, s));
     ++c->commit_gen;
     for (rx_track &x : c->trk)
@@ -577,7 +599,7 @@ int rxg_open(rxg_ctx **out, int device, uint32_t max_pkts, uint64_t max_bytes) {
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_udp_port, 65536 * sizeof(uint32_t))))) break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_udpc, 2 * RX_UDPC_MAX_FLOWS * sizeof(uint2))))) break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_udpw, RX_UDPW_MAX_PORTS * sizeof(uint16_t))))) break;
-        const size_t dbytes = (RX_DELTA_CAP + 2048) * sizeof(rx_delta);
+        const size_t dbytes = RX_DELTA_ROOM * sizeof(rx_delta);
         if ((rc = rx_set_hip_error(hipHostMalloc((void **)&c->h_delta, dbytes, 0)))) break;
         if ((rc = rx_set_hip_error(hipMalloc(&c->d_delta, dbytes)))) break;
         if ((rc = rx_set_hip_error(hipEventCreateWithFlags(&c->ev_commit, hipEventDisableTiming))))
@@ -631,7 +653,19 @@ void rxg_close(rxg_ctx *c) {
         return;
     }
     dev_guard dg(c->device);
-    (void)bursts_drain(c);
+    // waits for what the context can name without touching the caller's
+    // streams: their recorded events and the context's own streams.  The
+    // stream of the latest burst (c->cur, its event not recorded) may already
+    // be destroyed (the usual teardown order: synchronise, destroy the stream,
+    // close), so nothing is recorded on it; hipFree below synchronises the
+    // device before it releases memory a kernel could still read.
+    for (rx_track &x : c->trk)
+        if (x.used && &x != c->cur) (void)hipEventSynchronize(x.ev);
+    for (rxg_ctx::ws_use &u : c->wu)
+        if (u.used) (void)hipEventSynchronize(u.ev);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->s_h2d) (void)hipStreamSynchronize(c->s_h2d);
+    if (c->s_d2h) (void)hipStreamSynchronize(c->s_d2h);
     (void)hipFree(c->d_udp);
     (void)hipFree(c->d_tcp);
     (void)hipFree(c->d_listen);
@@ -722,6 +756,8 @@ int rxg_flows_sync(rxg_ctx *c, const rxg_udp_sock *u, uint32_t nu, const rxg_tcb
     if (!c || (nu && !u) || (nt && !t)) return RXG_EINVAL;
     rx_flowset &fs = c->fs;
     fs.clear();
+    c->czero_udp.clear(); // (the counts are zeroed whole below)
+    c->czero_tcp.clear();
     fs.port_table = !(c->tune_tables & RXG_TT_NO_UDP_PORT);
     fs.udp.blk.resize(nu);
     for (uint32_t i = 0; i < nu; ++i) {
@@ -844,6 +880,7 @@ int rxg_flows_remove(rxg_ctx *c, const uint32_t *udp_ids, uint32_t nu, const uin
         fs.udp.blk[id].live = false;
         --fs.udp.live;
         fs.udp.free_ids.push_back(id);
+        if (c->device != RXG_HOST_ONLY) c->czero_udp.push_back(id);
     }
     for (uint32_t k = 0; k < nt; ++k) {
         const uint32_t id = tcp_ids[k];
@@ -854,6 +891,7 @@ int rxg_flows_remove(rxg_ctx *c, const uint32_t *udp_ids, uint32_t nu, const uin
         x.live = false;
         --fs.tcp.live;
         fs.tcp.free_ids.push_back(id);
+        if (c->device != RXG_HOST_ONLY) c->czero_tcp.push_back(id);
     }
     if (nu) fs.small_rebuild();
     after_change(c, true);
@@ -934,6 +972,19 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
     c->tune_p = lanes_per_frame ? passes : 0;
     c->tune_fpg = lanes_per_frame ? frames_per_group : 0;
     c->tune_pipe = lanes_per_frame ? pipeline : ~0u;
+    return RXG_OK;
+}
+
+int rxg_kernel_variant(const rxg_ctx *c, uint32_t len_hint, uint32_t variant[4], char *name,
+                       uint32_t name_cap) {
+    if (!c) return RXG_EINVAL;
+    uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
+    if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe); // as classify_dev_impl
+    if (variant) variant[0] = g, variant[1] = p, variant[2] = fpg, variant[3] = pipe;
+    if (name && name_cap) {
+        strncpy(name, rx_variant_kernel(g, pipe), name_cap - 1);
+        name[name_cap - 1] = '\0';
+    }
     return RXG_OK;
 }
 
@@ -1040,9 +1091,12 @@ static hipError_t ws_mark(rxg_ctx *c, int r, hipStream_t s) {
 // after every earlier use
 static int ws_prepare(rxg_ctx *c, size_t ws, const rxg_ctx::ws_shape &layout, hipStream_t s) {
     if (ws > c->d_ws_cap) {
+        // every use of the old workspace has finished (its events): it is freed
+        // and the grown one allocated in stream order on s, without the
+        // device-wide synchronisation of hipFree
         for (rxg_ctx::ws_use &u : c->wu)
             if (u.used) HIPCHK(hipEventSynchronize(u.ev));
-        int rc = ensure_dev((void **)&c->d_ws, &c->d_ws_cap, ws);
+        int rc = ensure_dev_async((void **)&c->d_ws, &c->d_ws_cap, ws, s);
         if (rc) return rc;
     } else if (layout != c->ws_layout) {
         for (int r = 0; r < 3; ++r) HIPCHK(ws_wait(c, r, s));
@@ -1068,8 +1122,7 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
         }
         return RXG_OK;
     };
-    rx_set_bpc_cap(c->tune_bpc);
-    rx_set_bpc_cap8(c->tune_bpc);
+    c->ft.bpc_cap = c->tune_bpc; // (read by this burst's launches only: they copy c->ft)
     // the verdict format of this burst (rxg_classify_dev8: c->ft.v8)
     const auto k1 = c->ft.v8 ? rx_classify_launch8 : rx_classify_launch;
     if (!ws) {
@@ -1313,9 +1366,8 @@ static int compact_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off
     const uint32_t nf = c->fs.udp.id_space();
     if (nf == 0 || nf > RXG_COMPACT_MAX_FLOWS) return nf ? RXG_ERANGE : RXG_OK;
     const size_t ws = rx_compact_ws_bytes(n, nf);
-    if (ws > c->d_cp_ws_cap) {
-        HIPCHK(hipStreamSynchronize(s)); // (a grown workspace: the last use is on s)
-        int rc = ensure_dev(&c->d_cp_ws, &c->d_cp_ws_cap, ws);
+    if (ws > c->d_cp_ws_cap) { // (its uses are all on s: freed and grown in stream order)
+        int rc = ensure_dev_async(&c->d_cp_ws, &c->d_cp_ws_cap, ws, s);
         if (rc) return rc;
     }
     HIPCHK(rx_compact_launch(d_pkts, d_off, d_len, n, off_unit_log2, d_v, nf, d_dg, d_first,

@@ -61,7 +61,7 @@
 
 // This file is compiled twice (Makefile): RX_V8 = 0 writes the 16-B
 // rxg_verdict, RX_V8 = 1 the 8-B rxg_verdict8 (rxg_classify_dev8).  The
-// second build exports only rx_classify_launch8 and rx_set_bpc_cap8, so the
+// second build exports only rx_classify_launch8, so the
 // format is a compile-time choice in every kernel: no branch on either path
 // (a run-time switch measured 0.2-0.6% slower on the 16-B path, r03e).
 #ifndef RX_V8
@@ -75,8 +75,6 @@
 
 namespace {
 
-// resident blocks per CU the launchers use: min(occupancy, cap); 0 = no cap
-static thread_local uint32_t g_bpc_cap = 0;
 
 // Frames of one lane group for one trip: descriptors and the first P passes.
 // flow 65535 at exactly 65536 flows with 2-B count indices (rx_ft_dev::
@@ -504,7 +502,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
     uint64_t occ = (uint64_t)bpc;
-    if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
+    if (ft.bpc_cap && occ > ft.bpc_cap) occ = ft.bpc_cap;
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
@@ -1105,7 +1103,7 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
     if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + 255) / 256;
     uint64_t occ = (uint64_t)bpc;
-    if (g_bpc_cap && occ > g_bpc_cap) occ = g_bpc_cap;
+    if (ft.bpc_cap && occ > ft.bpc_cap) occ = ft.bpc_cap;
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
@@ -1211,11 +1209,10 @@ static hipError_t launch_binned(const uint8_t *pkts, const uint32_t *off, const 
     hipLaunchKernelGGL(rx_bin_kernel, dim3(blocks), dim3(256), 0, s, len, n, chunk, 64u, lists,
                        lens);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t user_cap = g_bpc_cap;
-    if (!user_cap) g_bpc_cap = 6;
-    e = launch_lane_udpc<0, 0, true, false>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
+    rx_ft_dev fl = ft;
+    if (!fl.bpc_cap) fl.bpc_cap = 6;
+    e = launch_lane_udpc<0, 0, true, false>(pkts, off, len, n, unit_log2, fl, out, counts, lds_bins, s,
                                         lists, lens);
-    g_bpc_cap = user_cap;
     if (e != hipSuccess) return e;
     return launch_v<8, 2, 1, 1>(pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s,
                                 lists + n, lens + 1);
@@ -2519,9 +2516,23 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
     }
 }
 
+// the kernel a variant launches, as rocprofv3 names it (without the template
+// arguments): rxg_kernel_variant, so a bench line names the dispatch that a
+// kernel trace of the same run shows
+const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
+    if (g == 1) return "rx_classify_lane_kernel";
+    if (g >= 4) return "rx_classify_kernel";
+    if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
+    switch (pipe % 1000u % 100u) {
+    case 60: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
+        return "rx_classify_sh_kernel";
+    default:
+        return "rx_classify_stream_kernel";
+    }
+}
+
 #endif
 
-void RX_K1_NAME(rx_set_bpc_cap)(uint32_t cap) { g_bpc_cap = cap; }
 
 #if !RX_V8
 
@@ -2593,11 +2604,10 @@ hipError_t RX_K1_NAME(rx_classify_launch)(const uint8_t *pkts, const uint32_t *o
             for (const variant_entry &v : k_variants)
                 if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
                     (pipe == 0xFFFFFFFFu || v.pipe == pipe)) {
-                    const uint32_t user_cap = g_bpc_cap;
-                    if (!user_cap) g_bpc_cap = v.bpc;
-                    e = v.fn(pkts, off, len, n, unit_log2, ft, out, kcounts, lds_bins, s, nullptr,
+                    rx_ft_dev fv = ft;
+                    if (!fv.bpc_cap) fv.bpc_cap = v.bpc; // (rxg_tune_grid's cap, else the variant's)
+                    e = v.fn(pkts, off, len, n, unit_log2, fv, out, kcounts, lds_bins, s, nullptr,
                              nullptr);
-                    g_bpc_cap = user_cap;
                     break;
                 }
         }

@@ -69,6 +69,10 @@ struct rx_ft_dev {
     // 8-B rxg_verdict8, rxg_classify_dev8), which picks the launcher of the
     // RX_V8 build of rx_classify.hip; the kernels never read it
     uint32_t v8;
+    // host side only: resident blocks per CU the launch may use (0 = as many
+    // as the occupancy allows): rxg_tune_grid's cap, else the variant's
+    // measured default (k_variants), set on rx_classify_launch's copy
+    uint32_t bpc_cap;
 };
 
 // rx_classify_launch phases (host side)

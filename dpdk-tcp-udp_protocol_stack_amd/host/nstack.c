@@ -673,6 +673,9 @@ static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags)
     return length;
 }
 
+static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
+                        struct sockaddr *src_addr);
+
 ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr *src_addr,
                   socklen_t *addrlen) { /* :517-565 */
     (void)addrlen;
@@ -680,6 +683,12 @@ ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr 
     struct localhost *h = get_hostinfo_fromfd(sockfd);
     pthread_mutex_unlock(&g_lock);
     if (!h) return -1;
+    return udp_recv(h, buf, len, flags, src_addr);
+}
+
+/* nrecvfrom after the descriptor lookup (common.c:526-565) */
+static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
+                        struct sockaddr *src_addr) {
     struct offload *o = NULL;
     pthread_mutex_lock(&h->mutex);
     while (ring_peek(h->rcvbuf, (void **)&o) < 0) {
@@ -1351,37 +1360,23 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
 }
 
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
+    /* The whole walk holds g_lock: a concurrent nstack_rx_burst (LAST_ACK) or
+     * nclose could otherwise free a block this loop still reads.
+     * Every receive ring is read to its end, EOF fragments included (they
+     * count as nothing), like oracle_drain_all. */
     uint64_t got = 0, nb = 0;
     pthread_mutex_lock(&g_lock);
-    int nfd = 0;
-    int *fds = NULL;
-    struct tcp_stream **tcbs = NULL;
-    uint32_t nt = 0;
-    for (struct localhost *h = g_pstHost; h; h = h->next) nfd++;
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) nt++;
-    fds = malloc((size_t)(nfd ? nfd : 1) * sizeof(int));
-    tcbs = malloc((size_t)(nt ? nt : 1) * sizeof(*tcbs));
-    if (!fds || !tcbs) {
-        pthread_mutex_unlock(&g_lock);
-        free(fds), free(tcbs);
-        return RXG_ENOMEM;
-    }
-    nfd = 0, nt = 0;
-    for (struct localhost *h = g_pstHost; h; h = h->next) fds[nfd++] = h->fd;
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) tcbs[nt++] = s;
-    pthread_mutex_unlock(&g_lock);
-    for (int k = 0; k < nfd; k++) { /* the application's nrecvfrom loop */
+    for (struct localhost *h = g_pstHost; h; h = h->next) { /* the application's nrecvfrom loop */
         ssize_t r;
         struct sockaddr_in a;
-        socklen_t al = sizeof(a);
-        while ((r = nrecvfrom(fds[k], buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a, &al)) >= 0)
+        while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0)
             got++, nb += (uint64_t)r;
     }
-    for (uint32_t k = 0; k < nt; k++) { /* nrecv on every tcb, its queued ACKs sent */
-        struct tcp_stream *s = tcbs[k];
+    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) { /* nrecv on every tcb */
         ssize_t r;
-        while ((r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT)) > 0) got++, nb += (uint64_t)r;
-        void *p;
+        while ((r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT)) >= 0)
+            if (r > 0) got++, nb += (uint64_t)r;
+        void *p; /* its queued control fragments (ACKs) sent */
         pthread_mutex_lock(&s->mutex);
         while (ring_dequeue(s->sndbuf, &p) == 0) {
             free(((struct tcp_fragment *)p)->data);
@@ -1389,7 +1384,7 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
         }
         pthread_mutex_unlock(&s->mutex);
     }
-    free(fds), free(tcbs);
+    pthread_mutex_unlock(&g_lock);
     if (bytes) *bytes = nb;
     return (int64_t)got;
 }

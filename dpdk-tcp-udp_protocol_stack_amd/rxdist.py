@@ -45,8 +45,8 @@ WORKLOADS = {
 
 def gen_cfg(name: str, rank: int = 0, world: int = 1, **over) -> R.GenCfg:
     """generator config of a workload; rank/world > 1 = the generator's own
-    rejection-sampled RSS shard (frames of the shard only).  The multi-GPU
-    bench instead generates the whole burst and splits it (build_shard)."""
+    rejection-sampled RSS shard (frames of the shard only: the multi-GPU
+    bench's default, build_shard mode "direct")."""
     w = WORKLOADS[name]
     kw = dict(w["gen"])
     kw.update(seed=0x5EED0001 + int(name[3:]), shard=rank, n_shards=world)
@@ -64,29 +64,39 @@ def allreduce_counts(counts, world: int, async_op: bool = False):
     return None
 
 
-def build_shard(ctx, name: str, rank: int, world: int, dev, stream):
+def build_shard(ctx, name: str, rank: int, world: int, dev, stream, mode: str = "direct"):
     """This rank's share of a workload's burst, resident in HBM.
 
-    world == 1: the burst itself (n frames).  world > 1: the GLOBAL burst of
-    world * n frames is generated chunk by chunk (n frames per chunk, frame i
-    the same pure function of (cfg, i) on every rank), RSS-split on the device
-    (rxg_rss_split_dev) and this rank's frames gathered into one packed burst
-    (rxg_gather_dev) — the frames a multi-queue NIC would DMA into this GPU's
-    queue.  Returns (pk, off, ln, n_local, gidx) with gidx = the global frame
-    index of every local frame (int64, host; None for world == 1)."""
+    world == 1: the burst itself (n frames).  world > 1:
+      mode "direct" (the default): this rank's n frames generated straight
+        into HBM by the generator's own RSS sharding (rxg_gen_cfg.shard /
+        n_shards: only tuples whose rxg_rss_hash % world == rank) — the frames
+        a multi-queue NIC would DMA into this GPU's queue, at one generation
+        pass per rank;
+      mode "split": the GLOBAL burst of world * n frames is generated chunk by
+        chunk (n frames per chunk, frame i the same pure function of (cfg, i)
+        on every rank), RSS-split on the device (rxg_rss_split_dev) and this
+        rank's frames gathered into one packed burst (rxg_gather_dev), so the
+        ranks' shards partition one burst whose first n frames carry golden
+        digests (2 * world generation passes per rank).
+    Returns (pk, off, ln, n_local, gidx, cfg): gidx = the global frame index
+    of every local frame (int64, host; None when the frames are local indices
+    of `cfg`'s stream), cfg = the generator config that regenerates them."""
     import numpy as np
     import torch
     w = WORKLOADS[name]
     cfg = gen_cfg(name)
     n, ul = w["n"], w["unit_log2"]
     sh = stream.cuda_stream
-    if world == 1:
+    if world == 1 or mode == "direct":
+        if world > 1:
+            cfg = gen_cfg(name, rank, world)
         pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
         off = torch.empty(n, dtype=torch.int32, device=dev)
         ln = torch.empty(n, dtype=torch.int16, device=dev)
         R.gen_dev(cfg, 0, n, pk, off, ln, ul, stream=sh)
         torch.cuda.synchronize(dev)
-        return pk, off, ln, n, None
+        return pk, off, ln, n, None, cfg
     c_pk = torch.empty(n * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
     c_off = torch.empty(n, dtype=torch.int32, device=dev)
     c_ln = torch.empty(n, dtype=torch.int16, device=dev)
@@ -128,4 +138,4 @@ def build_shard(ctx, name: str, rank: int, world: int, dev, stream):
     torch.cuda.synchronize(dev)
     del c_pk, c_off, c_ln, d_perm
     torch.cuda.empty_cache()
-    return pk, off, ln, frames, gidx
+    return pk, off, ln, frames, gidx, cfg

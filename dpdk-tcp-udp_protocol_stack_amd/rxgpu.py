@@ -164,6 +164,8 @@ _counts_reset = _sig("rxg_counts_reset", _i32, _vp)
 _num_flows = _sig("rxg_num_flows", _u32, _vp)
 _tune = _sig("rxg_tune", _i32, _vp, _u32, _u32, _u32, _u32)
 _tune_grid = _sig("rxg_tune_grid", _i32, _vp, _u32)
+_kernel_variant = (_sig("rxg_kernel_variant", _i32, _vp, _u32, _vp, C.c_char_p, _u32)
+                   if hasattr(_lib, "rxg_kernel_variant") else None)
 _tune_tx = _sig("rxg_tune_tx", _i32, _vp, _u32, _u32)
 _tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
 _tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
@@ -207,7 +209,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
-            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
+            "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum", "rxg_rss_split",
@@ -328,6 +330,16 @@ class Context:
              pipeline: int = 0xFFFFFFFF):
         """force a kernel variant (lanes_per_frame 0 = automatic); see KERNEL_VARIANTS"""
         _check(_tune(self._h, lanes_per_frame, passes, frames_per_group, pipeline), "rxg_tune")
+
+    def kernel_variant(self, len_hint: int):
+        """(kernel name as a trace shows it, [g, p, fpg, pipe]) of the classify
+        dispatch a burst with this len_hint runs (rxg_kernel_variant)"""
+        if _kernel_variant is None:
+            return None, None
+        v = np.zeros(4, np.uint32)
+        buf = C.create_string_buffer(128)
+        _check(_kernel_variant(self._h, len_hint, _ptr(v), buf, 128), "rxg_kernel_variant")
+        return buf.value.decode(), [int(x) for x in v]
 
     def tune_grid(self, blocks_per_cu: int = 0):
         """cap resident blocks per CU (0 = occupancy)"""

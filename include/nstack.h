@@ -141,8 +141,10 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * with nrecvfrom until empty, every tcb's receive queue read (nrecv) and its
  * queued ACKs taken off its send ring (as one tcp_out pass would).  buf/cap =
  * the receive buffer each call uses.  Returns the datagrams + fragments
- * received (a negative RXG_E* code on error); *bytes = the bytes the calls
- * returned. */
+ * received (EOF fragments are read and not counted, as oracle_drain_all does;
+ * a negative RXG_E* code on error); *bytes = the bytes the calls returned.
+ * Holds the stack's lock for the whole walk (a concurrent nstack_rx_burst
+ * waits for it), so no block it reads can be freed under it. */
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
 
 /* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),

@@ -69,9 +69,12 @@ enum {
 #define RXG_F_UDP_SHORT 0x04  /* UDP dgram_len <= 8 (rc -2, see RXG_RC_UDP_NOMEM) */
 
 typedef struct rxg_verdict {
-    uint32_t flow_id;      /* index of the matched control block in the arrays
-                              last given to rxg_flows_sync (UDP: into u[], TCP:
-                              into t[]); RXG_FLOW_NONE if no match / not looked up */
+    uint32_t flow_id;      /* stable id of the matched control block (UDP and TCP
+                              ids are separate spaces): id i for block i of the
+                              arrays given to rxg_flows_sync, or the id
+                              rxg_flows_add assigned.  A removed block's id may be
+                              reused by a later add.  RXG_FLOW_NONE if no match /
+                              not looked up */
     uint16_t payload_off;  /* UDP: 42 (udp.c:46 copies from udp+1); TCP: 34+hl */
     uint16_t payload_len;  /* UDP: dgram_len-8 (udp.c:38); TCP: tl-20-hl (tcp.c:145-159);
                               clamped at 0 (see flags) */
@@ -355,6 +358,15 @@ int rxg_tx_cksum(rxg_ctx *ctx, uint8_t *pkts, uint64_t span_bytes, const uint32_
  * lanes_per_frame > 0 combinations make the next burst fail with RXG_EHIP. */
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline);
+
+/* The classify variant a burst with this len_hint runs on this context (the
+ * rxg_tune override, else the default for len_hint): variant = {lanes per
+ * frame, passes, frames per group, pipeline}; name (nullable, name_cap bytes
+ * with the NUL) = the kernel it dispatches as a kernel trace names it
+ * (rocprofv3), without template arguments.  Diagnostics: it lets a benchmark
+ * line name the dispatch a profiler shows. */
+int rxg_kernel_variant(const rxg_ctx *ctx, uint32_t len_hint, uint32_t variant[4], char *name,
+                       uint32_t name_cap);
 
 /* Tuning hook: cap the resident 256-thread blocks per CU the launch uses
  * (0 = as many as the occupancy allows). */

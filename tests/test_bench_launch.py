@@ -59,3 +59,21 @@ def test_gpus_1_is_one_process():
     assert "launched" not in r.stderr
     assert "bench: rank 0 of 1" in r.stderr
     assert r.returncode == 4, r.stderr
+
+
+def test_hung_rank_ends_the_run_at_the_deadline_naming_its_stage():
+    """a rank that never reaches the rendezvous (here rank 1,
+    blocked on purpose by the BENCH_TEST_HANG_RANK hook) leaves rank 0 waiting
+    in it; past --deadline the launcher prints each rank's last stage,
+    stops both and exits 124 instead of hanging the driver's run"""
+    if not _no_gpu():
+        import pytest
+        pytest.skip("GPU present")
+    r = _run(["--gpus", "2", "--backend", "gloo", "--steps", "1", "--deadline", "15"],
+             env_extra=dict(BENCH_TEST_HANG_RANK="1"), timeout=120)
+    err = r.stderr
+    assert r.returncode == 124, (r.returncode, err)
+    assert "deadline 15 s passed; rank 1" in err, err
+    assert "last stage: rendezvous (BENCH_TEST_HANG_RANK: blocked on purpose)" in err, err
+    assert "deadline 15 s passed; rank 0" in err and "last stage: rendezvous" in err, err
+    assert r.stdout.strip() == ""

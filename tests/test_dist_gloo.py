@@ -9,9 +9,10 @@ the split's permutation, equal the verdicts of the unsharded burst; the
 all-reduced counts equal the unsharded histogram; every frame of a shard
 hashes to that shard by the oracle's independent Toeplitz restatement.
 
-No GPU here, so each shard is classified by the oracle (the checker) and the
-counts are reduced over gloo; the same split + classify + RCCL reduce runs on
-the GPU in tests/test_multigpu.py (one GPU, two contexts) and in bench.py
+On CPU each shard is classified by the oracle (the checker) and the counts
+are reduced over gloo; the -m gpu variant runs each rank's shard through its
+own librxgpu context (the HIP path).  The same split + classify + RCCL reduce
+runs in tests/test_multigpu.py (one GPU, two contexts) and in bench.py
 --gpus N (one rank per GPU)."""
 import os
 import socket
@@ -49,7 +50,7 @@ def _frame_shard(pk, o, l, world):
     return O.rss_hash(sip, dip, sp, dp) % world
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -57,7 +58,14 @@ def _worker(rank, world, port, name, q):
         first, perm = R.rss_split(pk, off, ln, 6, world)
         mine = perm[first[rank]:first[rank + 1]]
         bad = sum(_frame_shard(pk, off[i], ln[i], world) != rank for i in mine)
-        v, cnt = O.Tables(udp, tcb).classify(pk, off[mine], ln[mine], 6, counts=True)
+        if gpu:  # the HIP path: this rank's own context on the box's GPU
+            with R.Context(0, max_pkts=N_FRAMES, max_bytes=N_FRAMES * 1536) as ctx:
+                ctx.flows_sync(udp, tcb)
+                v = ctx.classify(pk, np.ascontiguousarray(off[mine]),
+                                 np.ascontiguousarray(ln[mine]), 6)
+                cnt = ctx.flow_counts()
+        else:
+            v, cnt = O.Tables(udp, tcb).classify(pk, off[mine], ln[mine], 6, counts=True)
         t = torch.from_numpy(cnt.astype(np.int64))
         work = rxdist.allreduce_counts(t, world, async_op=True)
         work.wait()
@@ -74,10 +82,26 @@ def _free_port():
 
 @pytest.mark.parametrize("name,world", [("cfg2", 2), ("cfg4", 2), ("cfg4", 4)])
 def test_rank_split_parity_and_count_reduce(name, world):
+    _split_run(name, world, gpu=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", [("cfg4", 2)])
+def test_rank_split_parity_and_count_reduce_hip(name, world):
+    """the same, each rank classifying its shard through its own librxgpu
+    context on the GPU (the ranks share the box's one GPU; gloo reduces)"""
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.fail("GPU tests need a GPU (no fallback path exists)")
+    _split_run(name, world, gpu=True)
+
+
+def _split_run(name, world, gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q, gpu))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]

@@ -365,3 +365,107 @@ def test_counts_move_with_the_id_space_tables_intact(torch_dev):
         nu = ctx.num_udp_ids
         assert all(int(c[nu + fid]) == n for fid, n in want_counts.items()), k
     ctx.close()
+
+
+def test_reused_id_counts_only_its_own_frames(torch_dev):
+    """ADVICE r3: a removed block's id is handed out again by the next add;
+    the new block's context count must hold only its own frames, not the
+    removed block's (the commit zeroes the counts of removed ids)"""
+    ctx = R.Context(0, max_pkts=4096, max_bytes=1 << 20)
+    lis = np.zeros(1, R.TCB_DTYPE)
+    lis[0] = (0, L, 0, P9999, R.TCP_STATUS_LISTEN)
+    t = np.zeros(2, R.TCB_DTYPE)
+    t[0] = (R.ip_raw("10.0.0.1"), L, R.port_raw(40001), P9999, 4)
+    t[1] = (R.ip_raw("10.0.0.2"), L, R.port_raw(40002), P9999, 4)
+    ctx.flows_sync(None, np.concatenate([lis, t]))
+    fr = [F.tcp_frame("10.0.0.1", 40001, "192.168.100.77", 9999, b"a" * 20)] * 7 + \
+         [F.tcp_frame("10.0.0.2", 40002, "192.168.100.77", 9999, b"b" * 20)] * 3
+    buf, off, lens = F.pack_frames(fr, 6)
+    ctx.classify(buf, off, lens, 6)
+    c = ctx.flow_counts()
+    nu = ctx.num_udp_ids
+    assert int(c[nu + 1]) == 7 and int(c[nu + 2]) == 3
+    ctx.flows_remove(None, [1])
+    nt = np.zeros(1, R.TCB_DTYPE)
+    nt[0] = (R.ip_raw("10.0.0.9"), L, R.port_raw(40009), P9999, 4)
+    _, tid, _ = ctx.flows_add(None, nt)
+    assert int(tid[0]) == 1  # the freed id, reused
+    fr2 = [F.tcp_frame("10.0.0.9", 40009, "192.168.100.77", 9999, b"c" * 20)] * 2
+    buf, off, lens = F.pack_frames(fr2, 6)
+    got = ctx.classify(buf, off, lens, 6)
+    assert list(got["flow_id"]) == [1, 1]
+    c = ctx.flow_counts()
+    nu = ctx.num_udp_ids
+    assert int(c[nu + 1]) == 2, c  # its own two frames only
+    assert int(c[nu + 2]) == 3
+    ctx.close()
+
+
+def test_close_after_the_burst_stream_is_destroyed(torch_dev):
+    """the usual teardown order — synchronise, destroy the stream
+    the last burst ran on, then close the context — must not touch the
+    destroyed stream (rxg_close records nothing on it)"""
+    import ctypes as C
+    torch, dev = torch_dev
+    hip = C.CDLL("libamdhip64.so")
+    st = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(st)) == 0
+    cfg = rxdist.gen_cfg("cfg2")
+    udp, tcb = R.gen_flows(cfg)
+    ctx = R.Context(0)
+    ctx.flows_sync(udp, tcb)
+    n = 4096
+    pk = torch.empty(n * 64 + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(n, dtype=torch.int32, device=dev)
+    ln = torch.empty(n, dtype=torch.int16, device=dev)
+    out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    R.gen_dev(cfg, 0, n, pk, off, ln, 6)
+    torch.cuda.synchronize(dev)
+    for _ in range(3):
+        ctx.classify_dev(pk, off, ln, n, 6, 64, out, None, stream=st.value)
+    assert hip.hipStreamSynchronize(st) == 0
+    assert hip.hipStreamDestroy(st) == 0
+    ctx.close()  # must neither crash nor fail
+    v = out.cpu().numpy().view(R.VERDICT_DTYPE)
+    assert np.all(v["rc"] <= 1)
+
+
+def test_workspace_growth_leaves_other_streams_running(torch_dev):
+    """a burst that grows the context's count workspace (slab path: > 8192
+    flows, a larger burst than any before) frees and reallocates it in stream
+    order: queued work on another stream is still running when the burst call
+    returns, and the burst's counts are exact"""
+    torch, dev = torch_dev
+    cfg = rxdist.gen_cfg("cfg4")
+    udp, tcb = R.gen_flows(cfg)
+    ctx = R.Context(0)
+    ctx.flows_sync(udp, tcb)
+    n0, n1 = 1 << 12, 1 << 16
+    pk = torch.empty(n1 * cfg.slot_bytes + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(n1, dtype=torch.int32, device=dev)
+    ln = torch.empty(n1, dtype=torch.int16, device=dev)
+    out = torch.empty(n1 * 16, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(ctx.num_flows, dtype=torch.int64, device=dev)
+    R.gen_dev(cfg, 0, n1, pk, off, ln, 6)
+    s = torch.cuda.current_stream(dev)
+    ctx.classify_dev(pk, off, ln, n0, 6, 0, out, cnt, stream=s.cuda_stream)  # small workspace
+    torch.cuda.synchronize(dev)
+    other = torch.cuda.Stream(dev)
+    a = torch.empty(1 << 28, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(other):
+        for _ in range(400):
+            b.copy_(a)
+    cnt.zero_()
+    ctx.classify_dev(pk, off, ln, n1, 6, 0, out, cnt, stream=s.cuda_stream)  # grows it
+    busy = not other.query()
+    torch.cuda.synchronize(dev)
+    assert busy, "the growing burst waited for another stream's work"
+    v = out[:n1 * 16].cpu().numpy().view(R.VERDICT_DTYPE)
+    ok = v["rc"] == 0
+    nu = len(udp)
+    idx = np.where(v["cls"][ok] == R.CLS_UDP, v["flow_id"][ok], nu + v["flow_id"][ok].astype(np.int64))
+    want = np.bincount(idx, minlength=ctx.num_flows).astype(np.uint64)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), want)
+    ctx.close()
