@@ -890,16 +890,23 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         ns.drain_all(rbuf)
         t_rx = t_dr = 0.0
         items = nbytes = delivered = 0
+        phases = []
         for _ in range(K):
             t0 = time.perf_counter()
             delivered += ns.rx_burst_mbufs(arr, B)
             t1 = time.perf_counter()
+            phases.append(ns.last_burst_phases())
             g, nb = ns.drain_all(rbuf)
             t2 = time.perf_counter()
             t_rx += t1 - t0
             t_dr += t2 - t1
             items += g
             nbytes += nb
+        # where rx_burst's time goes (nstack_last_burst_phases: host gather,
+        # then copy in / K1 / K3 + K4 / copy out from HIP events, then the host
+        # delivery steps), median over the bursts
+        res["rx_burst_phases_ms"] = {k: round(float(np.median([p[k] for p in phases])), 4)
+                                     for k in phases[0]}
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
                    rx_burst_ms=round(t_rx / K * 1e3, 3), app_recv_ms=round(t_dr / K * 1e3, 3),

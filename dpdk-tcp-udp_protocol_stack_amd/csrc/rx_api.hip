@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <new>
@@ -46,6 +47,11 @@ hipError_t rx_gather_launch(const uint8_t *pkts, const uint32_t *off, const uint
                             uint64_t cap, uint32_t *dst_off, uint16_t *dst_len, void *ws,
                             hipStream_t s);
 int rx_group_allreduce_u64(rxg_group *g, void *d, uint32_t n, hipStream_t s);
+size_t rx_segsort_ws_bytes(uint32_t n);
+hipError_t rx_segsort_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
+                             uint32_t n, uint32_t unit_log2, const uint4 *verd, uint32_t nt,
+                             rxg_segment *seg, uint8_t *payload, uint64_t cap, uint32_t *totals,
+                             void *ws, hipStream_t s);
 size_t rx_compact_ws_bytes(uint32_t n, uint32_t nflows);
 hipError_t rx_compact_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                              uint32_t n, uint32_t unit_log2, const uint4 *verd, uint32_t nflows,
@@ -241,6 +247,15 @@ struct rxg_ctx {
     uint32_t *d_cp_totals = nullptr, *h_cp_totals = nullptr;
     void *d_cp_ws = nullptr;
     size_t d_cp_ws_cap = 0;
+    // TCP segment sort + payload gather (K4, rxg_process_mbufs_deliver): device
+    // results and their pinned host copies, sized by max_pkts / max_bytes
+    rxg_segment *d_ss_seg = nullptr, *h_ss_seg = nullptr;
+    uint8_t *d_ss_payload = nullptr, *h_ss_payload = nullptr;
+    uint32_t *d_ss_totals = nullptr, *h_ss_totals = nullptr;
+    void *d_ss_ws = nullptr;
+    size_t d_ss_ws_cap = 0;
+    // phase timing of rxg_process_mbufs_deliver (timing-enabled events)
+    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 // a flow-table array of at least `bytes`, stream-ordered on s (hipMallocAsync /
@@ -683,6 +698,15 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_cp_payload);
     (void)hipFree(c->d_cp_totals);
     (void)hipFree(c->d_cp_ws);
+    (void)hipFree(c->d_ss_seg);
+    (void)hipFree(c->d_ss_payload);
+    (void)hipFree(c->d_ss_totals);
+    (void)hipFree(c->d_ss_ws);
+    if (c->h_ss_seg) (void)hipHostFree(c->h_ss_seg);
+    if (c->h_ss_payload) (void)hipHostFree(c->h_ss_payload);
+    if (c->h_ss_totals) (void)hipHostFree(c->h_ss_totals);
+    for (hipEvent_t e : c->tev)
+        if (e) (void)hipEventDestroy(e);
     if (c->h_cp_dg) (void)hipHostFree(c->h_cp_dg);
     if (c->h_cp_first) (void)hipHostFree(c->h_cp_first);
     if (c->h_cp_payload) (void)hipHostFree(c->h_cp_payload);
@@ -1455,6 +1479,151 @@ int rxg_process_mbufs_udp(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdic
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     return rxg_wait(c, t);
+}
+
+static int segsort_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, const uint4 *d_v,
+                        rxg_segment *d_seg, uint8_t *d_payload, uint64_t cap, uint32_t *d_totals,
+                        hipStream_t s) {
+    const size_t ws = rx_segsort_ws_bytes(n);
+    if (ws > c->d_ss_ws_cap) { // (its uses are all on s: freed and grown in stream order)
+        int rc = ensure_dev_async(&c->d_ss_ws, &c->d_ss_ws_cap, ws, s);
+        if (rc) return rc;
+    }
+    HIPCHK(rx_segsort_launch(d_pkts, d_off, d_len, n, off_unit_log2, d_v, c->fs.tcp.id_space(), d_seg,
+                             d_payload, cap, d_totals, c->d_ss_ws, s));
+    return RXG_OK;
+}
+
+int rxg_tcp_compact_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        const rxg_verdict *d_v, rxg_segment *d_seg, uint8_t *d_payload,
+                        uint64_t payload_cap, uint32_t *d_totals, void *stream) {
+    if (!c) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (!d_totals || (n && (!d_pkts || !d_off || !d_len || !d_v || !d_seg || !d_payload)))
+        return RXG_EINVAL;
+    if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
+    DEVGUARD(c);
+    return segsort_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, reinterpret_cast<const uint4 *>(d_v),
+                        d_seg, d_payload, payload_cap, d_totals, (hipStream_t)stream);
+}
+
+static double now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                              rxg_delivery *d, float ms[8]) {
+    if (!c || !d) return RXG_EINVAL;
+    memset(d, 0, sizeof(*d));
+    if (ms) memset(ms, 0, 8 * sizeof(float));
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (n && (!m || !out)) return RXG_EINVAL;
+    if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
+    const uint32_t nf = c->fs.udp.id_space();
+    const bool udp = nf > 0 && nf <= RXG_COMPACT_MAX_FLOWS;
+    DEVGUARD(c);
+    const double t0 = now_ms();
+    // results buffers, first use (each set last-allocated-first-checked: a
+    // failed allocation leaves the rest for the next call to retry)
+    if (udp && !c->h_cp_totals) {
+        if (!c->d_cp_dg) HIPCHK(hipMalloc(&c->d_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram)));
+        if (!c->d_cp_first)
+            HIPCHK(hipMalloc(&c->d_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t)));
+        if (!c->d_cp_payload) HIPCHK(hipMalloc(&c->d_cp_payload, c->max_bytes));
+        if (!c->d_cp_totals) HIPCHK(hipMalloc(&c->d_cp_totals, 4 * sizeof(uint32_t)));
+        if (!c->h_cp_dg)
+            HIPCHK(hipHostMalloc((void **)&c->h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
+        if (!c->h_cp_first)
+            HIPCHK(hipHostMalloc((void **)&c->h_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
+        if (!c->h_cp_payload) HIPCHK(hipHostMalloc((void **)&c->h_cp_payload, c->max_bytes, 0));
+        HIPCHK(hipHostMalloc((void **)&c->h_cp_totals, 4 * sizeof(uint32_t), 0));
+    }
+    if (!c->h_ss_totals) {
+        if (!c->d_ss_seg) HIPCHK(hipMalloc(&c->d_ss_seg, (size_t)c->max_pkts * sizeof(rxg_segment)));
+        if (!c->d_ss_payload) HIPCHK(hipMalloc(&c->d_ss_payload, c->max_bytes));
+        if (!c->d_ss_totals) HIPCHK(hipMalloc(&c->d_ss_totals, 4 * sizeof(uint32_t)));
+        if (!c->h_ss_seg)
+            HIPCHK(hipHostMalloc((void **)&c->h_ss_seg, (size_t)c->max_pkts * sizeof(rxg_segment), 0));
+        if (!c->h_ss_payload) HIPCHK(hipHostMalloc((void **)&c->h_ss_payload, c->max_bytes, 0));
+        HIPCHK(hipHostMalloc((void **)&c->h_ss_totals, 4 * sizeof(uint32_t), 0));
+    }
+    for (hipEvent_t &e : c->tev)
+        if (!e) HIPCHK(hipEventCreate(&e));
+    d->seg = c->h_ss_seg;
+    d->tcp_payload = c->h_ss_payload;
+    if (udp) {
+        d->dgram = c->h_cp_dg;
+        d->first = c->h_cp_first;
+        d->udp_payload = c->h_cp_payload;
+        memset(c->h_cp_first, 0, (nf + 1) * sizeof(uint32_t));
+    }
+    if (n == 0) return RXG_OK;
+    const uint64_t t = c->next_ticket++;
+    rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
+    uint64_t pos = 0;
+    int rc = gather_mbufs(c, sl, m, n, &pos);
+    if (rc) return rc;
+    const double t1 = now_ms();
+    HIPCHK(hipEventRecord(c->tev[0], c->s_h2d));
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->tev[1], c->s_h2d)); // after the copy in
+    HIPCHK(hipEventRecord(c->tev[2], c->stream)); // after K1
+    // the compactions follow the classify on the context's stream
+    if (udp)
+        if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_cp_dg,
+                               c->d_cp_first, c->d_cp_payload, c->max_bytes, c->d_cp_totals,
+                               c->stream)))
+            return rc;
+    const bool tcp = c->fs.tcp.id_space() > 0;
+    if (tcp)
+        if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_ss_seg,
+                               c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
+            return rc;
+    HIPCHK(hipEventRecord(c->tev[3], c->stream)); // after K3 / K4
+    if (udp) HIPCHK(hipMemcpyAsync(c->h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, c->stream));
+    if (tcp) HIPCHK(hipMemcpyAsync(c->h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if ((udp && c->h_cp_totals[2]) || (tcp && c->h_ss_totals[2]))
+        return RXG_ERANGE; // (not reached: staging bounds the payloads)
+    if (udp) {
+        d->ndgram = c->h_cp_totals[0];
+        d->udp_bytes = c->h_cp_totals[1];
+        HIPCHK(hipMemcpyAsync(c->h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        if (d->ndgram)
+            HIPCHK(hipMemcpyAsync(c->h_cp_dg, c->d_cp_dg, (size_t)d->ndgram * sizeof(rxg_dgram),
+                                  hipMemcpyDeviceToHost, c->stream));
+        if (d->udp_bytes)
+            HIPCHK(hipMemcpyAsync(c->h_cp_payload, c->d_cp_payload, d->udp_bytes,
+                                  hipMemcpyDeviceToHost, c->stream));
+    }
+    if (tcp) {
+        d->nseg = c->h_ss_totals[0];
+        d->tcp_bytes = c->h_ss_totals[1];
+        if (d->nseg)
+            HIPCHK(hipMemcpyAsync(c->h_ss_seg, c->d_ss_seg, (size_t)d->nseg * sizeof(rxg_segment),
+                                  hipMemcpyDeviceToHost, c->stream));
+        if (d->tcp_bytes)
+            HIPCHK(hipMemcpyAsync(c->h_ss_payload, c->d_ss_payload, d->tcp_bytes,
+                                  hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipEventRecord(c->tev[4], c->stream)); // after the results' copy out
+    HIPCHK(hipStreamSynchronize(c->stream));
+    rc = rxg_wait(c, t); // (the verdicts' copy out, on s_d2h)
+    if (rc) return rc;
+    if (ms) {
+        ms[0] = (float)(t1 - t0);
+        for (int k = 0; k < 4; ++k) HIPCHK(hipEventElapsedTime(&ms[k + 1], c->tev[k], c->tev[k + 1]));
+        ms[5] = (float)(now_ms() - t0);
+    }
+    return RXG_OK;
 }
 
 int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const uint16_t *d_len,

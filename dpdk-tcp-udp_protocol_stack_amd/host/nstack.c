@@ -152,8 +152,10 @@ struct tcp_stream {
     pthread_mutex_t mutex;
     pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
     uint32_t flow_id;           /* stable id in the GPU flow tables (verdict flow_id) */
+    uint32_t rq, sq;            /* fragments in rcvbuf / sndbuf (a batch item holds several) */
 };
 
+struct frag_batch;
 struct tcp_fragment {
     uint16_t sport, dport;
     uint32_t seqnum, acknum;
@@ -163,7 +165,96 @@ struct tcp_fragment {
     uint32_t option[10];
     unsigned char *data;
     uint32_t length;
+    struct frag_batch *batch; /* non-NULL: this ring item is a burst's fragments for the
+                                 tcb, in one allocation (GPU segment sort) */
 };
+
+/* The fragments one burst queues on one tcb (its receive fragments, or the
+ * ACKs it sends), as the GPU's segment sort hands a connection's segments
+ * over: one allocation holding the fragments and their payloads, one ring
+ * item.  Each fragment reads as the one tcp_process would have queued on its
+ * own (tcp.c:133-216); the tcb's rq / sq count fragments, not items, so the
+ * rings keep their D_RING_SIZE-fragment capacity. */
+struct frag_batch {
+    struct tcp_fragment item; /* the ring item (item.batch = this batch) */
+    uint32_t n, next;         /* fragments; the next one to read */
+    struct tcp_fragment *frag;
+};
+
+/* ---- a tcb's fragment queues: logical fragments over ring items ---------- */
+static void frag_item_free(struct tcp_fragment *f) {
+    if (f->batch) {
+        free(f->batch); /* (fragments and payloads live in the batch's allocation) */
+    } else {
+        free(f->data);
+        free(f);
+    }
+}
+/* a standalone fragment at the tail (ring full: -ENOBUFS, the caller keeps it) */
+static int tq_push(struct nring *r, uint32_t *cnt, struct tcp_fragment *f) {
+    if (*cnt >= D_RING_SIZE || ring_enqueue(r, f)) return -ENOBUFS;
+    (*cnt)++;
+    return 0;
+}
+/* the logical head, or NULL */
+static struct tcp_fragment *tq_front(struct nring *r) {
+    struct tcp_fragment *f;
+    if (ring_peek(r, (void **)&f)) return NULL;
+    return f->batch ? &f->batch->frag[f->batch->next] : f;
+}
+/* fragment k (0 = head), or NULL */
+static struct tcp_fragment *tq_at(struct nring *r, uint32_t k) {
+    void *p;
+    for (uint32_t i = 0; ring_peek_at(r, i, &p) == 0; i++) {
+        struct tcp_fragment *f = p;
+        const uint32_t left = f->batch ? f->batch->n - f->batch->next : 1u;
+        if (k < left) return f->batch ? &f->batch->frag[f->batch->next + k] : f;
+        k -= left;
+    }
+    return NULL;
+}
+/* drop the head fragment and its data */
+static void tq_pop(struct nring *r, uint32_t *cnt) {
+    struct tcp_fragment *f;
+    if (ring_peek(r, (void **)&f)) return;
+    (*cnt)--;
+    if (f->batch && ++f->batch->next < f->batch->n) return;
+    ring_dequeue(r, (void **)&f);
+    frag_item_free(f);
+}
+/* the head fragment taken out as a standalone one the caller owns (a batch
+ * member is copied out), or NULL */
+static struct tcp_fragment *tq_detach(struct nring *r, uint32_t *cnt) {
+    struct tcp_fragment *f;
+    if (ring_peek(r, (void **)&f)) return NULL;
+    if (!f->batch) {
+        ring_dequeue(r, (void **)&f);
+        (*cnt)--;
+        return f;
+    }
+    const struct tcp_fragment *m = &f->batch->frag[f->batch->next];
+    struct tcp_fragment *c = calloc(1, sizeof(*c));
+    if (!c) return NULL;
+    *c = *m;
+    c->batch = NULL;
+    c->data = NULL;
+    if (m->data) {
+        c->data = malloc((size_t)m->length + 1);
+        if (!c->data) {
+            free(c);
+            return NULL;
+        }
+        memcpy(c->data, m->data, m->length);
+        c->data[m->length] = 0;
+    }
+    tq_pop(r, cnt);
+    return c;
+}
+static void tq_clear(struct nring *r, uint32_t *cnt) {
+    void *p;
+    while (ring_dequeue(r, &p) == 0) frag_item_free(p);
+    *cnt = 0;
+}
 
 #define LL_ADD(item, list)                                                                         \
     do {                                                                                           \
@@ -224,6 +315,8 @@ static uint32_t *s_tcb_id;
 static uint32_t s_nt, s_tcb_xcap;
 static rxg_verdict *s_v;
 static uint32_t s_v_cap;
+static uint8_t *s_handled; /* per frame of the burst: delivered by the segment sort path */
+static uint32_t s_handled_cap;
 
 static int get_fd_frombitmap(void) { /* common.c:72-85 */
     for (int fd = D_DEFAULT_FD_NUM; fd < D_MAX_FD_COUNT; fd++)
@@ -246,6 +339,7 @@ static int set_fd_frombitmap(int fd) { /* common.c:87-95 */
  * the fd (naccept), or freed, so the socket calls look their descriptor up
  * in O(1) instead of walking up to 1024 blocks per nrecvfrom. */
 static void *g_fd_cb[D_MAX_FD_COUNT];
+static uint32_t g_fd_nblk[D_MAX_FD_COUNT]; /* live blocks carrying each fd */
 
 static void fd_refresh(int fd) {
     if (fd < 0 || fd >= D_MAX_FD_COUNT) return;
@@ -255,6 +349,30 @@ static void fd_refresh(int fd) {
     for (struct tcp_stream *s = g_tcb_set; s && !cb; s = s->next)
         if (s->fd == fd) cb = s;
     g_fd_cb[fd] = cb;
+}
+
+/* a block just took fd (nsocket, naccept): it is the newest of its list, so
+ * it is the answer unless it is a tcb and a UDP block holds the fd (the walk
+ * looks at the UDP list first).  The protocol byte sits at the same offset in
+ * both blocks (as the reference's get_hostinfo_fromfd assumes). */
+static void fd_add(int fd, void *cb) {
+    if (fd < 0 || fd >= D_MAX_FD_COUNT) return;
+    g_fd_nblk[fd]++;
+    const void *cur = g_fd_cb[fd];
+    if (!cur || ((const struct localhost *)cb)->protocol == IPPROTO_UDP ||
+        ((const struct localhost *)cur)->protocol != IPPROTO_UDP)
+        g_fd_cb[fd] = cb;
+}
+/* block cb (already unlinked) carried fd and is freed: O(1) unless it was the
+ * answer and another block still carries the fd (then the walk) */
+static void fd_del(int fd, const void *cb) {
+    if (fd < 0 || fd >= D_MAX_FD_COUNT) return;
+    if (g_fd_nblk[fd]) g_fd_nblk[fd]--;
+    if (g_fd_cb[fd] != cb) return;
+    if (!g_fd_nblk[fd])
+        g_fd_cb[fd] = NULL;
+    else
+        fd_refresh(fd);
 }
 
 static void *get_hostinfo_fromfd(int fd) {
@@ -415,26 +533,20 @@ void nstack_fini(void) {
     while (g_tcb_set) {
         struct tcp_stream *s = g_tcb_set;
         LL_REMOVE(s, g_tcb_set);
-        void *p;
-        while (ring_dequeue(s->rcvbuf, &p) == 0) {
-            free(((struct tcp_fragment *)p)->data);
-            free(p);
-        }
-        while (ring_dequeue(s->sndbuf, &p) == 0) {
-            free(((struct tcp_fragment *)p)->data);
-            free(p);
-        }
+        tq_clear(s->rcvbuf, &s->rq);
+        tq_clear(s->sndbuf, &s->sq);
         ring_free(s->rcvbuf);
         ring_free(s->sndbuf);
         free(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
     memset(g_fd_cb, 0, sizeof(g_fd_cb));
+    memset(g_fd_nblk, 0, sizeof(g_fd_nblk));
     free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v), free(s_udp_id),
-        free(s_tcb_id);
+        free(s_tcb_id), free(s_handled);
     s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL, s_udp_id = NULL,
-    s_tcb_id = NULL;
-    s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = s_udp_xcap = s_tcb_xcap = 0;
+    s_tcb_id = NULL, s_handled = NULL;
+    s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = s_udp_xcap = s_tcb_xcap = s_handled_cap = 0;
     memset(g_stat, 0, sizeof(g_stat));
     g_isn_seed = 0;
     while (g_arp) {
@@ -485,7 +597,7 @@ int nsocket(int domain, int type, int protocol) {
             goto fail;
         }
         LL_ADD(h, g_pstHost);
-        fd_refresh(fd);
+        fd_add(fd, h);
     } else if (type == SOCK_STREAM) { /* :304-337 */
         struct tcp_stream *s = calloc(1, sizeof(*s));
         if (!s) goto fail;
@@ -509,7 +621,7 @@ int nsocket(int domain, int type, int protocol) {
             goto fail;
         }
         LL_ADD(s, g_tcb_set);
-        fd_refresh(fd);
+        fd_add(fd, s);
     }
     pthread_mutex_unlock(&g_lock);
     return fd;
@@ -578,7 +690,7 @@ int naccept(int sockfd, struct sockaddr *addr, socklen_t *addrlen) { /* :388-416
         pthread_cond_wait(&s->accept_cond, &g_lock);
     }
     apt->fd = get_fd_frombitmap();
-    fd_refresh(apt->fd);
+    fd_add(apt->fd, apt);
     if (addr) {
         struct sockaddr_in *sa = (struct sockaddr_in *)addr;
         sa->sin_family = AF_INET;
@@ -615,7 +727,7 @@ ssize_t nsend(int sockfd, const void *buf, size_t len, int flags) { /* :418-460 
                 memcpy(f->data, buf, len);
                 f->length = (uint32_t)len;
                 pthread_mutex_lock(&s->mutex);
-                if (ring_enqueue(s->sndbuf, f)) {
+                if (tq_push(s->sndbuf, &s->sq, f)) {
                     free(f->data);
                     free(f);
                     n = -1;
@@ -642,9 +754,9 @@ ssize_t nrecv(int sockfd, void *buf, size_t len, int flags) { /* :462-515 */
 }
 
 static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags) {
-    struct tcp_fragment *f = NULL;
+    struct tcp_fragment *f;
     pthread_mutex_lock(&s->mutex);
-    while (ring_dequeue(s->rcvbuf, (void **)&f) < 0) {
+    while ((f = tq_front(s->rcvbuf)) == NULL) {
         if (flags & MSG_DONTWAIT) {
             pthread_mutex_unlock(&s->mutex);
             errno = EAGAIN;
@@ -653,21 +765,21 @@ static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags)
         pthread_cond_wait(&s->cond, &s->mutex);
     }
     ssize_t length;
-    if (f->length > len) { /* :483-496: split, re-enqueue the rest */
+    if (f->length > len) { /* :483-496: dequeue, split, re-enqueue the rest at the tail */
+        f = tq_detach(s->rcvbuf, &s->rq);
+        if (!f) {
+            pthread_mutex_unlock(&s->mutex);
+            return -1;
+        }
         memcpy(buf, f->data, len);
         memmove(f->data, f->data + len, f->length - len);
         f->length -= (uint32_t)len;
         length = f->length; /* the reference returns the REMAINING length here */
-        ring_enqueue(s->rcvbuf, f);
-    } else if (f->length == 0) { /* :497-501: 0-length fragment = EOF */
-        free(f->data);
-        free(f);
-        length = 0;
-    } else {
-        memcpy(buf, f->data, f->length);
+        if (tq_push(s->rcvbuf, &s->rq, f)) frag_item_free(f);
+    } else { /* :497-514: a 0-length fragment is EOF (returns 0) */
+        if (f->length) memcpy(buf, f->data, f->length);
         length = f->length;
-        free(f->data);
-        free(f);
+        tq_pop(s->rcvbuf, &s->rq);
     }
     pthread_mutex_unlock(&s->mutex);
     return length;
@@ -813,9 +925,9 @@ int nclose(int fd) { /* :609-666 */
         }
         ring_free(h->rcvbuf);
         ring_free(h->sndbuf);
+        fd_del(fd, h);
         free(h);
         set_fd_frombitmap(fd);
-        fd_refresh(fd);
     } else {
         struct tcp_stream *s = info;
         if (s->status != TCP_STATUS_LISTEN) { /* queue FIN, wait for LAST_ACK */
@@ -829,7 +941,7 @@ int nclose(int fd) { /* :609-666 */
                 f->windows = D_TCP_INITIAL_WINDOW;
                 f->hdrlen_off = 0x50;
                 pthread_mutex_lock(&s->mutex);
-                if (ring_enqueue(s->sndbuf, f)) free(f);
+                if (tq_push(s->sndbuf, &s->sq, f)) free(f);
                 pthread_mutex_unlock(&s->mutex);
             }
             s->status = TCP_STATUS_LAST_ACK;
@@ -838,10 +950,12 @@ int nclose(int fd) { /* :609-666 */
         } else {
             unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
+            tq_clear(s->rcvbuf, &s->rq);
+            tq_clear(s->sndbuf, &s->sq);
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
+            fd_del(fd, s);
             free(s);
-            fd_refresh(fd);
             /* the reference leaves the listener's fd set in the bitmap here */
         }
     }
@@ -868,13 +982,14 @@ static inline uint32_t rdbe32(const uint8_t *p) { return ntohl(rd32(p)); }
  * (rcv_nxt += payloadlen at :244-248 and :266-279, no ntohl round trip). */
 
 /* tcp_stream_search (common.c:31-55) over the live list: the exact 4-tuple
- * (status ignored), else the first LISTEN block on dport (dst IP ignored) */
+ * (status ignored), else the first LISTEN block on dport (dst IP ignored).
+ * Answered in O(1) by the context's host image of the flow tables, which
+ * every block change updates at once (reg_tcb / unreg_tcb / restate_tcb:
+ * newest-first chains per key, the newest LISTEN block per port), instead of
+ * the reference's two list walks (~192 us each at 64K tcbs). */
 static struct tcp_stream *tcb_search(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport) {
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
-        if (s->sip == sip && s->dip == dip && s->sport == sport && s->dport == dport) return s;
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
-        if (s->dport == dport && s->status == TCP_STATUS_LISTEN) return s;
-    return NULL;
+    const uint32_t id = rxg_ft_lookup_tcp(g_ctx, sip, dip, sport, dport);
+    return id < s_tcb_cap ? s_tcb_cb[id] : NULL;
 }
 
 static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport,
@@ -905,10 +1020,11 @@ static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, ui
     return s;
 }
 
-static void wake_acceptors(uint16_t dport) { /* tcp.c:107-116 */
-    for (struct tcp_stream *l = g_tcb_set; l; l = l->next)
-        if (l->dport == dport && l->status == TCP_STATUS_LISTEN)
-            pthread_cond_broadcast(&l->accept_cond);
+/* tcp.c:107-116: the listener tcp_stream_search(0, 0, 0, dport) finds is
+ * woken (its naccept) */
+static void wake_acceptors(uint16_t dport) {
+    struct tcp_stream *l = tcb_search(0, 0, 0, dport);
+    if (l) pthread_cond_broadcast(&l->accept_cond);
 }
 
 static void queue_ctl(struct tcp_stream *s, uint16_t sport_raw, uint16_t dport_raw, uint8_t flags) {
@@ -922,7 +1038,7 @@ static void queue_ctl(struct tcp_stream *s, uint16_t sport_raw, uint16_t dport_r
     f->windows = D_TCP_INITIAL_WINDOW;
     f->hdrlen_off = 0x50;
     pthread_mutex_lock(&s->mutex);
-    if (ring_enqueue(s->sndbuf, f)) free(f);
+    if (tq_push(s->sndbuf, &s->sq, f)) free(f);
     pthread_mutex_unlock(&s->mutex);
 }
 
@@ -950,7 +1066,7 @@ static void tcp_enqueue_rcv(struct tcp_stream *s, const uint8_t *f, uint32_t cap
         fr->length = (uint32_t)plen;
     }
     pthread_mutex_lock(&s->mutex);
-    int e = ring_enqueue(s->rcvbuf, fr);
+    int e = tq_push(s->rcvbuf, &s->rq, fr);
     if (!e) pthread_cond_signal(&s->cond);
     pthread_mutex_unlock(&s->mutex);
     if (e) {
@@ -1019,20 +1135,12 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
             s->status = TCP_STATUS_CLOSED;
             unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
-            void *p;
-            while (ring_dequeue(s->rcvbuf, &p) == 0) {
-                free(((struct tcp_fragment *)p)->data);
-                free(p);
-            }
-            while (ring_dequeue(s->sndbuf, &p) == 0) {
-                free(((struct tcp_fragment *)p)->data);
-                free(p);
-            }
+            tq_clear(s->rcvbuf, &s->rq);
+            tq_clear(s->sndbuf, &s->sq);
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
-            const int sfd = s->fd;
+            fd_del(s->fd, s);
             free(s);
-            fd_refresh(sfd);
             g_burst_mutated = 1;
         }
         break;
@@ -1063,11 +1171,11 @@ static int deliver_tcp(const rxg_mbuf *m, const rxg_verdict *v) {
     return RXG_RC_OK;
 }
 
-/* get_hostinfo_fromip_port (common.c:97-108) over the live list */
+/* get_hostinfo_fromip_port (common.c:97-108) over the live list, answered
+ * by the host image of the flow tables (O(1), as tcb_search) */
 static struct localhost *udp_search(uint32_t dip, uint16_t dport) {
-    for (struct localhost *h = g_pstHost; h; h = h->next)
-        if (h->localip == dip && h->localport == dport && h->protocol == IPPROTO_UDP) return h;
-    return NULL;
+    const uint32_t id = rxg_ft_lookup_udp(g_ctx, dip, dport);
+    return id < s_udp_cap ? s_udp_cb[id] : NULL;
 }
 
 /* udp.c:25-52 for one verdict (g_lock held).  A verdict made for an older
@@ -1149,11 +1257,13 @@ static void arp_learn(const rxg_mbuf *m) {
     arp_insert(rd32(f + 28), f + 6);
 }
 
-/* verdicts -> sockets, frame by frame in burst order (g_lock held) */
-static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out) {
+/* verdicts -> sockets, frame by frame in burst order (g_lock held); frames
+ * marked in `handled` (nullable) were delivered already (deliver_tcp_sorted) */
+static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, int *rc_out,
+                         const uint8_t *handled) {
     int delivered = 0;
-    g_burst_mutated = 0;
     for (uint32_t i = 0; i < n; i++) {
+        if (handled && handled[i]) continue;
         int rc = v[i].rc;
         if (v[i].cls == RXG_CLS_ARP) arp_learn(m[i]);
         if (v[i].cls == RXG_CLS_TCP)
@@ -1174,7 +1284,8 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
     int delivered = 0;
     if (rc == RXG_OK) {
         g_burst_stale = gen != g_snap_gen; /* classified against other lists */
-        delivered = deliver_burst(m, n, v, rc_out);
+        g_burst_mutated = 0;
+        delivered = deliver_burst(m, n, v, rc_out, NULL);
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
@@ -1246,35 +1357,215 @@ static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const ui
     return delivered;
 }
 
+/* A connection's segments of one burst, from the GPU's segment sort, through
+ * tcp_handle_established (tcp.c:218-297) in burst order (g_lock held).  Only
+ * for a tcb whose state cannot move a lookup: ESTABLISHED (it may go to
+ * CLOSE_WAIT on a FIN, which no lookup reads) and the states whose segments
+ * are no-ops (CLOSE_WAIT, CLOSED, ...).  Such a tcb's segments interact with
+ * no other frame of the burst (no block is created or freed for them, and
+ * every frame of their 4-tuple names this tcb), so running them connection
+ * by connection equals the reference's frame-by-frame loop.  The receive
+ * fragments the segments queue (ng_tcp_enqueue_recvbuffer, tcp.c:133-185)
+ * and the ACKs they send (tcp.c:187-216) go in as one batch item each: one
+ * allocation, payloads copied from the gathered buffer.  Returns 0, or 1 when
+ * the tcb's state needs the frame-by-frame path (LISTEN, SYN_RCVD, LAST_ACK). */
+static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_t k,
+                            const uint8_t *payload, uint8_t *handled, int *rc_out) {
+    if (s->status == TCP_STATUS_LISTEN || s->status == TCP_STATUS_SYN_RCVD ||
+        s->status == TCP_STATUS_LAST_ACK)
+        return 1;
+    /* the fragments and ACKs the segments make, in order (the state changes
+     * at most once: ESTABLISHED -> CLOSE_WAIT on a FIN) */
+    uint32_t nfr = 0, nack = 0;
+    uint64_t pbytes = 0;
+    int st = s->status;
+    for (uint32_t j = 0; j < k; j++) {
+        handled[sg[j].frame] = 1;
+        if (rc_out) rc_out[sg[j].frame] = RXG_RC_OK;
+        if (st != TCP_STATUS_ESTABLISHED) continue;
+        if (sg[j].flags & TCP_PSH) {
+            nfr++, nack++;
+            if (sg[j].plen > 0) pbytes += (uint64_t)sg[j].plen;
+        }
+        if (sg[j].flags & TCP_FIN) nfr++, nack++, st = TCP_STATUS_CLOSE_WAIT;
+    }
+    g_stat[2] += k;
+    if (!nfr) return 0;
+    pthread_mutex_lock(&s->mutex);
+    const uint32_t rroom = s->rq < D_RING_SIZE ? D_RING_SIZE - s->rq : 0;
+    const uint32_t aroom = s->sq < D_RING_SIZE ? D_RING_SIZE - s->sq : 0;
+    const uint32_t rtake = nfr < rroom ? nfr : rroom, atake = nack < aroom ? nack : aroom;
+    struct frag_batch *rb = NULL, *ab = NULL;
+    if (rtake) { /* payload room: only the fragments that fit (a full ring drops the rest) */
+        rb = malloc(sizeof(*rb) + rtake * sizeof(struct tcp_fragment) + pbytes + 1);
+        if (rb) {
+            memset(&rb->item, 0, sizeof(rb->item));
+            rb->item.batch = rb;
+            rb->n = rtake;
+            rb->next = 0;
+            rb->frag = (struct tcp_fragment *)(rb + 1);
+        }
+    }
+    if (atake) {
+        ab = malloc(sizeof(*ab) + atake * sizeof(struct tcp_fragment));
+        if (ab) {
+            memset(&ab->item, 0, sizeof(ab->item));
+            ab->item.batch = ab;
+            ab->n = atake;
+            ab->next = 0;
+            ab->frag = (struct tcp_fragment *)(ab + 1);
+        }
+    }
+    unsigned char *pp = rb ? (unsigned char *)(rb->frag + rtake) : NULL;
+    uint32_t fi = 0, ai = 0;
+    /* one receive fragment (tcp.c:133-185): plen > 0 a payload copy (bytes past
+     * the capture read 0), else the 0-length EOF; g_stat as tcp_enqueue_rcv */
+    #define PUT_FRAG(SEG, PLEN)                                                              \
+        do {                                                                                 \
+            if (fi < rtake && rb) {                                                          \
+                struct tcp_fragment *fr = &rb->frag[fi];                                     \
+                memset(fr, 0, sizeof(*fr));                                                  \
+                fr->dport = ntohs((SEG)->dport);                                             \
+                fr->sport = ntohs((SEG)->sport);                                             \
+                if ((PLEN) > 0) {                                                            \
+                    fr->data = pp;                                                           \
+                    fr->length = (uint32_t)(PLEN);                                           \
+                    memcpy(pp, payload + (SEG)->offset, (SEG)->ncopy);                       \
+                    if ((uint32_t)(PLEN) > (SEG)->ncopy)                                     \
+                        memset(pp + (SEG)->ncopy, 0, (uint32_t)(PLEN) - (SEG)->ncopy);       \
+                    pp += (uint32_t)(PLEN);                                                  \
+                }                                                                            \
+                g_stat[4]++;                                                                 \
+            } else {                                                                         \
+                g_stat[1]++;                                                                 \
+            }                                                                                \
+            fi++;                                                                            \
+        } while (0)
+    /* the ACK after it (ng_tcp_send_ackpkt, tcp.c:187-216) */
+    #define PUT_ACK(SEG)                                                                     \
+        do {                                                                                 \
+            if (ai < atake && ab) {                                                          \
+                struct tcp_fragment *a = &ab->frag[ai];                                      \
+                memset(a, 0, sizeof(*a));                                                    \
+                a->sport = (SEG)->dport;                                                     \
+                a->dport = (SEG)->sport;                                                     \
+                a->seqnum = s->snd_nxt;                                                      \
+                a->acknum = s->rcv_nxt;                                                      \
+                a->tcp_flags = TCP_ACK;                                                      \
+                a->windows = D_TCP_INITIAL_WINDOW;                                           \
+                a->hdrlen_off = 0x50;                                                        \
+            }                                                                                \
+            ai++;                                                                            \
+        } while (0)
+    for (uint32_t j = 0; j < k && s->status == TCP_STATUS_ESTABLISHED; j++) {
+        const rxg_segment *g = &sg[j];
+        if (g->flags & TCP_PSH) { /* tcp.c:226-262 */
+            PUT_FRAG(g, g->plen);
+            s->rcv_nxt += (uint32_t)g->plen;
+            s->snd_nxt = g->ack;
+            PUT_ACK(g);
+        }
+        if (g->flags & TCP_FIN) { /* tcp.c:264-294: CLOSE_WAIT, EOF, ACK */
+            s->status = TCP_STATUS_CLOSE_WAIT;
+            PUT_FRAG(g, 0);
+            s->rcv_nxt += 1;
+            s->snd_nxt = g->ack;
+            PUT_ACK(g);
+        }
+    }
+    #undef PUT_FRAG
+    #undef PUT_ACK
+    if (rb) {
+        if (ring_enqueue(s->rcvbuf, &rb->item)) { /* (not reached: items <= fragments <= capacity) */
+            free(rb);
+            g_stat[4] -= rtake, g_stat[1] += rtake;
+        } else {
+            s->rq += rtake;
+            pthread_cond_signal(&s->cond); /* tcp.c:178-180 */
+        }
+    }
+    if (ab) {
+        if (ring_enqueue(s->sndbuf, &ab->item))
+            free(ab);
+        else
+            s->sq += atake;
+    }
+    pthread_mutex_unlock(&s->mutex);
+    if (st == TCP_STATUS_CLOSE_WAIT) restate_tcb(s, 0);
+    return 0;
+}
+
+/* the sorted segments, connection by connection (g_lock held); frames of
+ * connections that need the frame-by-frame path are left unmarked */
+static void deliver_tcp_sorted(const rxg_delivery *d, uint8_t *handled, int *rc_out) {
+    const rxg_segment *sg = d->seg;
+    for (uint32_t a = 0, b; a < d->nseg; a = b) {
+        b = a + 1;
+        while (b < d->nseg && sg[b].flow == sg[a].flow) b++;
+        struct tcp_stream *s = sg[a].flow < s_tcb_cap ? s_tcb_cb[sg[a].flow] : NULL;
+        if (s) deliver_tcp_conn(s, sg + a, b - a, d->tcp_payload, handled, rc_out);
+    }
+}
+
+/* the last nstack_rx_burst's phases (nstack_last_burst_phases) */
+static float g_phase_ms[12];
+
+static double mono_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
     pthread_mutex_lock(&g_lock);
+    const double t0 = mono_ms();
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
-    const rxg_dgram *dg = NULL;
-    const uint32_t *first = NULL;
-    const uint8_t *payload = NULL;
-    uint32_t ndg = 0;
-    uint64_t nbytes = 0;
-    /* UDP payloads grouped per socket on the GPU (<= RXG_COMPACT_MAX_FLOWS ids:
-     * always, with the reference's 1024 descriptors) */
-    const int compact = rxg_num_udp_ids(g_ctx) <= RXG_COMPACT_MAX_FLOWS;
-    if (rc == RXG_OK)
-        rc = compact ? rxg_process_mbufs_udp(g_ctx, m, n, s_v, &dg, &first, &payload, &ndg, &nbytes)
-                     : rxg_process_mbufs(g_ctx, m, n, s_v);
+    if (rc == RXG_OK && grow((void **)&s_handled, &s_handled_cap, n ? n : 1, 1)) rc = RXG_ENOMEM;
+    rxg_delivery d;
+    float gms[8] = {0};
+    /* the device half of delivery in one pass: classify, UDP payloads grouped
+     * per socket (<= RXG_COMPACT_MAX_FLOWS ids: always, with the reference's
+     * 1024 descriptors), TCP segments sorted per connection with their
+     * payloads gathered */
+    if (rc == RXG_OK) rc = rxg_process_mbufs_deliver(g_ctx, m, n, s_v, &d, gms);
     int delivered = 0;
     if (rc == RXG_OK) {
+        const double t1 = mono_ms();
         if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
-        if (compact) {
-            delivered = deliver_udp_batches(m, dg, first, payload, rxg_num_udp_ids(g_ctx));
+        g_burst_mutated = 0;
+        if (d.first) {
+            delivered = deliver_udp_batches(m, d.dgram, d.first, d.udp_payload,
+                                            rxg_num_udp_ids(g_ctx));
             g_udp_done = 1; /* the per-frame loop leaves UDP alone */
         }
-        delivered += deliver_burst(m, n, s_v, rc_out);
+        const double t2 = mono_ms();
+        memset(s_handled, 0, n);
+        if (d.nseg) deliver_tcp_sorted(&d, s_handled, rc_out);
+        const double t3 = mono_ms();
+        delivered += deliver_burst(m, n, s_v, rc_out, s_handled);
         g_udp_done = 0;
+        const double t4 = mono_ms();
+        for (int k = 0; k < 6; k++) g_phase_ms[k] = gms[k];
+        g_phase_ms[6] = (float)(t2 - t1); /* UDP batches to the sockets */
+        g_phase_ms[7] = (float)(t3 - t2); /* TCP connections from the segment sort */
+        g_phase_ms[8] = (float)(t4 - t3); /* the frame-by-frame loop (the rest) */
+        g_phase_ms[9] = (float)(t4 - t0); /* the whole call */
+        g_phase_ms[10] = (float)d.nseg;
+        g_phase_ms[11] = (float)d.ndgram;
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
+}
+
+int nstack_last_burst_phases(float ms[12]) {
+    if (!ms) return RXG_EINVAL;
+    pthread_mutex_lock(&g_lock);
+    memcpy(ms, g_phase_ms, sizeof(g_phase_ms));
+    pthread_mutex_unlock(&g_lock);
+    return RXG_OK;
 }
 
 int nstack_tcb_state(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, int32_t *status,
@@ -1301,9 +1592,8 @@ int nstack_tcb_sndq(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport, 
     for (struct tcp_stream *s = g_tcb_set; s; s = s->next)
         if (s->sip == sip && s->dip == dip && s->sport == sport && s->dport == dport) {
             pthread_mutex_lock(&s->mutex);
-            void *p = NULL;
-            if (ring_peek_at(s->sndbuf, k, &p) == 0) {
-                const struct tcp_fragment *f = p;
+            const struct tcp_fragment *f = tq_at(s->sndbuf, k);
+            if (f) {
                 if (flags) *flags = f->tcp_flags;
                 if (acknum) *acknum = f->acknum;
                 rc = 0;
@@ -1376,12 +1666,8 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
         ssize_t r;
         while ((r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT)) >= 0)
             if (r > 0) got++, nb += (uint64_t)r;
-        void *p; /* its queued control fragments (ACKs) sent */
-        pthread_mutex_lock(&s->mutex);
-        while (ring_dequeue(s->sndbuf, &p) == 0) {
-            free(((struct tcp_fragment *)p)->data);
-            free(p);
-        }
+        pthread_mutex_lock(&s->mutex); /* its queued control fragments (ACKs) sent */
+        tq_clear(s->sndbuf, &s->sq);
         pthread_mutex_unlock(&s->mutex);
     }
     pthread_mutex_unlock(&g_lock);
@@ -1577,19 +1863,17 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
     }
     /* tcp_out, tcp.c:492-555: at most one fragment per tcb, list order */
     for (struct tcp_stream *s = g_tcb_set; s && n < max_frames && !full; s = s->next) {
-        struct tcp_fragment *f = NULL;
         pthread_mutex_lock(&s->mutex);
-        if (!s->sndbuf || ring_peek(s->sndbuf, (void **)&f) != 0) {
+        struct tcp_fragment *f = s->sndbuf ? tq_front(s->sndbuf) : NULL;
+        if (!f) {
             pthread_mutex_unlock(&s->mutex);
             continue;
         }
         const uint8_t *dmac = arp_lookup(s->sip); /* the remote side (tcp.c:521) */
         const uint64_t fl64 = dmac ? 54u + (uint64_t)f->optlen * 4u + f->length : 42u;
         if (fl64 > 65535u) {
-            ring_dequeue(s->sndbuf, (void **)&f);
+            tq_pop(s->sndbuf, &s->sq);
             pthread_mutex_unlock(&s->mutex);
-            free(f->data);
-            free(f);
             g_stat[1]++;
             continue;
         }
@@ -1599,22 +1883,19 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
             full = 1;
             break;
         }
-        ring_dequeue(s->sndbuf, (void **)&f);
         uint8_t *fp = pkts + pos;
-        if (!dmac) { /* tcp.c:522-535 */
+        if (!dmac) { /* tcp.c:522-535: an ARP request, the fragment dequeued and queued again */
             enc_arp(fp, k_default_arp_mac, s->dip, s->sip);
-            if (ring_enqueue(s->sndbuf, f)) {
-                free(f->data);
-                free(f);
+            struct tcp_fragment *d = tq_detach(s->sndbuf, &s->sq);
+            if (d && tq_push(s->sndbuf, &s->sq, d)) {
+                frag_item_free(d);
                 g_stat[1]++;
             }
-            pthread_mutex_unlock(&s->mutex);
         } else {
-            pthread_mutex_unlock(&s->mutex);
             enc_tcp(fp, s->localmac, dmac, s->dip, s->sip, f); /* local -> remote (tcp.c:542) */
-            free(f->data);
-            free(f);
+            tq_pop(s->sndbuf, &s->sq);
         }
+        pthread_mutex_unlock(&s->mutex);
         tx_place(fp, fl, &pos, off, len, &n);
     }
     rxg_ctx *ctx = g_ctx;

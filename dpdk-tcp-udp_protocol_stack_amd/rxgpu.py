@@ -103,6 +103,17 @@ DGRAM_DTYPE = np.dtype([("frame", "<u4"), ("offset", "<u4"), ("sip", "<u4"), ("s
                         ("len", "<u2")])
 assert DGRAM_DTYPE.itemsize == 16
 COMPACT_MAX_FLOWS = 1024
+SEGMENT_DTYPE = np.dtype([("frame", "<u4"), ("flow", "<u4"), ("seq", "<u4"), ("ack", "<u4"),
+                          ("plen", "<i4"), ("offset", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+                          ("ncopy", "<u2"), ("flags", "u1"), ("hl", "u1")])
+assert SEGMENT_DTYPE.itemsize == 32
+
+
+class Delivery(C.Structure):
+    """rxg_delivery (rxg_process_mbufs_deliver's results)"""
+    _fields_ = [("dgram", C.c_void_p), ("first", C.c_void_p), ("udp_payload", C.c_void_p),
+                ("ndgram", C.c_uint32), ("nseg", C.c_uint32), ("udp_bytes", C.c_uint64),
+                ("seg", C.c_void_p), ("tcp_payload", C.c_void_p), ("tcp_bytes", C.c_uint64)]
 
 
 class GenCfg(C.Structure):
@@ -150,6 +161,9 @@ _num_udp_ids = _sig("rxg_num_udp_ids", _u32, _vp)
 _udp_compact_dev = _sig("rxg_udp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp,
                         _vp, _u64, _vp, _vp)
 _flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
+_tcp_compact_dev = _sig("rxg_tcp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp,
+                        _u64, _vp, _vp)
+_process_mbufs_deliver = _sig("rxg_process_mbufs_deliver", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
                         _vp, _vp)
@@ -207,7 +221,7 @@ GROUP_ID_BYTES = 128
 EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_flows_sync",
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
-            "rxg_process_mbufs_udp",
+            "rxg_process_mbufs_udp", "rxg_tcp_compact_dev", "rxg_process_mbufs_deliver",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
@@ -433,6 +447,38 @@ class Context:
         _check(_udp_compact_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, p(d_v),
                                 p(d_dgram), p(d_first), p(d_payload), payload_cap, p(d_totals),
                                 stream), "rxg_udp_compact_dev")
+
+    def tcp_compact_dev(self, d_pkts, d_off, d_len, n: int, off_unit_log2: int, d_v, d_seg,
+                        d_payload, payload_cap: int, d_totals, stream=None):
+        """K4: a classified burst's rc-0 TCP segments sorted by tcb id and their
+        PSH payloads gathered (rxg_tcp_compact_dev), async on stream"""
+        def p(x):
+            return x if (x is None or isinstance(x, int)) else x.data_ptr()
+        _check(_tcp_compact_dev(self._h, p(d_pkts), p(d_off), p(d_len), n, off_unit_log2, p(d_v),
+                                p(d_seg), p(d_payload), payload_cap, p(d_totals), stream),
+               "rxg_tcp_compact_dev")
+
+    def process_mbufs_deliver(self, mbufs):
+        """rxg_process_mbufs_deliver over Mbuf structures: (verdicts, dgrams,
+        first, udp payload, segments, tcp payload, phase ms) as numpy copies"""
+        arr = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])
+        out = np.zeros(len(mbufs), VERDICT_DTYPE)
+        d = Delivery()
+        ms = (C.c_float * 8)()
+        _check(_process_mbufs_deliver(self._h, C.cast(arr, _vp), len(mbufs), _ptr(out),
+                                      C.byref(d), ms), "rxg_process_mbufs_deliver")
+
+        def grab(ptr, nbytes, dtype):
+            if not ptr or nbytes == 0:
+                return np.zeros(0, dtype)
+            return np.frombuffer((C.c_uint8 * nbytes).from_address(ptr), np.uint8).copy().view(dtype)
+        nf = _num_udp_ids(self._h)
+        dg = grab(d.dgram, d.ndgram * 16, DGRAM_DTYPE)
+        first = grab(d.first, (nf + 1) * 4, np.uint32) if d.first else None
+        up = grab(d.udp_payload, d.udp_bytes, np.uint8)
+        seg = grab(d.seg, d.nseg * 32, SEGMENT_DTYPE)
+        tp = grab(d.tcp_payload, d.tcp_bytes, np.uint8)
+        return out, dg, first, up, seg, tp, list(ms)
 
     def tx_cksum(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
                  off_unit_log2: int) -> np.ndarray:
@@ -670,6 +716,7 @@ class NStack:
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
                    ("nstack_flow_ids", _i32, [_vp, _u32, _vp, _u32]),
                    ("nstack_drain_all", C.c_int64, [_vp, C.c_size_t, _vp]),
+                   ("nstack_last_burst_phases", _i32, [_vp]),
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
                    ("nstack_tcb_count", _u32, []),
@@ -796,6 +843,15 @@ class NStack:
 
     def tcb_count(self):
         return self.lib.nstack_tcb_count()
+
+    PHASES = ("gather", "h2d", "classify", "compact", "d2h", "lib_call", "udp_deliver",
+              "tcp_deliver", "frame_loop", "rx_burst", "segments", "datagrams")
+
+    def last_burst_phases(self) -> dict:
+        """where the last rx_burst's time went (nstack_last_burst_phases, ms)"""
+        ms = (C.c_float * 12)()
+        _check(self.lib.nstack_last_burst_phases(ms), "nstack_last_burst_phases")
+        return dict(zip(self.PHASES, [float(x) for x in ms]))
 
     @staticmethod
     def mbufs(frames: list[bytes]):

@@ -29,9 +29,16 @@
  * nrecv and an ACK, +FIN queues the EOF marker and moves to CLOSE_WAIT,
  * LAST_ACK+ACK frees the tcb.  A burst is classified against one snapshot of
  * the tcb list; once the burst's own segments change that list (SYN, final
- * ACK), later segments of the burst are looked up again on the live list, so
- * the outcome is the reference's sequential one (a SYN and its ACK may share
- * a burst).  Unresolved merge-conflict hunks of tcp.c take the HEAD side.
+ * ACK), later segments of the burst are looked up again on the live list
+ * (through the host image of the flow tables, O(1) per lookup), so the
+ * outcome is the reference's sequential one (a SYN and its ACK may share a
+ * burst).  Segments of a tcb in ESTABLISHED (or a state whose segments are
+ * no-ops) depend on no other frame of the burst: the GPU sorts them per
+ * connection and gathers their payloads (rxg_process_mbufs_deliver), and
+ * they run connection by connection, each connection's fragments and ACKs
+ * queued as one batch (one allocation); every other frame keeps the
+ * frame-by-frame path.  Unresolved merge-conflict hunks of tcp.c take the
+ * HEAD side.
  */
 #ifndef NSTACK_H
 #define NSTACK_H
@@ -146,6 +153,15 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * Holds the stack's lock for the whole walk (a concurrent nstack_rx_burst
  * waits for it), so no block it reads can be freed under it. */
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
+
+/* Where the last nstack_rx_burst's time went, in ms: [0] gather of the mbufs
+ * into pinned staging (host), [1] copy in, [2] classify (K1), [3] UDP
+ * compaction + TCP segment sort (K3 + K4), [4] copy out of their results
+ * (device, HIP events), [5] the library call as a whole (host clock), then
+ * host delivery: [6] UDP batches to the sockets, [7] TCP connections from
+ * the segment sort, [8] the frame-by-frame loop over the rest, [9] the whole
+ * nstack_rx_burst; [10] segments sorted, [11] datagrams compacted. */
+int nstack_last_burst_phases(float ms[12]);
 
 /* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),
  * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,

@@ -333,6 +333,67 @@ int rxg_process_mbufs_udp(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verd
                           const rxg_dgram **dgram, const uint32_t **first, const uint8_t **payload,
                           uint32_t *ndgram, uint64_t *nbytes);
 
+/* ---- TCP delivery on the GPU: per-connection segment sort + payload gather
+ * The delivery half of tcp_process for segments that found a tcb (verdict
+ * rc 0): the reference walks them frame by frame through the state machine
+ * (tcp.c:373-415); an ESTABLISHED one with PSH gets a malloc'd fragment with
+ * a copy of its payload (ng_tcp_enqueue_recvbuffer, tcp.c:133-185) and an ACK
+ * (tcp.c:218-297).  Here one device pass sorts a classified burst's rc-0 TCP
+ * segments by tcb id — stable, so a connection's segments keep burst order,
+ * the order its state machine must see them in — decodes the header fields
+ * the state machine reads, and gathers the payload of every PSH segment into
+ * one buffer, connection after connection (each at a 16-B aligned offset), so
+ * the host runs each connection's segments in order with one allocation and
+ * one copy per connection per burst.  Any tcb id space. */
+typedef struct rxg_segment {
+    uint32_t frame;  /* burst index of the segment's frame */
+    uint32_t flow;   /* tcb id (the verdict's flow_id) */
+    uint32_t seq;    /* sent_seq, host order (ntohl of frame bytes 38-41) */
+    uint32_t ack;    /* recv_ack, host order (ntohl of frame bytes 42-45) */
+    int32_t plen;    /* total_length - 20 - 4*hl (signed: tcp.c:145-146, 391) */
+    uint32_t offset; /* first payload byte in the payload buffer (16-B aligned) */
+    uint16_t sport;  /* raw (network order) source port, frame bytes 34-35 */
+    uint16_t dport;  /* raw destination port, frame bytes 36-37 */
+    uint16_t ncopy;  /* payload bytes in the buffer: min(plen, caplen - 34 - 4*hl) for a
+                        PSH segment with plen > 0, else 0; the rest of a fragment's plen
+                        bytes read as 0 */
+    uint8_t flags;   /* tcp_flags, frame byte 47 */
+    uint8_t hl;      /* data_off >> 4, frame byte 46 */
+} rxg_segment;       /* 32 bytes; bytes past the captured length read as 0 */
+/* Device form, asynchronous on `stream`: d_v = the burst's verdicts; d_seg
+ * (room for n) gets the rc-0 TCP segments with a tcb id below the id space,
+ * sorted by (flow, frame); d_totals = {segments, payload bytes used, 1 if
+ * payload_cap was too small (those payloads are not written)}.  The device
+ * workspace grows on demand (stream-ordered). */
+int rxg_tcp_compact_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
+                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
+                        const rxg_verdict *d_v, rxg_segment *d_seg, uint8_t *d_payload,
+                        uint64_t payload_cap, uint32_t *d_totals, void *stream);
+
+/* One mbuf burst through the whole device half of delivery: classify
+ * (rxg_process_mbufs), then the UDP compaction (when the UDP id space is at
+ * most RXG_COMPACT_MAX_FLOWS; else dgram/first are NULL and ndgram 0) and
+ * the TCP segment sort and gather, all in one pass over the staged burst.
+ * Verdicts into `out`; the other results stay in pinned buffers the context
+ * owns, valid until its next burst call.  `ms` (nullable, 8 floats): the
+ * phases of this burst in ms — [0] host gather of the mbufs into pinned
+ * staging; from HIP events on the device: [1] copy in, [2] classify (K1),
+ * [3] the compactions (K3 + K4), [4] copy out of their results; [5] the
+ * whole call (host clock); [6], [7] 0.  Synchronous. */
+typedef struct rxg_delivery {
+    const rxg_dgram *dgram;     /* UDP: as rxg_process_mbufs_udp */
+    const uint32_t *first;
+    const uint8_t *udp_payload;
+    uint32_t ndgram;
+    uint32_t nseg;              /* TCP: segments, sorted by (tcb id, frame) */
+    uint64_t udp_bytes;
+    const rxg_segment *seg;
+    const uint8_t *tcp_payload;
+    uint64_t tcp_bytes;
+} rxg_delivery;
+int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                              rxg_delivery *d, float ms[8]);
+
 /* TX checksum generation (the send side's per-frame work, udp.c:84-95 and
  * tcp.c:444-463): for every IPv4 frame of the burst, the IPv4 header checksum
  * (rte_ipv4_cksum, rte_ip.h:255-265) is written at frame offset 24, and for

@@ -72,6 +72,9 @@ int oracle_tcb_state(const oracle_stack *st, uint32_t sip, uint32_t dip, uint16_
 int oracle_tcb_sndq(const oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t sport,
                     uint16_t dport, uint32_t k, uint8_t *flags, uint32_t *acknum);
 uint32_t oracle_tcb_count(const oracle_stack *st);
+/* test hook: install a tcb with this status (tcp_stream_create + LL_ADD) */
+int oracle_tcb_add(oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport,
+                   int status);
 
 #ifdef __cplusplus
 }

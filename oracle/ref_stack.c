@@ -556,6 +556,26 @@ int oracle_tcb_sndq(const oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t
     return -1;
 }
 
+/* test hook: a tcb installed as tcp_stream_create + LL_ADD would leave it
+ * (tcp.c:3-52), with the given status (e.g. ESTABLISHED, as after a
+ * handshake); the counterpart of nstack_tcb_add, for tests that need many
+ * connections without running their handshakes through both stacks */
+int oracle_tcb_add(oracle_stack *st, uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport,
+                   int status) {
+    o_tcb *n = (o_tcb *)calloc(1, sizeof(*n));
+    if (!n) return -1;
+    n->sip = sip;
+    n->dip = dip;
+    n->sport = sport;
+    n->dport = dport;
+    n->protocol = 6;
+    n->fd = -1;
+    n->status = status;
+    n->next = st->tcbs; /* LL_ADD */
+    st->tcbs = n;
+    return 0;
+}
+
 /* number of tcbs in the list (control blocks the stack holds) */
 uint32_t oracle_tcb_count(const oracle_stack *st) {
     uint32_t n = 0;

@@ -61,7 +61,10 @@ def udp_frame(src: str, sport: int, dst: str, dport: int, payload: bytes, *, cor
 
 def tcp_frame(src: str, sport: int, dst: str, dport: int, payload: bytes, *, flags=0x18,
               seq=1000, ack=2000, corrupt=False, data_off=0x50, tl=None,
-              pad_options=True) -> bytes:
+              pad_options=True, tl_cksum=False) -> bytes:
+    """tl_cksum: with an explicit tl, the checksum the reference computes for
+    it (over tl - 20 bytes from ip + 20, rte_ip.h:333), so the segment passes
+    tcp_process's check (tcp.c:349-357) whatever tl says"""
     tcp = bytearray(struct.pack(">HHIIBBHHH", sport, dport, seq, ack, data_off, flags, 14600, 0,
                                 0))
     hl = (data_off >> 4) * 4
@@ -69,7 +72,11 @@ def tcp_frame(src: str, sport: int, dst: str, dport: int, payload: bytes, *, fla
         tcp += bytes(hl - 20)
     tcp += payload
     ip = ipv4_header(src, dst, 6, len(tcp), tl=tl)
-    c = l4_cksum(ip, bytes(tcp), 6)
+    if tl is not None and tl_cksum:
+        n = max(tl - 20, 0)
+        c = l4_cksum(ip, bytes(tcp[:n]) + bytes(max(n - len(tcp), 0)), 6) if tl >= 20 else 0
+    else:
+        c = l4_cksum(ip, bytes(tcp), 6)
     tcp[16:18] = struct.pack("<H", c)
     if corrupt:
         tcp[-1] ^= 0x01

@@ -138,6 +138,7 @@ def _stack_sigs(l):
             ("oracle_tcb_state", C.c_int, [vp, u32, u32, u16, u16, vp, vp, vp, vp]),
             ("oracle_tcb_sndq", C.c_int, [vp, u32, u32, u16, u16, u32, vp, vp]),
             ("oracle_tcb_count", u32, [vp]),
+            ("oracle_tcb_add", C.c_int, [vp, u32, u32, u16, u16, C.c_int]),
             ("oracle_rx_burst", None, [vp, vp, vp, vp, u32, u32, vp]),
             ("oracle_drain_all", lng, [vp, vp, sz, vp])]:
         f = getattr(l, name)
@@ -214,6 +215,10 @@ class Stack:
 
     def tcb_count(self):
         return lib.oracle_tcb_count(self.h)
+
+    def tcb_add(self, sip, dip, sport, dport, status):
+        """test hook: install a tcb (raw network-order key) as a SYN would"""
+        return lib.oracle_tcb_add(self.h, sip, dip, sport, dport, status)
 
     def rx_burst(self, pkts, off, lens, off_unit_log2, rcs=None):
         """frames through oracle_rx in burst order (one C call)"""

@@ -60,7 +60,7 @@ def _client_script(rng, k, dport):
         elif kind < 0.2:
             seg.append(tcp(p, data_off=0x60))                     # options: 24-B header
         elif kind < 0.25:
-            seg.append(tcp(p, tl=30))                             # tl - 20 < hl: 0-length EOF
+            seg.append(tcp(p, tl=30, tl_cksum=True))              # tl - 20 < hl: 0-length EOF
         elif kind < 0.3:
             seg.append(tcp(flags=0x02))                           # SYN while established
         else:

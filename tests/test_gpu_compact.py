@@ -140,3 +140,160 @@ def test_socket_layer_batches_match_oracle(torch_dev):
                 assert (r1, d1) == (r2, d2)
     finally:
         ns.fini()
+
+
+# ---- TCP: the per-connection segment sort + payload gather (K4) -----------
+def _seg_model(buf, off, lens, v, nt):
+    """numpy/Python model of rxg_tcp_compact_dev over the oracle's verdicts:
+    rc-0 TCP segments with a tcb id < nt, stable-sorted by id; header fields
+    with bytes past the capture read as 0; PSH segments with plen > 0 keep
+    min(plen, cap - 34 - 4*hl) payload bytes at 16-B aligned offsets in
+    sorted order"""
+    elig = np.nonzero((v["cls"] == R.CLS_TCP) & (v["rc"] == 0) & (v["flow_id"] < nt))[0]
+    order = elig[np.argsort(v["flow_id"][elig], kind="stable")]
+    recs, payload, pos = [], bytearray(), 0
+    for i in order:
+        o, cap = int(off[i]) << 6, int(lens[i])
+
+        def b(k):
+            return int(buf[o + k]) if k < cap else 0
+        hl, fl = b(46) >> 4, b(47)
+        plen = ((b(16) << 8) | b(17)) - 20 - 4 * hl
+        src = 34 + 4 * hl
+        keep = min(plen, max(cap - src, 0)) if (fl & 0x08 and plen > 0) else 0
+        recs.append((int(i), int(v["flow_id"][i]),
+                     (b(38) << 24) | (b(39) << 16) | (b(40) << 8) | b(41),
+                     (b(42) << 24) | (b(43) << 16) | (b(44) << 8) | b(45),
+                     plen, pos, b(34) | (b(35) << 8), b(36) | (b(37) << 8), keep, fl, hl))
+        data = bytes(buf[o + src:o + src + keep])
+        pad = (keep + 15) // 16 * 16
+        payload += data + bytes(pad - keep)
+        pos += pad
+    out = np.zeros(len(recs), R.SEGMENT_DTYPE)
+    for k, r in enumerate(recs):
+        out[k] = r
+    return out, bytes(payload)
+
+
+def _tcp_burst(rng, n, keys, lis_port=9999):
+    """TCP segments over the connections `keys` ((client ip, port) -> :9999):
+    PSH data of assorted sizes, pure ACKs, FIN, PSH|FIN, 24-B headers, a
+    total_length shorter than the header (negative plen), bad checksums, SYNs
+    to the listener, 5% captures cut inside the segment, some UDP between"""
+    frames, caps = [], []
+    for k in range(n):
+        cip, cport = keys[int(rng.integers(len(keys)))]
+        r = rng.random()
+        p = bytes(rng.integers(0, 256, int(rng.choice([0, 1, 7, 100, 555, 1446])), dtype=np.uint8))
+        kw = dict(seq=int(rng.integers(0, 2 ** 32)), ack=int(rng.integers(0, 2 ** 32)))
+        if r < 0.5:
+            f = F.tcp_frame(cip, cport, L, lis_port, p, flags=0x18, **kw)
+        elif r < 0.6:
+            f = F.tcp_frame(cip, cport, L, lis_port, b"", flags=0x10, **kw)
+        elif r < 0.65:
+            f = F.tcp_frame(cip, cport, L, lis_port, b"", flags=0x11, **kw)
+        elif r < 0.7:
+            f = F.tcp_frame(cip, cport, L, lis_port, p, flags=0x19, **kw)  # PSH|FIN|ACK
+        elif r < 0.75:
+            f = F.tcp_frame(cip, cport, L, lis_port, p, flags=0x18, data_off=0x60, **kw)
+        elif r < 0.8:
+            f = F.tcp_frame(cip, cport, L, lis_port, p, flags=0x18, tl=30, tl_cksum=True,
+                            **kw)  # plen < 0 (the checksum of 10 L4 bytes: rc 0)
+        elif r < 0.85:
+            f = F.tcp_frame(cip, cport, L, lis_port, p, flags=0x18, corrupt=len(p) > 0, **kw)
+        elif r < 0.9:
+            f = F.tcp_frame("10.200.0.1", 50000 + k, L, lis_port, b"", flags=0x02, **kw)  # SYN
+        elif r < 0.95:
+            f = F.udp_frame("10.1.1.1", 5000, L, 8889, p)
+        else:
+            f = F.tcp_frame(cip, cport, L, 7, p, flags=0x18, **kw)  # no tcb, no listener
+        frames.append(f)
+        caps.append(len(f) if rng.random() > 0.05 else int(rng.integers(20, len(f) + 1)))
+    return frames, caps
+
+
+@pytest.mark.parametrize("ntcb,passes", [(3000, 2), (300000, 3), (100, 1)])
+def test_tcp_segment_sort_matches_model(torch_dev, ntcb, passes):
+    """every record and every payload byte of K4 against the model, at id
+    spaces that take 1, 2 and 3 radix passes; tcbs with consecutive ids get
+    the traffic so that flows interleave in the burst"""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(ntcb)
+    tcb = np.zeros(ntcb + 1, R.TCB_DTYPE)
+    tcb[0] = (0, R.ip_raw(L), 0, R.port_raw(9999), R.TCP_STATUS_LISTEN)
+    keys = []
+    for k in range(1, ntcb + 1):
+        cip, cport = f"10.{(k >> 16) & 255}.{(k >> 8) & 255}.{k & 255}", 1024 + k % 60000
+        tcb[k] = (R.ip_raw(cip), R.ip_raw(L), R.port_raw(cport), R.port_raw(9999), 4)
+        keys.append((cip, cport))
+    hot = keys[:50] + keys[-50:] + [keys[int(x)] for x in rng.integers(0, ntcb, 200)]
+    frames, caps = _tcp_burst(rng, 5000, hot)
+    buf, off, lens = F.pack_frames(frames, 6, caplens=caps)
+    n = len(frames)
+    want_v = O.Tables(np.zeros(0, R.UDP_SOCK_DTYPE), tcb).classify(buf, off, lens, 6)
+    want_seg, want_pl = _seg_model(buf, off, lens, want_v, ntcb + 1)
+    assert len(want_seg) > 2000
+    with R.Context(0) as ctx:
+        ctx.flows_sync(None, tcb)
+        d_pk = torch.from_numpy(np.concatenate([buf, np.zeros(64, np.uint8)])).to(dev)
+        d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+        d_ln = torch.from_numpy(lens.view(np.int16)).to(dev)
+        d_v = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        ctx.classify_dev(d_pk, d_off, d_ln, n, 6, 1500, d_v, None, stream=sh)
+        d_seg = torch.full((n * 32,), 0xEE, dtype=torch.uint8, device=dev)
+        cap = len(buf) + 4096
+        d_pl = torch.full((cap,), 0xCD, dtype=torch.uint8, device=dev)
+        d_tot = torch.empty(3, dtype=torch.int32, device=dev)
+        ctx.tcp_compact_dev(d_pk, d_off, d_ln, n, 6, d_v, d_seg, d_pl, cap, d_tot, stream=sh)
+        torch.cuda.synchronize(dev)
+        v = d_v.cpu().numpy().view(R.VERDICT_DTYPE)
+        tot = d_tot.cpu().numpy().view(np.uint32)
+        seg = d_seg.cpu().numpy().view(R.SEGMENT_DTYPE)[:tot[0]]
+        pl = d_pl.cpu().numpy()
+    assert v.tobytes() == want_v.tobytes()
+    assert tot[2] == 0 and tot[0] == len(want_seg) and tot[1] == len(want_pl)
+    bad = [k for k in range(len(seg)) if seg[k].tobytes() != want_seg[k].tobytes()]
+    assert not bad, [(k, seg[k], want_seg[k]) for k in bad[:5]]
+    assert pl[:len(want_pl)].tobytes() == want_pl
+    assert np.all(pl[len(want_pl):] == 0xCD)  # nothing written past the used bytes
+    assert any(s["plen"] < 0 for s in want_seg) and any((s["flags"] & 0x09) == 0x09
+                                                         for s in want_seg)
+
+
+def test_tcp_segment_sort_edge_bursts(torch_dev):
+    """an empty burst, a burst without TCP, one connection taking every
+    segment (one long run), and an id space of one listener"""
+    torch, dev = torch_dev
+    tcb = np.zeros(2, R.TCB_DTYPE)
+    tcb[0] = (0, R.ip_raw(L), 0, R.port_raw(9999), R.TCP_STATUS_LISTEN)
+    tcb[1] = (R.ip_raw("10.0.0.1"), R.ip_raw(L), R.port_raw(4000), R.port_raw(9999), 4)
+    rng = np.random.default_rng(9)
+    cases = [[], [F.udp_frame("10.1.1.1", 5000, L, 8889, b"x" * 30)] * 5,
+             [F.tcp_frame("10.0.0.1", 4000, L, 9999,
+                          bytes(rng.integers(0, 256, int(rng.integers(0, 1400)), dtype=np.uint8)),
+                          seq=k) for k in range(3000)]]
+    with R.Context(0) as ctx:
+        ctx.flows_sync(None, tcb)
+        for frames in cases:
+            n = len(frames)
+            buf, off, lens = F.pack_frames(frames or [b"\0" * 64], 6)
+            want_v = O.Tables(np.zeros(0, R.UDP_SOCK_DTYPE), tcb).classify(buf, off[:n], lens[:n], 6)
+            want_seg, want_pl = _seg_model(buf, off, lens, want_v, 2)
+            d_pk = torch.from_numpy(np.concatenate([buf, np.zeros(64, np.uint8)])).to(dev)
+            d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+            d_ln = torch.from_numpy(lens.view(np.int16)).to(dev)
+            d_v = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=dev)
+            sh = torch.cuda.current_stream(dev).cuda_stream
+            ctx.classify_dev(d_pk, d_off, d_ln, n, 6, 1500, d_v, None, stream=sh)
+            d_seg = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=dev)
+            cap = len(buf) + 4096
+            d_pl = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            d_tot = torch.full((3,), 7, dtype=torch.int32, device=dev)
+            ctx.tcp_compact_dev(d_pk, d_off, d_ln, n, 6, d_v, d_seg, d_pl, cap, d_tot, stream=sh)
+            torch.cuda.synchronize(dev)
+            tot = d_tot.cpu().numpy().view(np.uint32)
+            assert tot[0] == len(want_seg) and tot[1] == len(want_pl) and tot[2] == 0
+            seg = d_seg.cpu().numpy().view(R.SEGMENT_DTYPE)[:tot[0]]
+            assert seg.tobytes() == want_seg.tobytes()
+            assert d_pl.cpu().numpy()[:len(want_pl)].tobytes() == want_pl
