@@ -885,6 +885,14 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             res["established"] = int(ns.tcb_count()) - 1
         pk, off, ln = R.gen_host(cfg, 0, B, ul)
         arr, keep = R.NStack.mbufs_over(pk, off, ln, ul)
+        # the frames' memory registered with the stack, as a DPDK application
+        # registers its mbuf pool once (rte_mempool_mem_iter): the GPU pulls
+        # each burst's frames over PCIe instead of a host gather + copy
+        try:
+            ns.register_host(pk.ctypes.data, pk.nbytes)
+            res["pool_registered"] = True
+        except R.RxgError as e:  # reported, and the host gather carries the bursts
+            res["pool_registered"] = repr(e)
         rbuf = np.zeros(65536, np.uint8)
         ns.rx_burst_mbufs(arr, B)  # warm (staging, tables committed)
         ns.drain_all(rbuf)

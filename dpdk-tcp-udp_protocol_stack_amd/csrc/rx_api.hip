@@ -48,6 +48,8 @@ hipError_t rx_gather_launch(const uint8_t *pkts, const uint32_t *off, const uint
                             hipStream_t s);
 int rx_group_allreduce_u64(rxg_group *g, void *d, uint32_t n, hipStream_t s);
 size_t rx_segsort_ws_bytes(uint32_t n);
+hipError_t rx_ingest_launch(const unsigned long long *src, const uint32_t *off, const uint16_t *len,
+                            uint32_t n, uint8_t *dst, hipStream_t s);
 hipError_t rx_segsort_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                              uint32_t n, uint32_t unit_log2, const uint4 *verd, uint32_t nt,
                              rxg_segment *seg, uint8_t *payload, uint64_t cap, uint32_t *totals,
@@ -227,6 +229,7 @@ struct rxg_ctx {
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     struct slot {
         uint8_t *h_stage = nullptr; // pinned, mbuf gather
+        unsigned long long *h_src = nullptr, *d_src = nullptr; // device-pulled frames (registered)
         uint32_t *h_off = nullptr;
         uint16_t *h_len = nullptr;
         uint8_t *d_pkts = nullptr;
@@ -256,6 +259,15 @@ struct rxg_ctx {
     size_t d_ss_ws_cap = 0;
     // phase timing of rxg_process_mbufs_deliver (timing-enabled events)
     hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    // registered host memory (rxg_register_host): frames of an mbuf burst that
+    // all lie in it are pulled by the device instead of gathered on the host
+    struct host_region {
+        uint8_t *h = nullptr, *d = nullptr;
+        uint64_t bytes = 0;
+        bool ours = false; // registered here (unregistered at close)
+    };
+    std::vector<host_region> regions;
+    uint32_t region_hint = 0;
 };
 
 // a flow-table array of at least `bytes`, stream-ordered on s (hipMallocAsync /
@@ -726,10 +738,14 @@ void rxg_close(rxg_ctx *c) {
         if (sl.h_stage) (void)hipHostFree(sl.h_stage);
         if (sl.h_off) (void)hipHostFree(sl.h_off);
         if (sl.h_len) (void)hipHostFree(sl.h_len);
+        if (sl.h_src) (void)hipHostFree(sl.h_src);
+        (void)hipFree(sl.d_src);
         if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
         if (sl.ev_k) (void)hipEventDestroy(sl.ev_k);
         if (sl.ev_done) (void)hipEventDestroy(sl.ev_done);
     }
+    for (const rxg_ctx::host_region &r : c->regions)
+        if (r.ours) (void)hipHostUnregister(r.h);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
@@ -999,6 +1015,46 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
     return RXG_OK;
 }
 
+int rxg_register_host(rxg_ctx *c, void *base, uint64_t bytes) {
+    if (!c || !base || !bytes) return RXG_EINVAL;
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    DEVGUARD(c);
+    rxg_ctx::host_region r;
+    r.h = static_cast<uint8_t *>(base);
+    r.bytes = bytes;
+    hipError_t e = hipHostRegister(base, bytes, hipHostRegisterMapped);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+        (void)hipGetLastError();
+    } else {
+        HIPCHK(e);
+        r.ours = true;
+    }
+    void *d = nullptr;
+    e = hipHostGetDevicePointer(&d, base, 0);
+    if (e != hipSuccess) {
+        if (r.ours) (void)hipHostUnregister(base);
+        return rx_set_hip_error(e);
+    }
+    r.d = static_cast<uint8_t *>(d);
+    c->regions.push_back(r);
+    return RXG_OK;
+}
+
+int rxg_unregister_host(rxg_ctx *c, void *base) {
+    if (!c || !base) return RXG_EINVAL;
+    for (size_t k = 0; k < c->regions.size(); ++k)
+        if (c->regions[k].h == base) {
+            DEVGUARD(c);
+            int rc = bursts_drain(c); // no burst may still be pulling from it
+            if (rc) return rc;
+            if (c->regions[k].ours) HIPCHK(hipHostUnregister(base));
+            c->regions.erase(c->regions.begin() + (long)k);
+            c->region_hint = 0;
+            return RXG_OK;
+        }
+    return RXG_EINVAL;
+}
+
 int rxg_kernel_variant(const rxg_ctx *c, uint32_t len_hint, uint32_t variant[4], char *name,
                        uint32_t name_cap) {
     if (!c) return RXG_EINVAL;
@@ -1262,12 +1318,17 @@ static hipError_t copy_in_frames(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *p
 // kernel until the slot's previous verdicts have left d_out.
 static int submit_slot(rxg_ctx *c, rxg_ctx::slot &sl, const uint8_t *pkts, uint64_t span,
                        const uint32_t *off, const uint16_t *len, uint32_t n,
-                       uint32_t off_unit_log2, rxg_verdict *out, uint64_t ticket) {
+                       uint32_t off_unit_log2, rxg_verdict *out, uint64_t ticket,
+                       bool pulled = false) {
     const bool reused = sl.ticket != 0;
     if (reused) HIPCHK(hipStreamWaitEvent(c->s_h2d, sl.ev_k, 0));
-    HIPCHK(copy_in_frames(c, sl, pkts, span));
+    if (!pulled) HIPCHK(copy_in_frames(c, sl, pkts, span));
     HIPCHK(hipMemcpyAsync(sl.d_off, off, n * 4ull, hipMemcpyHostToDevice, c->s_h2d));
     HIPCHK(hipMemcpyAsync(sl.d_len, len, n * 2ull, hipMemcpyHostToDevice, c->s_h2d));
+    if (pulled) { // registered host frames: the device pulls them into the slot
+        HIPCHK(hipMemcpyAsync(sl.d_src, sl.h_src, n * 8ull, hipMemcpyHostToDevice, c->s_h2d));
+        HIPCHK(rx_ingest_launch(sl.d_src, sl.d_off, sl.d_len, n, sl.d_pkts, c->s_h2d));
+    }
     HIPCHK(hipEventRecord(sl.ev_in, c->s_h2d));
     HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_in, 0));
     if (reused) HIPCHK(hipStreamWaitEvent(c->stream, sl.ev_done, 0));
@@ -1348,8 +1409,57 @@ int rxg_classify(rxg_ctx *c, const uint8_t *pkts, const uint32_t *off, const uin
 
 // frames of an mbuf burst into slot sl's pinned staging at 64-B aligned
 // places (buf_addr + data_off, data_len bytes); *span = bytes used
+// the device address of [p, p + bytes) when it lies in a registered region
+static uint8_t *region_dev(rxg_ctx *c, const uint8_t *p, uint64_t bytes) {
+    const uint32_t nr = (uint32_t)c->regions.size();
+    for (uint32_t k = 0; k < nr; ++k) {
+        const uint32_t j = (c->region_hint + k) % nr;
+        const rxg_ctx::host_region &r = c->regions[j];
+        if (p >= r.h && p + bytes <= r.h + r.bytes) {
+            c->region_hint = j;
+            return r.d + (p - r.h);
+        }
+    }
+    return nullptr;
+}
+
+// an mbuf burst whose frames all lie in registered host memory, 16-B aligned:
+// descriptors and device source addresses only (the device pulls the frames,
+// rx_ingest_launch); false (nothing done) otherwise
+static int pull_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n, uint64_t *span,
+                      bool *pulled) {
+    *pulled = false;
+    if (c->regions.empty()) return RXG_OK;
+    if (!sl.h_src) {
+        HIPCHK(hipMalloc(&sl.d_src, (size_t)c->max_pkts * 8));
+        HIPCHK(hipHostMalloc((void **)&sl.h_src, (size_t)c->max_pkts * 8, 0));
+    }
+    if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_src
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
+        const uint8_t *f = (const uint8_t *)m[i]->buf_addr + m[i]->data_off;
+        const uint32_t l = m[i]->data_len;
+        uint8_t *d = ((uintptr_t)f & 15u) ? nullptr : region_dev(c, f, (l + 15ull) & ~15ull);
+        if (!d) return RXG_OK; // (the host gather takes the burst)
+        const uint64_t step = std::max<uint64_t>((l + 63ull) & ~63ull, 64);
+        if (pos + step > c->max_bytes) return RXG_ERANGE;
+        sl.h_src[i] = (unsigned long long)(uintptr_t)d;
+        sl.h_off[i] = (uint32_t)(pos >> 6);
+        sl.h_len[i] = (uint16_t)l;
+        pos += step;
+    }
+    *span = pos;
+    *pulled = true;
+    return RXG_OK;
+}
+
 static int gather_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n,
-                        uint64_t *span) {
+                        uint64_t *span, bool *pulled = nullptr) {
+    if (pulled) {
+        int rc = pull_mbufs(c, sl, m, n, span, pulled);
+        if (rc || *pulled) return rc;
+    }
     if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_stage
     uint64_t pos = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -1377,9 +1487,10 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
     uint64_t pos = 0;
-    int rc = gather_mbufs(c, sl, m, n, &pos);
+    bool pulled = false;
+    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
     if (rc) return rc;
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
     return rc ? rc : rxg_wait(c, t);
 }
 
@@ -1452,9 +1563,10 @@ int rxg_process_mbufs_udp(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdic
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
     uint64_t pos = 0;
-    int rc = gather_mbufs(c, sl, m, n, &pos);
+    bool pulled = false;
+    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
     if (rc) return rc;
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
     if (rc) return rc;
     // the compaction follows the classify on the context's stream (its inputs:
     // the staged frames and the device verdicts of this slot)
@@ -1565,11 +1677,12 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
     uint64_t pos = 0;
-    int rc = gather_mbufs(c, sl, m, n, &pos);
+    bool pulled = false;
+    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
     if (rc) return rc;
     const double t1 = now_ms();
     HIPCHK(hipEventRecord(c->tev[0], c->s_h2d));
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t);
+    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->tev[1], c->s_h2d)); // after the copy in
     HIPCHK(hipEventRecord(c->tev[2], c->stream)); // after K1

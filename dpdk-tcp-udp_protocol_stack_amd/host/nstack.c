@@ -1276,6 +1276,11 @@ static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, i
     return delivered;
 }
 
+static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8_t *payload,
+                               rxg_mbuf *const *m, uint8_t *handled, int *rc_out);
+static uint32_t host_segments(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v,
+                              rxg_segment *sg);
+
 int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
                    int *rc_out) {
     if (!m || !v) return n ? RXG_EINVAL : 0;
@@ -1285,7 +1290,18 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
     if (rc == RXG_OK) {
         g_burst_stale = gen != g_snap_gen; /* classified against other lists */
         g_burst_mutated = 0;
-        delivered = deliver_burst(m, n, v, rc_out, NULL);
+        const uint8_t *done = NULL;
+        if (!g_burst_stale && n) { /* the verdicts' flow ids name the live blocks */
+            rxg_segment *sg = malloc((size_t)n * sizeof(*sg));
+            if (!grow((void **)&s_handled, &s_handled_cap, n, 1) && sg) {
+                memset(s_handled, 0, n);
+                const uint32_t k = host_segments(m, n, v, sg);
+                deliver_tcp_sorted(sg, k, NULL, m, s_handled, rc_out);
+                done = s_handled;
+            }
+            free(sg);
+        }
+        delivered = deliver_burst(m, n, v, rc_out, done);
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
@@ -1370,7 +1386,8 @@ static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const ui
  * allocation, payloads copied from the gathered buffer.  Returns 0, or 1 when
  * the tcb's state needs the frame-by-frame path (LISTEN, SYN_RCVD, LAST_ACK). */
 static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_t k,
-                            const uint8_t *payload, uint8_t *handled, int *rc_out) {
+                            const uint8_t *payload, rxg_mbuf *const *m, uint8_t *handled,
+                            int *rc_out) {
     if (s->status == TCP_STATUS_LISTEN || s->status == TCP_STATUS_SYN_RCVD ||
         s->status == TCP_STATUS_LAST_ACK)
         return 1;
@@ -1430,7 +1447,10 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
                 if ((PLEN) > 0) {                                                            \
                     fr->data = pp;                                                           \
                     fr->length = (uint32_t)(PLEN);                                           \
-                    memcpy(pp, payload + (SEG)->offset, (SEG)->ncopy);                       \
+                    memcpy(pp, payload ? payload + (SEG)->offset                             \
+                                       : (const uint8_t *)m[(SEG)->frame]->buf_addr +        \
+                                             m[(SEG)->frame]->data_off + 34u + 4u * (SEG)->hl, \
+                           (SEG)->ncopy);                                                    \
                     if ((uint32_t)(PLEN) > (SEG)->ncopy)                                     \
                         memset(pp + (SEG)->ncopy, 0, (uint32_t)(PLEN) - (SEG)->ncopy);       \
                     pp += (uint32_t)(PLEN);                                                  \
@@ -1497,14 +1517,51 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
 
 /* the sorted segments, connection by connection (g_lock held); frames of
  * connections that need the frame-by-frame path are left unmarked */
-static void deliver_tcp_sorted(const rxg_delivery *d, uint8_t *handled, int *rc_out) {
-    const rxg_segment *sg = d->seg;
-    for (uint32_t a = 0, b; a < d->nseg; a = b) {
+static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8_t *payload,
+                               rxg_mbuf *const *m, uint8_t *handled, int *rc_out) {
+    for (uint32_t a = 0, b; a < nseg; a = b) {
         b = a + 1;
-        while (b < d->nseg && sg[b].flow == sg[a].flow) b++;
+        while (b < nseg && sg[b].flow == sg[a].flow) b++;
         struct tcp_stream *s = sg[a].flow < s_tcb_cap ? s_tcb_cb[sg[a].flow] : NULL;
-        if (s) deliver_tcp_conn(s, sg + a, b - a, d->tcp_payload, handled, rc_out);
+        if (s) deliver_tcp_conn(s, sg + a, b - a, payload, m, handled, rc_out);
     }
+}
+
+/* The segment records of a burst whose verdicts came from elsewhere
+ * (nstack_deliver): the same fields the GPU's segment sort decodes (rc-0 TCP
+ * verdicts naming a live tcb id, bytes past the capture read as 0), stably
+ * sorted by tcb id on the host; payloads are then copied from the frames */
+static int seg_cmp(const void *a, const void *b) {
+    const rxg_segment *x = a, *y = b;
+    if (x->flow != y->flow) return x->flow < y->flow ? -1 : 1;
+    return x->frame < y->frame ? -1 : (x->frame > y->frame);
+}
+static uint32_t host_segments(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v,
+                              rxg_segment *sg) {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (v[i].cls != RXG_CLS_TCP || v[i].rc != RXG_RC_OK || v[i].flow_id >= s_tcb_cap) continue;
+        const uint8_t *f = (const uint8_t *)m[i]->buf_addr + m[i]->data_off;
+        const uint32_t cap = m[i]->data_len;
+#define B8(j) ((uint32_t)((j) < cap ? f[(j)] : 0u))
+        rxg_segment *g = &sg[k++];
+        memset(g, 0, sizeof(*g));
+        g->frame = i;
+        g->flow = v[i].flow_id;
+        g->seq = B8(38) << 24 | B8(39) << 16 | B8(40) << 8 | B8(41);
+        g->ack = B8(42) << 24 | B8(43) << 16 | B8(44) << 8 | B8(45);
+        g->hl = (uint8_t)(B8(46) >> 4);
+        g->flags = (uint8_t)B8(47);
+        g->plen = (int32_t)(B8(16) << 8 | B8(17)) - 20 - 4 * (int32_t)g->hl;
+        g->sport = (uint16_t)(B8(34) | B8(35) << 8);
+        g->dport = (uint16_t)(B8(36) | B8(37) << 8);
+#undef B8
+        const uint32_t from = 34u + 4u * g->hl, avail = cap > from ? cap - from : 0u;
+        if ((g->flags & TCP_PSH) && g->plen > 0)
+            g->ncopy = (uint16_t)((uint32_t)g->plen < avail ? (uint32_t)g->plen : avail);
+    }
+    qsort(sg, k, sizeof(*sg), seg_cmp);
+    return k;
 }
 
 /* the last nstack_rx_burst's phases (nstack_last_burst_phases) */
@@ -1543,7 +1600,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         }
         const double t2 = mono_ms();
         memset(s_handled, 0, n);
-        if (d.nseg) deliver_tcp_sorted(&d, s_handled, rc_out);
+        if (d.nseg) deliver_tcp_sorted(d.seg, d.nseg, d.tcp_payload, m, s_handled, rc_out);
         const double t3 = mono_ms();
         delivered += deliver_burst(m, n, s_v, rc_out, s_handled);
         g_udp_done = 0;
@@ -1688,6 +1745,13 @@ int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t
 }
 
 rxg_ctx *nstack_ctx(void) { return g_ctx; }
+
+int nstack_register_host(void *base, uint64_t bytes) {
+    pthread_mutex_lock(&g_lock);
+    const int rc = g_ctx ? rxg_register_host(g_ctx, base, bytes) : RXG_EINVAL;
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
 
 uint32_t nstack_lookup_udp(uint32_t dip, uint16_t dport) {
     pthread_mutex_lock(&g_lock);

@@ -164,6 +164,8 @@ _flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
 _tcp_compact_dev = _sig("rxg_tcp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp,
                         _u64, _vp, _vp)
 _process_mbufs_deliver = _sig("rxg_process_mbufs_deliver", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
+_register_host = _sig("rxg_register_host", _i32, _vp, _vp, _u64)
+_unregister_host = _sig("rxg_unregister_host", _i32, _vp, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
                         _vp, _vp)
@@ -222,6 +224,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp", "rxg_tcp_compact_dev", "rxg_process_mbufs_deliver",
+            "rxg_register_host", "rxg_unregister_host",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",
@@ -458,10 +461,20 @@ class Context:
                                 p(d_seg), p(d_payload), payload_cap, p(d_totals), stream),
                "rxg_tcp_compact_dev")
 
+    def register_host(self, ptr: int, nbytes: int):
+        """rxg_register_host: frames in [ptr, ptr + nbytes) are pulled by the
+        device (keep the memory alive until unregister_host / close)"""
+        _check(_register_host(self._h, ptr, nbytes), "rxg_register_host")
+
+    def unregister_host(self, ptr: int):
+        _check(_unregister_host(self._h, ptr), "rxg_unregister_host")
+
     def process_mbufs_deliver(self, mbufs):
         """rxg_process_mbufs_deliver over Mbuf structures: (verdicts, dgrams,
         first, udp payload, segments, tcp payload, phase ms) as numpy copies"""
-        arr = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])
+        if not isinstance(mbufs, C.Array):
+            mbufs = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])
+        arr = mbufs
         out = np.zeros(len(mbufs), VERDICT_DTYPE)
         d = Delivery()
         ms = (C.c_float * 8)()
@@ -723,6 +736,7 @@ class NStack:
                    ("nstack_lookup_udp", _u32, [_u32, _u16]),
                    ("nstack_lookup_tcp", _u32, [_u32, _u32, _u16, _u16]),
                    ("nstack_ctx", _vp, []),
+                   ("nstack_register_host", _i32, [_vp, _u64]),
                    ("nstack_stat", _u64, [_i32]),
                    ("nstack_set_local", _i32, [_u32, _vp]),
                    ("nstack_arp_insert", _i32, [_u32, _vp]),
@@ -807,6 +821,10 @@ class NStack:
     def lookup_tcp(self, sip: int, dip: int, sport: int, dport: int) -> int:
         """the flow id the library's tables give a TCP 4-tuple (raw), listener included"""
         return self.lib.nstack_lookup_tcp(sip, dip, sport, dport)
+
+    def register_host(self, ptr: int, nbytes: int):
+        """nstack_register_host: frames in this memory are pulled by the GPU"""
+        _check(self.lib.nstack_register_host(ptr, nbytes), "nstack_register_host")
 
     def ft_dump(self, which: int, device: bool):
         """diagnostics: (table, info) of the socket layer's context (rxg_ft_dump)"""

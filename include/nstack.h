@@ -110,6 +110,10 @@ int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t
  * of what the device probes) give a key — UDP (dst ip, dst port), TCP (the
  * exact 4-tuple, else the listener on dport); RXG_FLOW_NONE if none. */
 uint32_t nstack_lookup_udp(uint32_t dip, uint16_t dport);
+/* The mbuf pool's memory (rxg_register_host on the stack's context): bursts
+ * whose frames lie in it are pulled by the GPU instead of gathered on the
+ * host (DPDK: once per memory chunk of the pool, rte_mempool_mem_iter). */
+int nstack_register_host(void *base, uint64_t bytes);
 /* the library context the socket layer classifies with (diagnostics) */
 rxg_ctx *nstack_ctx(void);
 uint32_t nstack_lookup_tcp(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport);

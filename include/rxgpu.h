@@ -282,6 +282,19 @@ int rxg_classify_span(rxg_ctx *ctx, const uint8_t *pkts, uint64_t span_bytes, co
  * netfamily.c:147.  Frames are gathered into the context's staging buffer. */
 int rxg_process_mbufs(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out);
 
+/* Register host memory that holds frames — the mbuf pool's memory, as DPDK
+ * hands it out (rte_mempool_mem_iter) — with the context: it is pinned and
+ * mapped for the device once, and from then on an mbuf burst
+ * (rxg_process_mbufs*) whose frames all lie in registered memory, 16-B
+ * aligned with their 16-B rounded ends inside it, is pulled by the device
+ * straight from that memory over PCIe (the DMA a NIC does into its ring)
+ * instead of being gathered into pinned staging by a host memcpy and copied.
+ * Other bursts take the host gather as before.  Memory registered elsewhere
+ * already is accepted (and left registered at close).  Unregister waits for
+ * this context's bursts. */
+int rxg_register_host(rxg_ctx *ctx, void *base, uint64_t bytes);
+int rxg_unregister_host(rxg_ctx *ctx, void *base);
+
 /* Pipelined host-buffer bursts (PCIe-inclusive, overlapped).  The context owns
  * RXG_PIPE_DEPTH staging slots (each sized by rxg_open's max_pkts/max_bytes);
  * burst t copies in while burst t-1 is classified and burst t-2's verdicts

@@ -63,6 +63,8 @@ def _client_script(rng, k, dport):
             seg.append(tcp(p, tl=30, tl_cksum=True))              # tl - 20 < hl: 0-length EOF
         elif kind < 0.3:
             seg.append(tcp(flags=0x02))                           # SYN while established
+        elif kind < 0.35:
+            seg.append(tcp(p, flags=0x19))                        # PSH|FIN|ACK in one segment
         else:
             seg.append(tcp(p))                                    # PSH|ACK data
         seq += n
@@ -261,7 +263,7 @@ def ns_host():
     s.fini()
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_delivery_matches_oracle(ns_host, seed):
     _run(ns_host, "cpu", seed)
 

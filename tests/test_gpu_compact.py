@@ -297,3 +297,51 @@ def test_tcp_segment_sort_edge_bursts(torch_dev):
             seg = d_seg.cpu().numpy().view(R.SEGMENT_DTYPE)[:tot[0]]
             assert seg.tobytes() == want_seg.tobytes()
             assert d_pl.cpu().numpy()[:len(want_pl)].tobytes() == want_pl
+
+
+def test_registered_pool_is_pulled_by_the_device(torch_dev):
+    """rxg_register_host: a burst whose frames lie in registered memory is
+    pulled by the GPU (no host gather); every output of
+    rxg_process_mbufs_deliver equals the host-gathered burst's and the
+    oracle's verdicts; one frame outside the registered memory sends the burst
+    back to the host gather, with the same results"""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(21)
+    nsock = 300
+    udp = np.zeros(nsock, R.UDP_SOCK_DTYPE)
+    udp["localip"] = R.ip_raw(L)
+    udp["localport"] = [R.port_raw(30000 + k) for k in range(nsock)]
+    udp["protocol"] = 17
+    tcb = np.zeros(401, R.TCB_DTYPE)
+    tcb[0] = (0, R.ip_raw(L), 0, R.port_raw(9999), R.TCP_STATUS_LISTEN)
+    keys = []
+    for k in range(1, 401):
+        cip, cport = f"10.7.{k >> 8}.{k & 255}", 2000 + k
+        tcb[k] = (R.ip_raw(cip), R.ip_raw(L), R.port_raw(cport), R.port_raw(9999), 4)
+        keys.append((cip, cport))
+    uf, ucaps = _burst(rng, 1500, nsock)
+    tf, tcaps = _tcp_burst(rng, 1500, keys)
+    order = rng.permutation(3000)
+    frames = [(uf + tf)[i] for i in order]
+    caps = [(ucaps + tcaps)[i] for i in order]
+    buf, off, lens = F.pack_frames(frames, 6, caplens=caps)
+    buf = np.concatenate([buf, np.zeros(4096, np.uint8)])
+    want_v = O.Tables(udp, tcb).classify(buf, off, lens, 6)
+    arr, keep = R.NStack.mbufs_over(buf, off, lens, 6)
+    with R.Context(0, max_pkts=4096, max_bytes=len(buf) + 65536) as ctx:
+        ctx.flows_sync(udp, tcb)
+        host = ctx.process_mbufs_deliver(arr)
+        ctx.register_host(buf.ctypes.data, buf.nbytes)
+        pulled = ctx.process_mbufs_deliver(arr)
+        # one frame outside the registered memory: the burst is gathered on the host
+        o5 = int(off[5]) << 6
+        extra = np.zeros(2048, np.uint8)
+        extra[:int(lens[5])] = buf[o5:o5 + int(lens[5])]
+        keep[5].buf_addr = extra.ctypes.data
+        mixed = ctx.process_mbufs_deliver(arr)
+        ctx.unregister_host(buf.ctypes.data)
+    assert host[0].tobytes() == want_v.tobytes()
+    for got in (pulled, mixed):
+        for a, b in zip(host[:6], got[:6]):
+            assert (a is None and b is None) or a.tobytes() == b.tobytes()
+    assert len(host[4]) > 500 and host[6][1] >= 0
