@@ -8,6 +8,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -254,6 +255,15 @@ struct rxg_ctx {
     // results and their pinned host copies, sized by max_pkts / max_bytes
     rxg_segment *d_ss_seg = nullptr, *h_ss_seg = nullptr;
     uint8_t *d_ss_payload = nullptr, *h_ss_payload = nullptr;
+    // pinned payload buffers a caller may keep past the next burst
+    // (rxg_payload_hold / _release: the receive fragments of a burst point
+    // into them until the application has read them); refs counts the holds,
+    // the library's own one included (until its next burst call)
+    struct pl_buf {
+        uint8_t *h = nullptr;
+        std::atomic<int> refs{0};
+    } pl[RXG_PAYLOAD_BUFS];
+    int pl_cur = -1; // the buffer of the latest burst (held by the library)
     uint32_t *d_ss_totals = nullptr, *h_ss_totals = nullptr;
     void *d_ss_ws = nullptr;
     size_t d_ss_ws_cap = 0;
@@ -717,6 +727,8 @@ void rxg_close(rxg_ctx *c) {
     if (c->h_ss_seg) (void)hipHostFree(c->h_ss_seg);
     if (c->h_ss_payload) (void)hipHostFree(c->h_ss_payload);
     if (c->h_ss_totals) (void)hipHostFree(c->h_ss_totals);
+    for (rxg_ctx::pl_buf &b : c->pl)
+        if (b.h) (void)hipHostFree(b.h);
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->h_cp_dg) (void)hipHostFree(c->h_cp_dg);
@@ -1607,6 +1619,18 @@ static int segsort_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off
     return RXG_OK;
 }
 
+int rxg_payload_hold(rxg_ctx *c, int32_t ref) {
+    if (!c || ref < 0 || ref >= RXG_PAYLOAD_BUFS) return RXG_EINVAL;
+    c->pl[ref].refs.fetch_add(1, std::memory_order_acq_rel);
+    return RXG_OK;
+}
+
+int rxg_payload_release(rxg_ctx *c, int32_t ref) {
+    if (!c || ref < 0 || ref >= RXG_PAYLOAD_BUFS) return RXG_EINVAL;
+    c->pl[ref].refs.fetch_sub(1, std::memory_order_acq_rel);
+    return RXG_OK;
+}
+
 int rxg_tcp_compact_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off,
                         const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
                         const rxg_verdict *d_v, rxg_segment *d_seg, uint8_t *d_payload,
@@ -1666,7 +1690,24 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
     for (hipEvent_t &e : c->tev)
         if (!e) HIPCHK(hipEventCreate(&e));
     d->seg = c->h_ss_seg;
-    d->tcp_payload = c->h_ss_payload;
+    // the TCP payloads of this burst: a free pooled buffer (a hold the caller
+    // can take, rxg_payload_hold), else the context's own one (valid until the
+    // next call only: tcp_payload_ref = -1)
+    if (c->pl_cur >= 0) c->pl[c->pl_cur].refs.fetch_sub(1, std::memory_order_acq_rel);
+    c->pl_cur = -1;
+    for (int k = 0; k < RXG_PAYLOAD_BUFS && c->pl_cur < 0; ++k) {
+        rxg_ctx::pl_buf &b = c->pl[k];
+        if (b.refs.load(std::memory_order_acquire) != 0) continue;
+        if (!b.h && hipHostMalloc((void **)&b.h, c->max_bytes, 0) != hipSuccess) {
+            b.h = nullptr; // (out of pinned memory: the context's own buffer)
+            (void)hipGetLastError();
+            break;
+        }
+        b.refs.store(1, std::memory_order_release);
+        c->pl_cur = k;
+    }
+    d->tcp_payload_ref = c->pl_cur;
+    d->tcp_payload = c->pl_cur >= 0 ? c->pl[c->pl_cur].h : c->h_ss_payload;
     if (udp) {
         d->dgram = c->h_cp_dg;
         d->first = c->h_cp_first;
@@ -1724,7 +1765,7 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
             HIPCHK(hipMemcpyAsync(c->h_ss_seg, c->d_ss_seg, (size_t)d->nseg * sizeof(rxg_segment),
                                   hipMemcpyDeviceToHost, c->stream));
         if (d->tcp_bytes)
-            HIPCHK(hipMemcpyAsync(c->h_ss_payload, c->d_ss_payload, d->tcp_bytes,
+            HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, d->tcp_bytes,
                                   hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(hipEventRecord(c->tev[4], c->stream)); // after the results' copy out

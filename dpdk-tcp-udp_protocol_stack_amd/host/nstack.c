@@ -179,11 +179,15 @@ struct frag_batch {
     struct tcp_fragment item; /* the ring item (item.batch = this batch) */
     uint32_t n, next;         /* fragments; the next one to read */
     struct tcp_fragment *frag;
+    int32_t pl_ref;           /* >= 0: payloads point into the library's pinned buffer
+                                 pl_ref, held (rxg_payload_hold) until the batch is freed */
 };
 
 /* ---- a tcb's fragment queues: logical fragments over ring items ---------- */
+static rxg_ctx *g_ctx;
 static void frag_item_free(struct tcp_fragment *f) {
     if (f->batch) {
+        if (f->batch->pl_ref >= 0) rxg_payload_release(g_ctx, f->batch->pl_ref);
         free(f->batch); /* (fragments and payloads live in the batch's allocation) */
     } else {
         free(f->data);
@@ -277,7 +281,6 @@ static struct localhost *g_pstHost;
 static struct tcp_stream *g_tcb_set;
 static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
-static rxg_ctx *g_ctx;
 static int g_dirty = 1;       /* the creation-order export (nstack_flows) is stale */
 static uint64_t g_snap_gen; /* bumped whenever a lookup result may change */
 static int g_burst_stale;   /* the burst's verdicts were made for an older snapshot */
@@ -1277,7 +1280,8 @@ static int deliver_burst(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, i
 }
 
 static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8_t *payload,
-                               rxg_mbuf *const *m, uint8_t *handled, int *rc_out);
+                               int32_t pl_ref, rxg_mbuf *const *m, uint8_t *handled,
+                               int *rc_out);
 static uint32_t host_segments(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v,
                               rxg_segment *sg);
 
@@ -1296,7 +1300,7 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
             if (!grow((void **)&s_handled, &s_handled_cap, n, 1) && sg) {
                 memset(s_handled, 0, n);
                 const uint32_t k = host_segments(m, n, v, sg);
-                deliver_tcp_sorted(sg, k, NULL, m, s_handled, rc_out);
+                deliver_tcp_sorted(sg, k, NULL, -1, m, s_handled, rc_out);
                 done = s_handled;
             }
             free(sg);
@@ -1383,11 +1387,14 @@ static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const ui
  * by connection equals the reference's frame-by-frame loop.  The receive
  * fragments the segments queue (ng_tcp_enqueue_recvbuffer, tcp.c:133-185)
  * and the ACKs they send (tcp.c:187-216) go in as one batch item each: one
- * allocation, payloads copied from the gathered buffer.  Returns 0, or 1 when
- * the tcb's state needs the frame-by-frame path (LISTEN, SYN_RCVD, LAST_ACK). */
+ * allocation.  With a held payload buffer (pl_ref >= 0) a fragment whose
+ * payload was captured whole points straight into it (no copy: the batch
+ * holds the buffer until it is freed); otherwise the payload is copied, zero
+ * filled past the capture.  Returns 0, or 1 when the tcb's state needs the
+ * frame-by-frame path (LISTEN, SYN_RCVD, LAST_ACK). */
 static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_t k,
-                            const uint8_t *payload, rxg_mbuf *const *m, uint8_t *handled,
-                            int *rc_out) {
+                            const uint8_t *payload, int32_t pl_ref, rxg_mbuf *const *m,
+                            uint8_t *handled, int *rc_out) {
     if (s->status == TCP_STATUS_LISTEN || s->status == TCP_STATUS_SYN_RCVD ||
         s->status == TCP_STATUS_LAST_ACK)
         return 1;
@@ -1402,7 +1409,8 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
         if (st != TCP_STATUS_ESTABLISHED) continue;
         if (sg[j].flags & TCP_PSH) {
             nfr++, nack++;
-            if (sg[j].plen > 0) pbytes += (uint64_t)sg[j].plen;
+            if (sg[j].plen > 0 && (pl_ref < 0 || sg[j].ncopy != (uint32_t)sg[j].plen))
+                pbytes += (uint64_t)sg[j].plen; /* (copied) */
         }
         if (sg[j].flags & TCP_FIN) nfr++, nack++, st = TCP_STATUS_CLOSE_WAIT;
     }
@@ -1421,6 +1429,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
             rb->n = rtake;
             rb->next = 0;
             rb->frag = (struct tcp_fragment *)(rb + 1);
+            rb->pl_ref = -1;
         }
     }
     if (atake) {
@@ -1431,6 +1440,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
             ab->n = atake;
             ab->next = 0;
             ab->frag = (struct tcp_fragment *)(ab + 1);
+            ab->pl_ref = -1;
         }
     }
     unsigned char *pp = rb ? (unsigned char *)(rb->frag + rtake) : NULL;
@@ -1444,7 +1454,11 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
                 memset(fr, 0, sizeof(*fr));                                                  \
                 fr->dport = ntohs((SEG)->dport);                                             \
                 fr->sport = ntohs((SEG)->sport);                                             \
-                if ((PLEN) > 0) {                                                            \
+                if ((PLEN) > 0 && pl_ref >= 0 && (SEG)->ncopy == (uint32_t)(PLEN)) {         \
+                    fr->data = (unsigned char *)payload + (SEG)->offset; /* (no copy) */     \
+                    fr->length = (uint32_t)(PLEN);                                           \
+                    rb->pl_ref = pl_ref;                                                     \
+                } else if ((PLEN) > 0) {                                                     \
                     fr->data = pp;                                                           \
                     fr->length = (uint32_t)(PLEN);                                           \
                     memcpy(pp, payload ? payload + (SEG)->offset                             \
@@ -1496,8 +1510,9 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
     #undef PUT_FRAG
     #undef PUT_ACK
     if (rb) {
+        if (rb->pl_ref >= 0) rxg_payload_hold(g_ctx, rb->pl_ref); /* until the batch is freed */
         if (ring_enqueue(s->rcvbuf, &rb->item)) { /* (not reached: items <= fragments <= capacity) */
-            free(rb);
+            frag_item_free(&rb->item);
             g_stat[4] -= rtake, g_stat[1] += rtake;
         } else {
             s->rq += rtake;
@@ -1518,12 +1533,13 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
 /* the sorted segments, connection by connection (g_lock held); frames of
  * connections that need the frame-by-frame path are left unmarked */
 static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8_t *payload,
-                               rxg_mbuf *const *m, uint8_t *handled, int *rc_out) {
+                               int32_t pl_ref, rxg_mbuf *const *m, uint8_t *handled,
+                               int *rc_out) {
     for (uint32_t a = 0, b; a < nseg; a = b) {
         b = a + 1;
         while (b < nseg && sg[b].flow == sg[a].flow) b++;
         struct tcp_stream *s = sg[a].flow < s_tcb_cap ? s_tcb_cb[sg[a].flow] : NULL;
-        if (s) deliver_tcp_conn(s, sg + a, b - a, payload, m, handled, rc_out);
+        if (s) deliver_tcp_conn(s, sg + a, b - a, payload, pl_ref, m, handled, rc_out);
     }
 }
 
@@ -1600,7 +1616,9 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         }
         const double t2 = mono_ms();
         memset(s_handled, 0, n);
-        if (d.nseg) deliver_tcp_sorted(d.seg, d.nseg, d.tcp_payload, m, s_handled, rc_out);
+        if (d.nseg)
+            deliver_tcp_sorted(d.seg, d.nseg, d.tcp_payload, d.tcp_payload_ref, m, s_handled,
+                               rc_out);
         const double t3 = mono_ms();
         delivered += deliver_burst(m, n, s_v, rc_out, s_handled);
         g_udp_done = 0;

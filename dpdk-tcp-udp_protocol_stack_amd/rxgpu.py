@@ -113,7 +113,8 @@ class Delivery(C.Structure):
     """rxg_delivery (rxg_process_mbufs_deliver's results)"""
     _fields_ = [("dgram", C.c_void_p), ("first", C.c_void_p), ("udp_payload", C.c_void_p),
                 ("ndgram", C.c_uint32), ("nseg", C.c_uint32), ("udp_bytes", C.c_uint64),
-                ("seg", C.c_void_p), ("tcp_payload", C.c_void_p), ("tcp_bytes", C.c_uint64)]
+                ("seg", C.c_void_p), ("tcp_payload", C.c_void_p), ("tcp_bytes", C.c_uint64),
+                ("tcp_payload_ref", C.c_int32), ("_pad", C.c_uint32)]
 
 
 class GenCfg(C.Structure):
@@ -165,6 +166,8 @@ _tcp_compact_dev = _sig("rxg_tcp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _
                         _u64, _vp, _vp)
 _process_mbufs_deliver = _sig("rxg_process_mbufs_deliver", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
 _register_host = _sig("rxg_register_host", _i32, _vp, _vp, _u64)
+_payload_hold = _sig("rxg_payload_hold", _i32, _vp, _i32)
+_payload_release = _sig("rxg_payload_release", _i32, _vp, _i32)
 _unregister_host = _sig("rxg_unregister_host", _i32, _vp, _vp)
 _classify_dev = _sig("rxg_classify_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp)
 _classify_dev_cs = _sig("rxg_classify_dev_cs", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp,
@@ -224,7 +227,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp", "rxg_tcp_compact_dev", "rxg_process_mbufs_deliver",
-            "rxg_register_host", "rxg_unregister_host",
+            "rxg_register_host", "rxg_unregister_host", "rxg_payload_hold", "rxg_payload_release",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
             "rxg_rss_hash", "rxg_gen_flows", "rxg_gen_host", "rxg_gen_dev", "rxg_submit", "rxg_wait",

@@ -403,9 +403,24 @@ typedef struct rxg_delivery {
     const rxg_segment *seg;
     const uint8_t *tcp_payload;
     uint64_t tcp_bytes;
+    int32_t tcp_payload_ref;    /* >= 0: tcp_payload is pooled buffer `ref`, which the caller
+                                   may keep past the next call with rxg_payload_hold (and
+                                   must then rxg_payload_release); -1: valid until the next
+                                   call only */
+    uint32_t _pad;
 } rxg_delivery;
 int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
                               rxg_delivery *d, float ms[8]);
+/* Keep a burst's TCP payload buffer (rxg_delivery.tcp_payload_ref) alive past
+ * the context's next burst call — e.g. while receive fragments that point into
+ * it wait in a socket's ring — and let it go again.  Holds are counted; a
+ * buffer is reused once none is left.  RXG_PAYLOAD_BUFS buffers of max_bytes
+ * are pinned at most; with all of them held, the payloads of a burst come in
+ * the context's own buffer (tcp_payload_ref -1) and must be copied.  Both
+ * calls are safe from any thread (atomic counts). */
+#define RXG_PAYLOAD_BUFS 6
+int rxg_payload_hold(rxg_ctx *ctx, int32_t ref);
+int rxg_payload_release(rxg_ctx *ctx, int32_t ref);
 
 /* TX checksum generation (the send side's per-frame work, udp.c:84-95 and
  * tcp.c:444-463): for every IPv4 frame of the burst, the IPv4 header checksum
