@@ -1739,39 +1739,36 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
                                c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
             return rc;
     HIPCHK(hipEventRecord(c->tev[3], c->stream)); // after K3 / K4
-    if (udp) HIPCHK(hipMemcpyAsync(c->h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, c->stream));
-    if (tcp) HIPCHK(hipMemcpyAsync(c->h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if ((udp && c->h_cp_totals[2]) || (tcp && c->h_ss_totals[2]))
-        return RXG_ERANGE; // (not reached: staging bounds the payloads)
+    // every result in one round trip: the counts with upper-bound copies of
+    // the records (n of each) and payloads (the staged span bounds the sum of
+    // the 16-B padded payloads), so no synchronisation sits between the
+    // compactions and their copy out
     if (udp) {
-        d->ndgram = c->h_cp_totals[0];
-        d->udp_bytes = c->h_cp_totals[1];
+        HIPCHK(hipMemcpyAsync(c->h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(c->h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, c->stream));
-        if (d->ndgram)
-            HIPCHK(hipMemcpyAsync(c->h_cp_dg, c->d_cp_dg, (size_t)d->ndgram * sizeof(rxg_dgram),
-                                  hipMemcpyDeviceToHost, c->stream));
-        if (d->udp_bytes)
-            HIPCHK(hipMemcpyAsync(c->h_cp_payload, c->d_cp_payload, d->udp_bytes,
-                                  hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_cp_dg, c->d_cp_dg, (size_t)n * sizeof(rxg_dgram),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_cp_payload, c->d_cp_payload, pos, hipMemcpyDeviceToHost,
+                              c->stream));
     }
     if (tcp) {
-        d->nseg = c->h_ss_totals[0];
-        d->tcp_bytes = c->h_ss_totals[1];
-        if (d->nseg)
-            HIPCHK(hipMemcpyAsync(c->h_ss_seg, c->d_ss_seg, (size_t)d->nseg * sizeof(rxg_segment),
-                                  hipMemcpyDeviceToHost, c->stream));
-        if (d->tcp_bytes)
-            HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, d->tcp_bytes,
-                                  hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
+                              hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(hipEventRecord(c->tev[4], c->stream)); // after the results' copy out
     HIPCHK(hipStreamSynchronize(c->stream));
     rc = rxg_wait(c, t); // (the verdicts' copy out, on s_d2h)
     if (rc) return rc;
+    if ((udp && c->h_cp_totals[2]) || (tcp && c->h_ss_totals[2]))
+        return RXG_ERANGE; // (not reached: staging bounds the payloads)
+    if (udp) d->ndgram = c->h_cp_totals[0], d->udp_bytes = c->h_cp_totals[1];
+    if (tcp) d->nseg = c->h_ss_totals[0], d->tcp_bytes = c->h_ss_totals[1];
     if (ms) {
         ms[0] = (float)(t1 - t0);
         for (int k = 0; k < 4; ++k) HIPCHK(hipEventElapsedTime(&ms[k + 1], c->tev[k], c->tev[k + 1]));
