@@ -915,6 +915,40 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # delivery steps), median over the bursts
         res["rx_burst_phases_ms"] = {k: round(float(np.median([p[k] for p in phases])), 4)
                                      for k in phases[0]}
+        # the same bursts with the application on its own thread, as the
+        # reference runs it (app lcore beside the protocol lcore,
+        # netfamily.c:424-430): the app drains every socket in a loop while the
+        # protocol thread runs the bursts (nstack_rx_burst releases the stack's
+        # lock while a burst is on the GPU)
+        import threading
+        stop = threading.Event()
+        ov = [0, 0]
+
+        def app_thread():
+            b2 = np.zeros(65536, np.uint8)
+            while not stop.is_set():
+                g2, n2 = ns.drain_all(b2)
+                ov[0] += g2
+                ov[1] += n2
+                if g2 == 0:  # nothing queued: let the protocol thread take the lock
+                    time.sleep(0.0001)
+            g2, n2 = ns.drain_all(b2)
+            ov[0] += g2
+            ov[1] += n2
+        d0 = int(ns.stat(1))
+        th = threading.Thread(target=app_thread)
+        t0 = time.perf_counter()
+        th.start()
+        for _ in range(K):
+            ns.rx_burst_mbufs(arr, B)
+        stop.set()
+        th.join()
+        t_ov = time.perf_counter() - t0
+        res["overlapped"] = dict(mpps=round(B * K / t_ov / 1e6, 3), ms_per_burst=round(t_ov / K * 1e3, 3),
+                                 received=ov[0], payload_bytes=ov[1],
+                                 received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
+                                 note="application thread draining while the protocol thread runs "
+                                      "the bursts")
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
                    rx_burst_ms=round(t_rx / K * 1e3, 3), app_recv_ms=round(t_dr / K * 1e3, 3),

@@ -264,6 +264,12 @@ struct rxg_ctx {
         std::atomic<int> refs{0};
     } pl[RXG_PAYLOAD_BUFS];
     int pl_cur = -1; // the buffer of the latest burst (held by the library)
+    // a delivery burst between rxg_deliver_submit and rxg_deliver_wait
+    struct pending_delivery {
+        bool on = false, udp = false, tcp = false;
+        uint64_t ticket = 0;
+        double t0 = 0, t1 = 0;
+    } dl;
     uint32_t *d_ss_totals = nullptr, *h_ss_totals = nullptr;
     void *d_ss_ws = nullptr;
     size_t d_ss_ws_cap = 0;
@@ -1651,12 +1657,12 @@ static double now_ms() {
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
-int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
-                              rxg_delivery *d, float ms[8]) {
+int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                       rxg_delivery *d) {
     if (!c || !d) return RXG_EINVAL;
     memset(d, 0, sizeof(*d));
-    if (ms) memset(ms, 0, 8 * sizeof(float));
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (c->dl.on) return RXG_EINVAL; // (one delivery burst in flight per context)
     if (n && (!m || !out)) return RXG_EINVAL;
     if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
     const uint32_t nf = c->fs.udp.id_space();
@@ -1714,6 +1720,8 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
         d->udp_payload = c->h_cp_payload;
         memset(c->h_cp_first, 0, (nf + 1) * sizeof(uint32_t));
     }
+    c->dl = rxg_ctx::pending_delivery();
+    c->dl.t0 = t0;
     if (n == 0) return RXG_OK;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
@@ -1762,19 +1770,48 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
                               hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(hipEventRecord(c->tev[4], c->stream)); // after the results' copy out
-    HIPCHK(hipStreamSynchronize(c->stream));
-    rc = rxg_wait(c, t); // (the verdicts' copy out, on s_d2h)
+    c->dl.on = true;
+    c->dl.udp = udp;
+    c->dl.tcp = tcp;
+    c->dl.ticket = t;
+    c->dl.t1 = t1;
+    return RXG_OK;
+}
+
+// no field of the context's flow tables is read here: the control plane
+// (rxg_flows_*) may run beside it, from another thread (rxgpu.h)
+int rxg_deliver_wait(rxg_ctx *c, rxg_delivery *d, float ms[8]) {
+    if (!c || !d) return RXG_EINVAL;
+    if (ms) memset(ms, 0, 8 * sizeof(float));
+    if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
+    if (!c->dl.on) return RXG_OK; // (an empty burst: nothing in flight)
+    c->dl.on = false;
+    DEVGUARD(c);
+    HIPCHK(hipEventSynchronize(c->tev[4]));
+    int rc = rxg_wait(c, c->dl.ticket); // (the verdicts' copy out, on s_d2h)
     if (rc) return rc;
+    const bool udp = c->dl.udp, tcp = c->dl.tcp;
     if ((udp && c->h_cp_totals[2]) || (tcp && c->h_ss_totals[2]))
         return RXG_ERANGE; // (not reached: staging bounds the payloads)
     if (udp) d->ndgram = c->h_cp_totals[0], d->udp_bytes = c->h_cp_totals[1];
     if (tcp) d->nseg = c->h_ss_totals[0], d->tcp_bytes = c->h_ss_totals[1];
     if (ms) {
-        ms[0] = (float)(t1 - t0);
+        ms[0] = (float)(c->dl.t1 - c->dl.t0);
         for (int k = 0; k < 4; ++k) HIPCHK(hipEventElapsedTime(&ms[k + 1], c->tev[k], c->tev[k + 1]));
-        ms[5] = (float)(now_ms() - t0);
+        ms[5] = (float)(now_ms() - c->dl.t0);
     }
     return RXG_OK;
+}
+
+int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                              rxg_delivery *d, float ms[8]) {
+    int rc = rxg_deliver_submit(c, m, n, out, d);
+    if (rc) {
+        if (c) c->dl.on = false;
+        if (ms) memset(ms, 0, 8 * sizeof(float));
+        return rc;
+    }
+    return rxg_deliver_wait(c, d, ms);
 }
 
 int rxg_tx_cksum_dev(rxg_ctx *c, uint8_t *d_pkts, const uint32_t *d_off, const uint16_t *d_len,

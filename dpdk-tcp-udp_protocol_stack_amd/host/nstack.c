@@ -299,6 +299,7 @@ static uint32_t g_local_ip;
 static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
+static int g_rx_in_flight;      /* nstack_rx_burst waits for the GPU (g_lock released) */
 static int g_udp_done;          /* this burst's UDP datagrams went out as batches */
 
 /* the control block of each stable flow id (NULL: free id).  Blocks are
@@ -1593,7 +1594,9 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     if (!m && n) return RXG_EINVAL;
     pthread_mutex_lock(&g_lock);
     const double t0 = mono_ms();
-    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    /* one protocol thread (the reference's pkt_process lcore): a second
+     * rx_burst while one waits for the GPU is refused */
+    int rc = g_ctx && !g_rx_in_flight ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
     if (rc == RXG_OK && grow((void **)&s_handled, &s_handled_cap, n ? n : 1, 1)) rc = RXG_ENOMEM;
@@ -1602,13 +1605,28 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     /* the device half of delivery in one pass: classify, UDP payloads grouped
      * per socket (<= RXG_COMPACT_MAX_FLOWS ids: always, with the reference's
      * 1024 descriptors), TCP segments sorted per connection with their
-     * payloads gathered */
-    if (rc == RXG_OK) rc = rxg_process_mbufs_deliver(g_ctx, m, n, s_v, &d, gms);
+     * payloads gathered.  While it runs on the GPU the stack's lock is free:
+     * the application's socket calls proceed (the reference's app lcore runs
+     * beside its protocol lcore).  If they changed the blocks meanwhile, the
+     * burst is delivered like verdicts of an older snapshot: frame by frame,
+     * every lookup made again on the live lists. */
+    const uint64_t gen0 = g_snap_gen;
+    if (rc == RXG_OK) rc = rxg_deliver_submit(g_ctx, m, n, s_v, &d);
+    if (rc == RXG_OK) {
+        rxg_ctx *ctx = g_ctx;
+        g_rx_in_flight = 1;
+        pthread_mutex_unlock(&g_lock);
+        rc = rxg_deliver_wait(ctx, &d, gms);
+        pthread_mutex_lock(&g_lock);
+        g_rx_in_flight = 0;
+    }
     int delivered = 0;
     if (rc == RXG_OK) {
         const double t1 = mono_ms();
         if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
         g_burst_mutated = 0;
+        g_burst_stale = gen0 != g_snap_gen;
+        if (g_burst_stale) d.first = NULL, d.nseg = 0; /* (ids may name other blocks now) */
         if (d.first) {
             delivered = deliver_udp_batches(m, d.dgram, d.first, d.udp_payload,
                                             rxg_num_udp_ids(g_ctx));
@@ -1622,6 +1640,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         const double t3 = mono_ms();
         delivered += deliver_burst(m, n, s_v, rc_out, s_handled);
         g_udp_done = 0;
+        g_burst_stale = 0;
         const double t4 = mono_ms();
         for (int k = 0; k < 6; k++) g_phase_ms[k] = gms[k];
         g_phase_ms[6] = (float)(t2 - t1); /* UDP batches to the sockets */

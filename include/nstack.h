@@ -75,7 +75,11 @@ int nclose(int fd);
 /* Receive burst: the loop body of pkt_process (netfamily.c:152-200) for n
  * frames at once.  rc_out[i] (nullable) = what udp_process/tcp_process would
  * have returned (KNI frames: 1); v_out (nullable) = the verdicts.
- * Returns the number of UDP datagrams delivered, or a negative RXG_E* code. */
+ * Returns the number of UDP datagrams delivered, or a negative RXG_E* code.
+ * Called by one protocol thread, which also runs nstack_tx_burst (as
+ * pkt_process runs udp_out / tcp_out); while the burst is on the GPU the
+ * stack's lock is released, so application threads' socket calls run beside
+ * it (a second concurrent nstack_rx_burst gets RXG_EINVAL). */
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 
 /* Delivery half only: apply verdicts computed by rxg_* to the frames (UDP ->

@@ -411,6 +411,19 @@ typedef struct rxg_delivery {
 } rxg_delivery;
 int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
                               rxg_delivery *d, float ms[8]);
+/* rxg_process_mbufs_deliver in two halves, so the caller can let other work
+ * run while the burst is on the GPU: rxg_deliver_submit stages the burst and
+ * queues every device step and copy (d gets its buffer pointers), and
+ * rxg_deliver_wait(ctx, d, ms) waits for them and fills in d's counts and
+ * the phase times.  One delivery burst in flight per context (a second
+ * submit is RXG_EINVAL).  Between the two calls the context's control plane
+ * (rxg_flows_add / remove / update / commit-free changes) may run from another
+ * thread: rxg_deliver_wait reads none of the flow-table state; any other call
+ * on the context waits for rxg_deliver_wait first. */
+int rxg_deliver_submit(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
+                       rxg_delivery *d);
+int rxg_deliver_wait(rxg_ctx *ctx, rxg_delivery *d, float ms[8]);
+
 /* Keep a burst's TCP payload buffer (rxg_delivery.tcp_payload_ref) alive past
  * the context's next burst call — e.g. while receive fragments that point into
  * it wait in a socket's ring — and let it go again.  Holds are counted; a
