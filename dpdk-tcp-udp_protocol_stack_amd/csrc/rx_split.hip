@@ -323,39 +323,50 @@ extern "C" int rxg_rss_split(const uint8_t *pkts, const uint32_t *off, const uin
 // Frames that live in registered host memory (rxg_register_host: the mbuf
 // pool, pinned and mapped) into a staging burst on the device: the device
 // pulls each frame over PCIe, as a NIC's DMA into the ring would, instead of
-// a host memcpy into pinned staging followed by a copy.  A wave per frame:
-// 16-B loads from the mapped host address, stores at dst + (off << 6), bytes
-// past the frame's length zeroed to its 64-B end (the staging layout the
-// classify kernels read).  The host checked that every source is 16-B aligned
-// and that its 16-B rounded end stays inside its registered region.
+// a host memcpy into pinned staging followed by a copy.  Four lanes per
+// frame, 16 frames per wave (a 64-B frame is one 16-B load per lane, so a
+// wave instruction still moves 1 KiB), each group striding over its frame's
+// 16-B chunks, four loads in flight per lane; stores at dst + (off << 6),
+// bytes past the frame's length zeroed to its 64-B end (the staging layout
+// the classify kernels read).  The host checked that every source is 16-B
+// aligned and that its 16-B rounded end stays inside its registered region.
 namespace {
+__device__ __forceinline__ uint4 ingest_mask(uint4 v, uint32_t b, uint32_t l) {
+    if (b >= l) return make_uint4(0u, 0u, 0u, 0u);
+    if (b + 16u <= l) return v;
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t q = 0; q < 4u; ++q) {
+        const uint32_t b0 = b + 4u * q;
+        const uint32_t keep = l > b0 ? l - b0 : 0u;
+        if (keep < 4u) w[q] &= keep ? ((1u << (8u * keep)) - 1u) : 0u;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __global__ __launch_bounds__(256) void ingest_copy_kernel(const unsigned long long *__restrict__ src,
                                                           const uint32_t *__restrict__ off,
                                                           const uint16_t *__restrict__ len,
                                                           uint32_t n, uint8_t *__restrict__ dst) {
-    const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t f = blockIdx.x * 64u + (threadIdx.x >> 2), q = threadIdx.x & 3u;
     if (f >= n) return;
     const uint4 *s = reinterpret_cast<const uint4 *>(src[f]);
     const uint32_t l = len[f];
     const uint32_t nch = (l ? ((l + 63u) & ~63u) : 64u) >> 4; // chunks to the 64-B end
+    const uint32_t nsrc = (l + 15u) >> 4;                     // chunks holding frame bytes
     uint4 *d = reinterpret_cast<uint4 *>(dst + ((uint64_t)off[f] << 6));
-    for (uint32_t c = lane; c < nch; c += 64u) {
-        const uint32_t b = 16u * c;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (b < l) {
-            v = s[c];
-            if (b + 16u > l) { // the frame's last bytes: the rest of the chunk zeroed
-                uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t c0 = q; c0 < nch; c0 += 16u) {
+        uint4 v[4];
 #pragma unroll
-                for (uint32_t q = 0; q < 4u; ++q) {
-                    const uint32_t b0 = b + 4u * q;
-                    const uint32_t keep = l > b0 ? l - b0 : 0u;
-                    if (keep < 4u) w[q] &= keep ? ((1u << (8u * keep)) - 1u) : 0u;
-                }
-                v = make_uint4(w[0], w[1], w[2], w[3]);
-            }
+        for (uint32_t u = 0; u < 4u; ++u) {
+            const uint32_t c = c0 + 4u * u;
+            v[u] = c < nsrc ? s[c] : make_uint4(0u, 0u, 0u, 0u);
         }
-        d[c] = v;
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) {
+            const uint32_t c = c0 + 4u * u;
+            if (c < nch) d[c] = ingest_mask(v[u], 16u * c, l);
+        }
     }
 }
 } // namespace
@@ -363,6 +374,6 @@ __global__ __launch_bounds__(256) void ingest_copy_kernel(const unsigned long lo
 hipError_t rx_ingest_launch(const unsigned long long *src, const uint32_t *off, const uint16_t *len,
                             uint32_t n, uint8_t *dst, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(ingest_copy_kernel, dim3((n + 3u) / 4u), dim3(256), 0, s, src, off, len, n, dst);
+    hipLaunchKernelGGL(ingest_copy_kernel, dim3((n + 63u) / 64u), dim3(256), 0, s, src, off, len, n, dst);
     return hipGetLastError();
 }

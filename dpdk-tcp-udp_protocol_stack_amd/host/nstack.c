@@ -1743,28 +1743,74 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
     return rc;
 }
 
+/* the next fragment's payload into the cache while this one is copied (a
+ * batch's fragments sit one after the other in the pinned payload buffer) */
+static inline void prefetch_next(const struct tcp_fragment *f, struct nring *r) {
+    struct tcp_fragment *it;
+    if (ring_peek(r, (void **)&it) || !it->batch || f != &it->batch->frag[it->batch->next]) return;
+    const struct frag_batch *b = it->batch;
+    if (b->next + 1 >= b->n) return;
+    const unsigned char *d = b->frag[b->next + 1].data;
+    const uint32_t l = b->frag[b->next + 1].length;
+    for (uint32_t o = 0; d && o < l; o += 64) __builtin_prefetch(d + o, 0, 0);
+}
+
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
-    /* The whole walk holds g_lock: a concurrent nstack_rx_burst (LAST_ACK) or
-     * nclose could otherwise free a block this loop still reads.
-     * Every receive ring is read to its end, EOF fragments included (they
-     * count as nothing), like oracle_drain_all. */
+    /* The application side of the benchmark: every socket read until empty,
+     * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
+     * visited by stable id, DRAIN_CHUNK of them per hold of the stack's lock:
+     * a block is freed only under that lock (no block is read after
+     * a concurrent nstack_rx_burst freed it), and between chunks the protocol
+     * thread can take the lock.  A tcb's receive ring is read under one hold
+     * of its mutex: nrecv's semantics call by call (a fragment longer than
+     * `cap` takes nrecv's split path). */
+    enum { DRAIN_CHUNK = 64 };
     uint64_t got = 0, nb = 0;
-    pthread_mutex_lock(&g_lock);
-    for (struct localhost *h = g_pstHost; h; h = h->next) { /* the application's nrecvfrom loop */
-        ssize_t r;
-        struct sockaddr_in a;
-        while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0)
-            got++, nb += (uint64_t)r;
+    for (int kind = 0; kind < 2; kind++) {
+        uint32_t id = 0;
+        for (;;) {
+            pthread_mutex_lock(&g_lock);
+            const uint32_t ncap = kind ? s_tcb_cap : s_udp_cap;
+            if (id >= ncap) {
+                pthread_mutex_unlock(&g_lock);
+                break;
+            }
+            const uint32_t end = id + DRAIN_CHUNK < ncap ? id + DRAIN_CHUNK : ncap;
+            for (; id < end; id++) {
+                if (!kind) {
+                    struct localhost *h = s_udp_cb[id];
+                    if (!h) continue;
+                    ssize_t r;
+                    struct sockaddr_in a;
+                    while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0)
+                        got++, nb += (uint64_t)r;
+                    continue;
+                }
+                struct tcp_stream *s = s_tcb_cb[id];
+                if (!s) continue;
+                pthread_mutex_lock(&s->mutex);
+                struct tcp_fragment *f;
+                while ((f = tq_front(s->rcvbuf)) != NULL) {
+                    if (f->length > cap) { /* nrecv's split path */
+                        pthread_mutex_unlock(&s->mutex);
+                        const ssize_t r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT);
+                        if (r > 0) got++, nb += (uint64_t)r;
+                        pthread_mutex_lock(&s->mutex);
+                        continue;
+                    }
+                    if (f->length) {
+                        prefetch_next(f, s->rcvbuf);
+                        memcpy(buf, f->data, f->length);
+                        got++, nb += f->length;
+                    }
+                    tq_pop(s->rcvbuf, &s->rq);
+                }
+                tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
+                pthread_mutex_unlock(&s->mutex);
+            }
+            pthread_mutex_unlock(&g_lock);
+        }
     }
-    for (struct tcp_stream *s = g_tcb_set; s; s = s->next) { /* nrecv on every tcb */
-        ssize_t r;
-        while ((r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT)) >= 0)
-            if (r > 0) got++, nb += (uint64_t)r;
-        pthread_mutex_lock(&s->mutex); /* its queued control fragments (ACKs) sent */
-        tq_clear(s->sndbuf, &s->sq);
-        pthread_mutex_unlock(&s->mutex);
-    }
-    pthread_mutex_unlock(&g_lock);
     if (bytes) *bytes = nb;
     return (int64_t)got;
 }

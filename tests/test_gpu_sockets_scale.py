@@ -186,6 +186,15 @@ def test_socket_layer_256k_tcbs_churn_matches_oracle():
             times[kind].append(time.perf_counter() - t0)
             st.ns.drain_all(np.zeros(65536, np.uint8))
         med = {k: float(np.median(v)) * 1e3 for k, v in times.items()}
+        import json
+        import os
+        out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+        if os.path.isdir(out):  # the session's record
+            with open(os.path.join(out, "sockets_scale_256k.json"), "w") as f:
+                json.dump(dict(tcbs=N_EST, frames_per_burst=4000, rx_burst_ms_median=med,
+                               ratio=med["mutated"] / med["unmutated"],
+                               times_ms={k: [t * 1e3 for t in v] for k, v in times.items()},
+                               last_compared_burst_phases_ms=ph), f, indent=1)
         print(f"\n256K tcbs: rx_burst of 4000 data segments {med['unmutated']:.3f} ms, "
               f"with 16 SYNs mid-burst {med['mutated']:.3f} ms "
               f"(x{med['mutated'] / med['unmutated']:.2f}); last compared burst phases {ph}")
