@@ -16,7 +16,7 @@ step() { local name=$1 t=$2; shift 2; echo "== $name: $*"; date +%T; timeout -k 
 if [ "${TESTS:-1}" = 1 ]; then
   # plain test failures (rc 1) still let the bench run; anything else (a
   # timeout, an abort, a fault) ends the session
-  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 170 --timeout-method thread ${PYTEST_K:-}
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 170 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
   rc=$?; [ $rc -le 1 ] || exit $rc
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
