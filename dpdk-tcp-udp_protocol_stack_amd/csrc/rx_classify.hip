@@ -1777,6 +1777,56 @@ __device__ __forceinline__ sh_head sh_parse(const uint4 (&c)[4], int32_t cp) {
     return h;
 }
 
+// a parsed head in two words besides its key (EP: kept through the stream):
+// a = tl | dgl << 16, b = stored | proto << 16 | cl << 24 | hl << 28
+__device__ __forceinline__ uint32_t sh_pack_a(const sh_head &h) { return h.tl | (h.dgl << 16); }
+__device__ __forceinline__ uint32_t sh_pack_b(const sh_head &h) {
+    return h.stored | (h.proto << 16) | (h.cl << 24) | (h.hl << 28);
+}
+__device__ __forceinline__ sh_head sh_unpack(uint32_t ka, uint32_t kb, uint32_t kc, uint32_t a,
+                                             uint32_t b, int32_t cp) {
+    sh_head h;
+    h.tl = a & 0xFFFFu;
+    h.dgl = a >> 16;
+    h.stored = b & 0xFFFFu;
+    h.proto = (b >> 16) & 0xFFu;
+    h.cl = (b >> 24) & 0xFu;
+    h.hl = b >> 28;
+    h.ka = ka;
+    h.kb = kb;
+    h.kc = kc;
+    h.is_udp = h.cl == RXG_CLS_UDP;
+    h.is_tcp = h.cl == RXG_CLS_TCP;
+    h.l4 = h.is_udp || h.is_tcp;
+    h.nd = h.cl == RXG_CLS_ARP ? 42u
+         : h.cl == RXG_CLS_NON_IP ? 14u
+         : h.is_udp ? 42u
+         : h.is_tcp ? 54u
+                    : 24u;
+    h.l4n = h.tl >= 20u ? h.tl - 20u : 0u;
+    h.do_sum = h.l4 && h.tl >= 20u;
+    if (h.l4 && 34u + h.l4n > h.nd) h.nd = 34u + h.l4n;
+    h.e = h.do_sum ? 34 + (int32_t)h.l4n : 0;
+    if (h.e > cp) h.e = cp;
+    return h;
+}
+
+// the checksum words of head chunks 1..3 (the header bytes [0, 26) and the
+// L4 checksum field excluded) plus the pseudo-header's {proto, L4 length}
+__device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_head &h) {
+    uint4 h1 = c[1], h2 = c[2], h3 = c[3];
+    h1.x = 0;
+    h1.y = 0;
+    h1.z &= 0xFFFF0000u;
+    if (h.is_udp) h2.z &= 0xFFFF0000u;
+    if (h.is_tcp) h3.x &= 0x0000FFFFu;
+    uint32_t acc = lane_chunk_sum(0u, h1, 16, h.e);
+    acc = lane_chunk_sum(acc, h2, 32, h.e);
+    acc = lane_chunk_sum(acc, h3, 48, h.e);
+    if (h.do_sum) acc += (h.proto << 8) + rx_bswap16(h.l4n); // pseudo-header words
+    return acc;
+}
+
 // ABL (diagnostic builds, pipes 160 / 264): 1 = no flow-table probe (flow id
 // from the port; wrong verdicts by construction), 2 = every partial last
 // chunk loaded from HBM after the stream (no partial marks).  PW: slots of the first probe window
@@ -1786,24 +1836,51 @@ __device__ __forceinline__ sh_head sh_parse(const uint4 (&c)[4], int32_t cp) {
 // MAPC: span chunks the head map covers.  (A map for 256 frames of 1500 B,
 // 388 KiB of span at 3 blocks/CU, ran cfg3 at 1.161 vs 1.042 ms for the G=8
 // group kernel: profiles/r02ac.)
-template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC>
-__global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_kernel(
+// EP (pipe 65): every frame's probe is issued as soon as its head is known,
+// inside the stream, instead of after it, so the block no longer ends on the
+// probe round trip.  A frame whose head completes in tile t < last has it
+// parsed from LDS after tile t's barrier; a frame whose head completes in the
+// block's LAST tile ("early") has its four head chunks loaded at the block
+// start by LDS-DMA (no VGPRs held through the stream; its head chunks are not
+// marked in the map) and parsed after tile 0.  The parsed head is kept as 7
+// words per lane; the probe window (PW <= 3 slots) is loaded by LDS-DMA into
+// the frame's own head slots 1..3, which the parse has freed (s_hd is
+// slot-major, [k][256], so one wave's slot k is the lane-linear 1 KiB an
+// LDS-DMA instruction writes).  An early frame's s_rel carries bit 15, so the
+// stream never takes one of its chunks for a head chunk (a chunk no frame
+// marked reads as thread 255's).
+// PS: the lane that streams a frame's partial last chunk sums it (masked at
+// the capture, from s_cp) into s_psum instead of storing the chunk in head
+// slot 0, so a head takes 48 B of LDS instead of 64 (with 8-KiB tiles the
+// block fits 6 per CU: 26.1 KiB).
+template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
+          bool PS = false>
+__global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    constexpr uint32_t LPT = 4;          // 16-B chunks per thread per tile
+    // 16-B chunks per thread per tile (EP: 12-KiB tiles, so the parse inside
+    // the stream fits the 96 VGPRs of 5 blocks/CU without scratch)
+    constexpr uint32_t LPT = L;
     constexpr uint32_t TCH = 256u * LPT; // chunks per tile (16 KiB)
     __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
     __shared__ __attribute__((aligned(16))) uint8_t s_map[MAPC];
-    __shared__ __attribute__((aligned(16))) uint4 s_hd[256 * 4];
+    static_assert(!(EP && PS), "EP keeps chunk 0 in head slot 0");
+    __shared__ __attribute__((aligned(16))) uint4 s_hd[256 * (PS ? 3 : 4)];
+    __shared__ uint32_t s_psum[PS ? 256 : 1]; // PS: each frame's partial-chunk sum
+    __shared__ uint16_t s_cp[PS ? 256 : 1];   // PS: each frame's capture length
     __shared__ uint16_t s_rel[256]; // each frame's first chunk in the span
     __shared__ uint32_t s_et[16];   // each frame's ether-type class, 2 bits (1 IPv4, 2 ARP)
     __shared__ unsigned long long s_lo, s_hi;
     __shared__ uint32_t s_tail, s_pk255; // thread 255's partial chunk (an unmarked chunk reads as 255)
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
+    // head slot k of frame m
+    auto hdi = [](uint32_t m, uint32_t k) -> uint32_t {
+        return EP ? k * 256u + m : (PS ? (k - 1u) * 256u + m : m * 4u + k);
+    };
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
     if (tid == 0) {
         s_lo = ~0ull;
@@ -1845,12 +1922,19 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     tile_load(va, 0);
     const uint32_t rel = (streamed && cp > 0) ? (uint32_t)(fc - lo) : 0u;
     const uint32_t nh = nch < 4u ? nch : 4u;
+    // EP: the stream's last tile, the tile that completes this frame's head
+    const uint32_t tlast = span ? (span - 1u) / TCH : 0u;
+    const uint32_t thead = cp > 0 ? (rel + nh - 1u) / TCH : 0u;
+    const bool early = EP && streamed && cp >= 14 && tlast > 0 && thead == tlast;
+    const uint32_t relx = early ? 0x8000u : 0u; // (rel < MAPC < 0x8000)
     if (streamed) {
-        for (uint32_t k = 0; k < nh; ++k) s_map[rel + k] = (uint8_t)tid;
-        s_rel[tid] = (uint16_t)rel;
+        if (!early)
+            for (uint32_t k = 0; k < nh; ++k) s_map[rel + k] = (uint8_t)tid;
+        s_rel[tid] = (uint16_t)(rel + relx);
         if (part && !(ABL & 2)) {
             s_map[rel + ((uint32_t)cf >> 4)] = (uint8_t)tid;
-            if (tid == 255) s_pk255 = (uint32_t)cf >> 4;
+            if constexpr (PS) s_cp[tid] = (uint16_t)cp;
+            if (tid == 255) s_pk255 = ((uint32_t)cf >> 4) - relx;
         }
     }
     __syncthreads(); // map complete
@@ -1861,30 +1945,51 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     bool direct = cp > 0 && (!streamed || cp < 14);
     bool plost = false;
     if (streamed) {
-        for (uint32_t k = 0; k < nh; ++k)
-            if (s_map[rel + k] != (uint8_t)tid) direct = true; // shared head chunk
+        if (!early)
+            for (uint32_t k = 0; k < nh; ++k)
+                if (s_map[rel + k] != (uint8_t)tid) direct = true; // shared head chunk
         plost = part && ((ABL & 2) || s_map[rel + ((uint32_t)cf >> 4)] != (uint8_t)tid);
+    }
+    // EP: the frames whose probe goes out inside the stream (the rest, rare,
+    // keep the after-stream path)
+    const bool inflight = EP && streamed && cp >= 14 && !direct && tlast > 0;
+    if constexpr (EP) {
+        if (__ballot(early) != 0ull) { // the early heads, by LDS-DMA into slots 0..3
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                    rx_lds_addr(&s_hd[hdi(64u * wvu, (uint32_t)k)]));
+                if (early) rx_dma16(16 * k < cp ? fb + 16 * k : fb, dst);
+            }
+        }
     }
 
     // ---- flow probe loads: the port entry (UDP: the direct port table; TCP:
     // the listener) and the hashed table's home slot, issued once per frame
     static_assert(PW == 1 || PW == 2 || PW == 4, "probe window");
+    static_assert(!EP || PW <= 2, "EP: the window lives in head slots 1..2, the parsed key in 3");
     static_assert(PW - 1 <= RX_FT_MIRROR, "window past the mirrored slots");
     uint32_t pe = RXG_FLOW_NONE;
     uint4 sw[PW];
-    auto issue_probe = [&](const uint4 (&c)[4]) {
-        const sh_head h = sh_parse(c, cp);
+    // the probe's first loads of a parsed head: the port entry (returned) and
+    // the hashed table's home window (sp0, when hash0)
+    auto probe_src = [&](const sh_head &h, bool &hash0, const uint4 *&sp0) -> uint32_t {
         const bool probe0 =
             valid && h.l4 && (h.is_udp ? ft.udp_probe : ft.tcp_probe) > 0 && !(ABL & 1);
         const bool udp_port = h.is_udp && ft.udp_port != nullptr;
         const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
         const uint32_t dport = h.is_udp ? h.kb : (h.kc >> 16);
-        const bool hash0 = probe0 && !udp_port;
-        const uint4 *sp0 =
-            hash0 ? (h.is_udp ? ft.udp : ft.tcp) +
-                        (rx_hash3s(ft.hseed, h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask))
-                  : reinterpret_cast<const uint4 *>(pkts);
-        pe = (ABL & 1) ? RXG_FLOW_NONE : ptab[h.l4 ? dport : 0u];
+        hash0 = probe0 && !udp_port;
+        sp0 = hash0 ? (h.is_udp ? ft.udp : ft.tcp) +
+                          (rx_hash3s(ft.hseed, h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask))
+                    : reinterpret_cast<const uint4 *>(pkts);
+        return (ABL & 1) ? RXG_FLOW_NONE : ptab[h.l4 ? dport : 0u];
+    };
+    auto issue_probe = [&](const uint4 (&c)[4]) {
+        const sh_head h = sh_parse(c, cp);
+        bool hash0;
+        const uint4 *sp0;
+        pe = probe_src(h, hash0, sp0);
 #pragma unroll
         for (int w = 0; w < PW; ++w) sw[w] = ld_slot(sp0 + (hash0 ? w : 0));
     };
@@ -1894,7 +1999,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         const uint32_t ec = (s_et[tid >> 4] >> (2u * (tid & 15u))) & 3u;
         c[0] = make_uint4(0, 0, 0, ec == 1u ? 0x0008u : (ec == 2u ? 0x0608u : 0u));
 #pragma unroll
-        for (int k = 1; k < 4; ++k) c[k] = chunk_below(s_hd[tid * 4u + k], 16 * k, cp);
+        for (int k = 1; k < 4; ++k) c[k] = chunk_below(s_hd[hdi(tid, (uint32_t)k)], 16 * k, cp);
     };
 
     // ---- stream: tile prefixes, head capture, boundary pickup ---------------
@@ -1918,7 +2023,10 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
                 } else if (hk < 4u || m != 255u || hk == pk255) {
                     // head chunks 1..3, or the owner's partial chunk (the only
                     // other chunk it marks) into slot 0
-                    s_hd[m * 4u + (hk < 4u ? hk : 0u)] = v[j];
+                    if (!PS || hk < 4u)
+                        s_hd[hdi(m, hk < 4u ? hk : 0u)] = v[j];
+                    else
+                        s_psum[m] = lane_chunk_sum(0u, v[j], 16 * (int32_t)hk, (int32_t)s_cp[m]);
                 }
             }
         }
@@ -1953,14 +2061,46 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
         }
         carry = base;
     };
+    // EP: after tile c0's barrier, the frames whose head is now known parse it,
+    // keep it packed, load the port entry and send the window's LDS-DMA
+    uint32_t spa = 0, spb = 0;
+    auto ep_issue = [&](uint32_t c0) {
+        if constexpr (EP) {
+            const bool due = inflight && (early ? c0 == 0u : (thead >> 1) * (2u * TCH) == c0);
+            if (__ballot(due) == 0ull) return;
+            // the early heads' LDS-DMA went out before the next tile's LPT
+            // loads (the counter retires in order; the stream waited as far)
+            if (c0 == 0u) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+            if (due) {
+                uint4 c[4];
+                head_of(c);
+                if (early) c[0] = s_hd[hdi(tid, 0u)]; // (only its ether type is parsed)
+                const sh_head h = sh_parse(c, cp);
+                spa = sh_pack_a(h);
+                spb = sh_pack_b(h);
+                // slots 1..3 were read above: the key and the head sum to slot 3
+                s_hd[hdi(tid, 3u)] = make_uint4(h.ka, h.kb, h.kc, sh_head_sum(c, h));
+                bool hash0;
+                const uint4 *sp0;
+                pe = probe_src(h, hash0, sp0);
+                if (hash0) // the window to slots 1..PW
+#pragma unroll
+                    for (int w = 0; w < PW; ++w)
+                        rx_dma16(sp0 + w, __builtin_amdgcn_readfirstlane(
+                                              rx_lds_addr(&s_hd[hdi(64u * wvu, 1u + w)])));
+            }
+        }
+    };
     uint32_t c0 = 0;
     for (; c0 < span; c0 += 2 * TCH) {
         tile_load(vb, c0 + TCH);
         stile(va, c0, 0);
         tile_load(va, c0 + 2 * TCH);
         stile(vb, c0 + TCH, 1);
+        ep_issue(c0); // the heads completed in this pair of tiles
     }
     __syncthreads(); // the last tile's prefixes and every head slot written
+    if constexpr (EP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the windows landed
     if (streamed) {
         const uint32_t p0 = c0 - TCH;
         if (cs - p0 < TCH) es = s_pre[1][cs - p0];
@@ -1979,31 +2119,41 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
 #pragma unroll
             for (int k = 0; k < 4; ++k) c[k] = chunk_below(hd[k], 16 * k, cp);
     }
-    issue_probe(c);
-    const sh_head h = sh_parse(c, cp);
-    uint4 h1 = c[1], h2 = c[2], h3 = c[3];
-    h1.x = 0;
-    h1.y = 0;
-    h1.z &= 0xFFFF0000u;
-    if (h.is_udp) h2.z &= 0xFFFF0000u;
-    if (h.is_tcp) h3.x &= 0x0000FFFFu;
+    sh_head h;
+    uint32_t acc;
+    if (EP && inflight) { // parsed inside the stream; the window in slots 1..PW
+        const uint4 k3 = s_hd[hdi(tid, 3u)];
+        h = sh_unpack(k3.x, k3.y, k3.z, spa, spb, cp);
+        acc = k3.w;
+#pragma unroll
+        for (int w = 0; w < PW; ++w) sw[w] = s_hd[hdi(tid, 1u + w)];
+    } else {
+        issue_probe(c);
+        h = sh_parse(c, cp);
+        acc = sh_head_sum(c, h);
+    }
     const int32_t e = h.e;
-    uint32_t acc = lane_chunk_sum(0u, h1, 16, e);
-    acc = lane_chunk_sum(acc, h2, 32, e);
-    acc = lane_chunk_sum(acc, h3, 48, e);
-    if (h.do_sum) acc += (h.proto << 8) + rx_bswap16(h.l4n); // pseudo-header words
     // the sum ends where the capture does (the common case): tail from the
     // stream prefixes, the partial chunk from its slot; otherwise re-sum from HBM
     if (h.do_sum && e > 64) {
         if (streamed && e == cp) {
             if (tailf) acc += ee - es;
             if (part) {
-                uint4 pv = s_hd[tid * 4u];
-                if (__ballot(plost) != 0ull) { // rare (wave-uniform branch): lost mark
-                    const uint4 ph = ldg16<false>(plost ? fb + cf : pkts);
-                    if (plost) pv = ph;
+                if constexpr (PS) {
+                    uint32_t ps = plost ? 0u : s_psum[tid];
+                    if (__ballot(plost) != 0ull) { // rare (wave-uniform branch): lost mark
+                        const uint4 ph = ldg16<false>(plost ? fb + cf : pkts);
+                        if (plost) ps = lane_chunk_sum(0u, ph, cf, e);
+                    }
+                    acc += ps;
+                } else {
+                    uint4 pv = s_hd[hdi(tid, 0u)];
+                    if (__ballot(plost) != 0ull) { // rare (wave-uniform branch): lost mark
+                        const uint4 ph = ldg16<false>(plost ? fb + cf : pkts);
+                        if (plost) pv = ph;
+                    }
+                    acc = lane_chunk_sum(acc, pv, cf, e);
                 }
-                acc = lane_chunk_sum(acc, pv, cf, e);
             }
         } else {
             for (int32_t s = 64; s < e; s += 16) acc = lane_chunk_sum(acc, ldg16<false>(fb + s), s, e);
@@ -2105,14 +2255,18 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : 5) void rx_classify_sh_ke
     }
 }
 
-template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC>
+template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
+          bool PS = false>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                      const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC>), dim3((uint32_t)blocks), dim3(256),
+    if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
+        return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
+                                              lds_bins, s, nullptr, nullptr);
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2476,6 +2630,16 @@ static const variant_entry k_variants[] = {
     // 63 / 64: 60 with a two / four-slot first probe window
     {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
     {0, 1, 1, 63, launch_sh<0, 2>}, {0, 1, 1, 64, launch_sh<0, 4>},
+    // 65 / 61: probes issued inside the stream (early heads and windows by
+    // LDS-DMA), a two / one-slot window
+    {0, 1, 1, 65, launch_sh<0, 2, SH_MAPC, true>}, {0, 1, 1, 61, launch_sh<0, 1, SH_MAPC, true>},
+    // 66 / 67: 64 with 12-KiB / 8-KiB tiles; 62: 65 with 8-KiB tiles
+    {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>}, {0, 1, 1, 67, launch_sh<0, 4, SH_MAPC, false, 2>},
+    {0, 1, 1, 62, launch_sh<0, 2, SH_MAPC, true, 2>},
+    // 68 / 69: 67 / 66 with partial-chunk sums in the stream (48-B heads:
+    // 68 fits 6 blocks per CU)
+    {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},
+    {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
     {0, 1, 1, 264, launch_sh<2, 4>},
@@ -2524,7 +2688,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (g >= 4) return "rx_classify_kernel";
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
-    case 60: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
+    case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";

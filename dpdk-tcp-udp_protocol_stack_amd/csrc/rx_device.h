@@ -88,6 +88,30 @@ __device__ __forceinline__ uint4 ld_slot(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// LDS byte address of a __shared__ object
+__device__ __forceinline__ uint32_t rx_lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char *)p);
+}
+// LDS-DMA (global_load_lds_dwordx4): each active lane loads the 16 B at src
+// (16-B aligned) into LDS at lds + 16 * lane; lds is wave-uniform.  No VGPR
+// is written.  The compiler does not count it: its data is read only after an
+// s_waitcnt vmcnt the caller places (by the issuing wave; other waves also
+// need a barrier after that wait).  The lgkmcnt(0) retires the wave's pending
+// LDS reads first, so none of them can see the DMA's bytes.  M0 is set and
+// restored inside the statement (the compiler owns it).
+__device__ __forceinline__ void rx_dma16(const void *src, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                 "s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %2\n\t"
+                 "s_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+
 // the streamed 16-B outputs (verdicts, count indices).  RX_ST_POLICY 0: nt
 // stores, which KEEP the written line in the XCD's L2; 1: sc1 (write-through)
 // stores, which drop it (MI355X_MICROARCH.md, store flavours), so hundreds of

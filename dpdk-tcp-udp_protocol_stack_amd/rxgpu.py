@@ -69,7 +69,10 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 46),  # 38 with the span from the descriptors
                    (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
                    (0, 0, 0, 60),  # heads taken out of the block stream
-                   (0, 0, 0, 63), (0, 0, 0, 64)]  # 60 with a 2 / 4-slot probe window
+                   (0, 0, 0, 63), (0, 0, 0, 64),  # 60 with a 2 / 4-slot probe window
+                   (0, 0, 0, 66), (0, 0, 0, 67),  # 64 with 12-KiB / 8-KiB tiles
+                   (0, 0, 0, 68), (0, 0, 0, 69),  # 67 / 66 with partial-chunk sums in the stream
+                   (0, 0, 0, 65), (0, 0, 0, 61), (0, 0, 0, 62)]  # probes inside the stream (LDS-DMA)
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

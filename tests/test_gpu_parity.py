@@ -290,7 +290,9 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
 @pytest.mark.parametrize("load_log2", [1, 4])
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
                                      (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 60),
-                                     (0, 0, 0, 63), (0, 0, 0, 64), (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
+                                     (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65), (0, 0, 0, 61),
+                                     (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
+                                     (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor
     (rxg_tune_flow_load: longer probe chains at <= 1/2, sparse tables at
@@ -329,7 +331,9 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 @pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
-                                     (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (4, 1, 2, 0),
+                                     (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
+                                     (0, 0, 0, 61), (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
+                                     (4, 1, 2, 0),
                                      (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),
                                      (0, 0, 0, 739)])
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
@@ -398,7 +402,9 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
     assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), len(hints) * wcnt)
 
 
-@pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 54)])
+@pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
+                                     (0, 0, 0, 61), (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
+                                     (0, 0, 0, 54)])
 @pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix", "dirty_gaps", "reversed",
                                   "empty"])
 def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
