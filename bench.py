@@ -915,6 +915,27 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # delivery steps), median over the bursts
         res["rx_burst_phases_ms"] = {k: round(float(np.median([p[k] for p in phases])), 4)
                                      for k in phases[0]}
+        # A/B: each burst as two halves, both on the GPU at once
+        # (nstack_set_halves; off by default)
+        ns.set_halves(B // 2)
+        h_rx = h_dr = 0.0
+        h_items = 0
+        h_ph = []
+        for _ in range(K):
+            t0 = time.perf_counter()
+            ns.rx_burst_mbufs(arr, B)
+            t1 = time.perf_counter()
+            h_ph.append(ns.last_burst_phases())
+            g, _ = ns.drain_all(rbuf)
+            h_rx += t1 - t0
+            h_dr += time.perf_counter() - t1
+            h_items += g
+        ns.set_halves(0)
+        res["halves"] = dict(mpps=round(B * K / (h_rx + h_dr) / 1e6, 3),
+                             rx_burst_ms=round(h_rx / K * 1e3, 3), app_recv_ms=round(h_dr / K * 1e3, 3),
+                             received_equal=h_items == items,
+                             rx_burst_phases_ms={k: round(float(np.median([p[k] for p in h_ph])), 4)
+                                                 for k in h_ph[0]})
         # the same bursts with the application on its own thread, as the
         # reference runs it (app lcore beside the protocol lcore,
         # netfamily.c:424-430): the app drains every socket in a loop while the
@@ -935,7 +956,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             g2, n2 = ns.drain_all(b2)
             ov[0] += g2
             ov[1] += n2
-        d0 = int(ns.stat(1))
+        d0, s0 = int(ns.stat(1)), int(ns.stat(5))
         th = threading.Thread(target=app_thread)
         t0 = time.perf_counter()
         th.start()
@@ -947,6 +968,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         res["overlapped"] = dict(mpps=round(B * K / t_ov / 1e6, 3), ms_per_burst=round(t_ov / K * 1e3, 3),
                                  received=ov[0], payload_bytes=ov[1],
                                  received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
+                                 stale_bursts=int(ns.stat(5)) - s0,
                                  note="application thread draining while the protocol thread runs "
                                       "the bursts")
         frame_bytes = int(ln.astype(np.int64).sum())

@@ -253,8 +253,8 @@ struct rxg_ctx {
     size_t d_cp_ws_cap = 0;
     // TCP segment sort + payload gather (K4, rxg_process_mbufs_deliver): device
     // results and their pinned host copies, sized by max_pkts / max_bytes
-    rxg_segment *d_ss_seg = nullptr, *h_ss_seg = nullptr;
-    uint8_t *d_ss_payload = nullptr, *h_ss_payload = nullptr;
+    rxg_segment *d_ss_seg = nullptr;
+    uint8_t *d_ss_payload = nullptr;
     // pinned payload buffers a caller may keep past the next burst
     // (rxg_payload_hold / _release: the receive fragments of a burst point
     // into them until the application has read them); refs counts the holds,
@@ -263,18 +263,27 @@ struct rxg_ctx {
         uint8_t *h = nullptr;
         std::atomic<int> refs{0};
     } pl[RXG_PAYLOAD_BUFS];
-    int pl_cur = -1; // the buffer of the latest burst (held by the library)
-    // a delivery burst between rxg_deliver_submit and rxg_deliver_wait
-    struct pending_delivery {
+    // the delivery sets (rxg_deliver_submit / _wait): up to RXG_DELIVER_DEPTH
+    // bursts in flight, each with its own pinned copies of the results (the
+    // device buffers are shared: every step runs on `stream`, in order) and its
+    // phase events; a set's results stay valid until the set is reused
+    struct delivery_set {
         bool on = false, udp = false, tcp = false;
         uint64_t ticket = 0;
         double t0 = 0, t1 = 0;
-    } dl;
-    uint32_t *d_ss_totals = nullptr, *h_ss_totals = nullptr;
+        int pl = -1; // the pooled payload buffer the library holds for this set
+        rxg_dgram *h_cp_dg = nullptr;
+        uint32_t *h_cp_first = nullptr, *h_cp_totals = nullptr;
+        uint8_t *h_cp_payload = nullptr;
+        rxg_segment *h_ss_seg = nullptr;
+        uint8_t *h_ss_payload = nullptr;
+        uint32_t *h_ss_totals = nullptr;
+        hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    } dls[RXG_DELIVER_DEPTH];
+    uint32_t dl_next = 0; // the set the next submit takes (round robin)
+    uint32_t *d_ss_totals = nullptr;
     void *d_ss_ws = nullptr;
     size_t d_ss_ws_cap = 0;
-    // phase timing of rxg_process_mbufs_deliver (timing-enabled events)
-    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // registered host memory (rxg_register_host): frames of an mbuf burst that
     // all lie in it are pulled by the device instead of gathered on the host
     struct host_region {
@@ -730,13 +739,16 @@ void rxg_close(rxg_ctx *c) {
     (void)hipFree(c->d_ss_payload);
     (void)hipFree(c->d_ss_totals);
     (void)hipFree(c->d_ss_ws);
-    if (c->h_ss_seg) (void)hipHostFree(c->h_ss_seg);
-    if (c->h_ss_payload) (void)hipHostFree(c->h_ss_payload);
-    if (c->h_ss_totals) (void)hipHostFree(c->h_ss_totals);
+    for (rxg_ctx::delivery_set &ds : c->dls) {
+        for (void *h : {(void *)ds.h_cp_dg, (void *)ds.h_cp_first, (void *)ds.h_cp_totals,
+                        (void *)ds.h_cp_payload, (void *)ds.h_ss_seg, (void *)ds.h_ss_payload,
+                        (void *)ds.h_ss_totals})
+            if (h) (void)hipHostFree(h);
+        for (hipEvent_t e : ds.tev)
+            if (e) (void)hipEventDestroy(e);
+    }
     for (rxg_ctx::pl_buf &b : c->pl)
         if (b.h) (void)hipHostFree(b.h);
-    for (hipEvent_t e : c->tev)
-        if (e) (void)hipEventDestroy(e);
     if (c->h_cp_dg) (void)hipHostFree(c->h_cp_dg);
     if (c->h_cp_first) (void)hipHostFree(c->h_cp_first);
     if (c->h_cp_payload) (void)hipHostFree(c->h_cp_payload);
@@ -1662,66 +1674,73 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
     if (!c || !d) return RXG_EINVAL;
     memset(d, 0, sizeof(*d));
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (c->dl.on) return RXG_EINVAL; // (one delivery burst in flight per context)
     if (n && (!m || !out)) return RXG_EINVAL;
     if (n > c->max_pkts || !c->slots[0].h_stage) return RXG_ERANGE;
+    // the next set in turn, which must have been waited for
+    const uint32_t si = c->dl_next;
+    rxg_ctx::delivery_set &ds = c->dls[si];
+    if (ds.on) return RXG_EINVAL; // (RXG_DELIVER_DEPTH bursts in flight already)
     const uint32_t nf = c->fs.udp.id_space();
     const bool udp = nf > 0 && nf <= RXG_COMPACT_MAX_FLOWS;
     DEVGUARD(c);
     const double t0 = now_ms();
     // results buffers, first use (each set last-allocated-first-checked: a
     // failed allocation leaves the rest for the next call to retry)
-    if (udp && !c->h_cp_totals) {
+    if (udp && !ds.h_cp_totals) {
         if (!c->d_cp_dg) HIPCHK(hipMalloc(&c->d_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram)));
         if (!c->d_cp_first)
             HIPCHK(hipMalloc(&c->d_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t)));
         if (!c->d_cp_payload) HIPCHK(hipMalloc(&c->d_cp_payload, c->max_bytes));
         if (!c->d_cp_totals) HIPCHK(hipMalloc(&c->d_cp_totals, 4 * sizeof(uint32_t)));
-        if (!c->h_cp_dg)
-            HIPCHK(hipHostMalloc((void **)&c->h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
-        if (!c->h_cp_first)
-            HIPCHK(hipHostMalloc((void **)&c->h_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
-        if (!c->h_cp_payload) HIPCHK(hipHostMalloc((void **)&c->h_cp_payload, c->max_bytes, 0));
-        HIPCHK(hipHostMalloc((void **)&c->h_cp_totals, 4 * sizeof(uint32_t), 0));
+        if (!ds.h_cp_dg)
+            HIPCHK(hipHostMalloc((void **)&ds.h_cp_dg, (size_t)c->max_pkts * sizeof(rxg_dgram), 0));
+        if (!ds.h_cp_first)
+            HIPCHK(hipHostMalloc((void **)&ds.h_cp_first, (RXG_COMPACT_MAX_FLOWS + 1) * sizeof(uint32_t), 0));
+        if (!ds.h_cp_payload) HIPCHK(hipHostMalloc((void **)&ds.h_cp_payload, c->max_bytes, 0));
+        HIPCHK(hipHostMalloc((void **)&ds.h_cp_totals, 4 * sizeof(uint32_t), 0));
     }
-    if (!c->h_ss_totals) {
+    if (!ds.h_ss_totals) {
         if (!c->d_ss_seg) HIPCHK(hipMalloc(&c->d_ss_seg, (size_t)c->max_pkts * sizeof(rxg_segment)));
         if (!c->d_ss_payload) HIPCHK(hipMalloc(&c->d_ss_payload, c->max_bytes));
         if (!c->d_ss_totals) HIPCHK(hipMalloc(&c->d_ss_totals, 4 * sizeof(uint32_t)));
-        if (!c->h_ss_seg)
-            HIPCHK(hipHostMalloc((void **)&c->h_ss_seg, (size_t)c->max_pkts * sizeof(rxg_segment), 0));
-        if (!c->h_ss_payload) HIPCHK(hipHostMalloc((void **)&c->h_ss_payload, c->max_bytes, 0));
-        HIPCHK(hipHostMalloc((void **)&c->h_ss_totals, 4 * sizeof(uint32_t), 0));
+        if (!ds.h_ss_seg)
+            HIPCHK(hipHostMalloc((void **)&ds.h_ss_seg, (size_t)c->max_pkts * sizeof(rxg_segment), 0));
+        HIPCHK(hipHostMalloc((void **)&ds.h_ss_totals, 4 * sizeof(uint32_t), 0));
     }
-    for (hipEvent_t &e : c->tev)
+    for (hipEvent_t &e : ds.tev)
         if (!e) HIPCHK(hipEventCreate(&e));
-    d->seg = c->h_ss_seg;
     // the TCP payloads of this burst: a free pooled buffer (a hold the caller
-    // can take, rxg_payload_hold), else the context's own one (valid until the
-    // next call only: tcp_payload_ref = -1)
-    if (c->pl_cur >= 0) c->pl[c->pl_cur].refs.fetch_sub(1, std::memory_order_acq_rel);
-    c->pl_cur = -1;
-    for (int k = 0; k < RXG_PAYLOAD_BUFS && c->pl_cur < 0; ++k) {
+    // can take, rxg_payload_hold), else the set's own one (valid until the
+    // set is reused: tcp_payload_ref = -1).  The library's hold on the
+    // buffer of this set's previous burst ends here.
+    if (ds.pl >= 0) c->pl[ds.pl].refs.fetch_sub(1, std::memory_order_acq_rel);
+    ds.pl = -1;
+    for (int k = 0; k < RXG_PAYLOAD_BUFS && ds.pl < 0; ++k) {
         rxg_ctx::pl_buf &b = c->pl[k];
         if (b.refs.load(std::memory_order_acquire) != 0) continue;
         if (!b.h && hipHostMalloc((void **)&b.h, c->max_bytes, 0) != hipSuccess) {
-            b.h = nullptr; // (out of pinned memory: the context's own buffer)
+            b.h = nullptr; // (out of pinned memory: the set's own buffer)
             (void)hipGetLastError();
             break;
         }
         b.refs.store(1, std::memory_order_release);
-        c->pl_cur = k;
+        ds.pl = k;
     }
-    d->tcp_payload_ref = c->pl_cur;
-    d->tcp_payload = c->pl_cur >= 0 ? c->pl[c->pl_cur].h : c->h_ss_payload;
+    if (ds.pl < 0 && !ds.h_ss_payload) HIPCHK(hipHostMalloc((void **)&ds.h_ss_payload, c->max_bytes, 0));
+    d->seg = ds.h_ss_seg;
+    d->tcp_payload_ref = ds.pl;
+    d->tcp_payload = ds.pl >= 0 ? c->pl[ds.pl].h : ds.h_ss_payload;
+    d->set = si + 1;
     if (udp) {
-        d->dgram = c->h_cp_dg;
-        d->first = c->h_cp_first;
-        d->udp_payload = c->h_cp_payload;
-        memset(c->h_cp_first, 0, (nf + 1) * sizeof(uint32_t));
+        d->dgram = ds.h_cp_dg;
+        d->first = ds.h_cp_first;
+        d->udp_payload = ds.h_cp_payload;
+        memset(ds.h_cp_first, 0, (nf + 1) * sizeof(uint32_t));
     }
-    c->dl = rxg_ctx::pending_delivery();
-    c->dl.t0 = t0;
+    ds.on = ds.udp = ds.tcp = false;
+    ds.ticket = 0;
+    ds.t0 = t0;
+    c->dl_next = (si + 1) % RXG_DELIVER_DEPTH;
     if (n == 0) return RXG_OK;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
@@ -1730,11 +1749,11 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
     int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
     if (rc) return rc;
     const double t1 = now_ms();
-    HIPCHK(hipEventRecord(c->tev[0], c->s_h2d));
+    HIPCHK(hipEventRecord(ds.tev[0], c->s_h2d));
     rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->tev[1], c->s_h2d)); // after the copy in
-    HIPCHK(hipEventRecord(c->tev[2], c->stream)); // after K1
+    HIPCHK(hipEventRecord(ds.tev[1], c->s_h2d)); // after the copy in
+    HIPCHK(hipEventRecord(ds.tev[2], c->stream)); // after K1
     // the compactions follow the classify on the context's stream
     if (udp)
         if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_cp_dg,
@@ -1746,35 +1765,36 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
         if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_ss_seg,
                                c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
             return rc;
-    HIPCHK(hipEventRecord(c->tev[3], c->stream)); // after K3 / K4
+    HIPCHK(hipEventRecord(ds.tev[3], c->stream)); // after K3 / K4
     // every result in one round trip: the counts with upper-bound copies of
     // the records (n of each) and payloads (the staged span bounds the sum of
     // the 16-B padded payloads), so no synchronisation sits between the
-    // compactions and their copy out
+    // compactions and their copy out.  The next set's compactions reuse the
+    // device buffers after these copies, in stream order.
     if (udp) {
-        HIPCHK(hipMemcpyAsync(c->h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
+        HIPCHK(hipMemcpyAsync(ds.h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
+        HIPCHK(hipMemcpyAsync(ds.h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->h_cp_dg, c->d_cp_dg, (size_t)n * sizeof(rxg_dgram),
+        HIPCHK(hipMemcpyAsync(ds.h_cp_dg, c->d_cp_dg, (size_t)n * sizeof(rxg_dgram),
                               hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->h_cp_payload, c->d_cp_payload, pos, hipMemcpyDeviceToHost,
+        HIPCHK(hipMemcpyAsync(ds.h_cp_payload, c->d_cp_payload, pos, hipMemcpyDeviceToHost,
                               c->stream));
     }
     if (tcp) {
-        HIPCHK(hipMemcpyAsync(c->h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
+        HIPCHK(hipMemcpyAsync(ds.h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
+        HIPCHK(hipMemcpyAsync(ds.h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
                               hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
                               hipMemcpyDeviceToHost, c->stream));
     }
-    HIPCHK(hipEventRecord(c->tev[4], c->stream)); // after the results' copy out
-    c->dl.on = true;
-    c->dl.udp = udp;
-    c->dl.tcp = tcp;
-    c->dl.ticket = t;
-    c->dl.t1 = t1;
+    HIPCHK(hipEventRecord(ds.tev[4], c->stream)); // after the results' copy out
+    ds.on = true;
+    ds.udp = udp;
+    ds.tcp = tcp;
+    ds.ticket = t;
+    ds.t1 = t1;
     return RXG_OK;
 }
 
@@ -1784,21 +1804,23 @@ int rxg_deliver_wait(rxg_ctx *c, rxg_delivery *d, float ms[8]) {
     if (!c || !d) return RXG_EINVAL;
     if (ms) memset(ms, 0, 8 * sizeof(float));
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (!c->dl.on) return RXG_OK; // (an empty burst: nothing in flight)
-    c->dl.on = false;
+    if (d->set < 1 || d->set > RXG_DELIVER_DEPTH) return RXG_EINVAL;
+    rxg_ctx::delivery_set &ds = c->dls[d->set - 1];
+    if (!ds.on) return RXG_OK; // (an empty burst, or waited for already)
+    ds.on = false;
     DEVGUARD(c);
-    HIPCHK(hipEventSynchronize(c->tev[4]));
-    int rc = rxg_wait(c, c->dl.ticket); // (the verdicts' copy out, on s_d2h)
+    HIPCHK(hipEventSynchronize(ds.tev[4]));
+    int rc = rxg_wait(c, ds.ticket); // (the verdicts' copy out, on s_d2h)
     if (rc) return rc;
-    const bool udp = c->dl.udp, tcp = c->dl.tcp;
-    if ((udp && c->h_cp_totals[2]) || (tcp && c->h_ss_totals[2]))
+    const bool udp = ds.udp, tcp = ds.tcp;
+    if ((udp && ds.h_cp_totals[2]) || (tcp && ds.h_ss_totals[2]))
         return RXG_ERANGE; // (not reached: staging bounds the payloads)
-    if (udp) d->ndgram = c->h_cp_totals[0], d->udp_bytes = c->h_cp_totals[1];
-    if (tcp) d->nseg = c->h_ss_totals[0], d->tcp_bytes = c->h_ss_totals[1];
+    if (udp) d->ndgram = ds.h_cp_totals[0], d->udp_bytes = ds.h_cp_totals[1];
+    if (tcp) d->nseg = ds.h_ss_totals[0], d->tcp_bytes = ds.h_ss_totals[1];
     if (ms) {
-        ms[0] = (float)(c->dl.t1 - c->dl.t0);
-        for (int k = 0; k < 4; ++k) HIPCHK(hipEventElapsedTime(&ms[k + 1], c->tev[k], c->tev[k + 1]));
-        ms[5] = (float)(now_ms() - c->dl.t0);
+        ms[0] = (float)(ds.t1 - ds.t0);
+        for (int k = 0; k < 4; ++k) HIPCHK(hipEventElapsedTime(&ms[k + 1], ds.tev[k], ds.tev[k + 1]));
+        ms[5] = (float)(now_ms() - ds.t0);
     }
     return RXG_OK;
 }
@@ -1807,7 +1829,7 @@ int rxg_process_mbufs_deliver(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_ve
                               rxg_delivery *d, float ms[8]) {
     int rc = rxg_deliver_submit(c, m, n, out, d);
     if (rc) {
-        if (c) c->dl.on = false;
+        if (c && d && d->set) c->dls[d->set - 1].on = false;
         if (ms) memset(ms, 0, 8 * sizeof(float));
         return rc;
     }

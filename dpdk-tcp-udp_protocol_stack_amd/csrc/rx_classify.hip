@@ -2639,6 +2639,8 @@ static const variant_entry k_variants[] = {
     // 68 / 69: 67 / 66 with partial-chunk sums in the stream (48-B heads:
     // 68 fits 6 blocks per CU)
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},
+    // 70: 64 with 4-KiB tiles
+    {0, 1, 1, 70, launch_sh<0, 4, SH_MAPC, false, 1>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2664,10 +2666,11 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 4-6, r02m, r02o)
         *g = 1, *p = 4, *fpg = 1, *pipe = 14;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
-        // out of the block stream and a four-slot first probe window (SH, pipe 64): 1.2704 vs
-        // 1.3417 ms for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716
-        // on another (counts on, interleaved sweeps, profiles/r02ab)
-        *g = 0, *p = 0, *fpg = 0, *pipe = 64;
+        // out of the block stream and a four-slot first probe window (SH): 1.2704 vs 1.3417 ms
+        // for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716 on
+        // another (counts on, interleaved sweeps, profiles/r02ab); 8-KiB stream tiles (pipe 67)
+        // instead of 16: 1.0586 vs 1.1364 and 1.1590 vs 1.1997 ms (profiles/r04b)
+        *g = 0, *p = 0, *fpg = 0, *pipe = 67;
     } else if (len_hint <= 1536) { // cfg3: 1500 B.  Write-through verdict stores (pipe 40):
         // 1.0191 vs 1.0322 ms for pipe 0 (interleaved sweep, profiles/r03c/sweep_cfg3_wt.txt),
         // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt)
@@ -2689,6 +2692,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
+    case 70:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";

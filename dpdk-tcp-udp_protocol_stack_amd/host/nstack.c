@@ -13,6 +13,8 @@
 #include <errno.h>
 #include <netinet/in.h>
 #include <pthread.h>
+#include <sched.h>
+#include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -300,6 +302,24 @@ static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 static int g_rx_in_flight;      /* nstack_rx_burst waits for the GPU (g_lock released) */
+/* The protocol thread (rx / tx bursts) takes g_lock ahead of application
+ * loops: a pthread mutex is not fair, and drain_all, which re-takes the lock
+ * chunk after chunk, could otherwise keep the protocol thread out for a whole
+ * pass over the sockets.  g_proto_waiting counts its waits; such loops step
+ * aside (app_yield) before each re-take while it is non-zero. */
+static atomic_int g_proto_waiting;
+static void proto_lock(void) {
+    atomic_fetch_add_explicit(&g_proto_waiting, 1, memory_order_relaxed);
+    pthread_mutex_lock(&g_lock);
+    atomic_fetch_sub_explicit(&g_proto_waiting, 1, memory_order_relaxed);
+}
+static void app_yield(void) {
+    while (atomic_load_explicit(&g_proto_waiting, memory_order_relaxed)) sched_yield();
+}
+/* bursts of at least 2 * g_half_min frames run as two halves in flight
+ * (nstack_set_halves; 0 = never) */
+static uint32_t g_half_min;
+static uint64_t g_stale_parts; /* burst halves delivered against changed lists */
 static int g_udp_done;          /* this burst's UDP datagrams went out as batches */
 
 /* the control block of each stable flow id (NULL: free id).  Blocks are
@@ -1590,9 +1610,16 @@ static double mono_ms(void) {
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
+int nstack_set_halves(uint32_t min_half) {
+    pthread_mutex_lock(&g_lock);
+    g_half_min = min_half;
+    pthread_mutex_unlock(&g_lock);
+    return RXG_OK;
+}
+
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
-    pthread_mutex_lock(&g_lock);
+    proto_lock();
     const double t0 = mono_ms();
     /* one protocol thread (the reference's pkt_process lcore): a second
      * rx_burst while one waits for the GPU is refused */
@@ -1600,55 +1627,80 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
     if (rc == RXG_OK && grow((void **)&s_handled, &s_handled_cap, n ? n : 1, 1)) rc = RXG_ENOMEM;
-    rxg_delivery d;
-    float gms[8] = {0};
-    /* the device half of delivery in one pass: classify, UDP payloads grouped
-     * per socket (<= RXG_COMPACT_MAX_FLOWS ids: always, with the reference's
-     * 1024 descriptors), TCP segments sorted per connection with their
-     * payloads gathered.  While it runs on the GPU the stack's lock is free:
-     * the application's socket calls proceed (the reference's app lcore runs
-     * beside its protocol lcore).  If they changed the blocks meanwhile, the
-     * burst is delivered like verdicts of an older snapshot: frame by frame,
-     * every lookup made again on the live lists. */
+    /* the device half of delivery: classify, UDP payloads grouped per socket
+     * (<= RXG_COMPACT_MAX_FLOWS ids: always, with the reference's 1024
+     * descriptors), TCP segments sorted per connection with their payloads
+     * gathered.  While it runs on the GPU the stack's lock is free: the
+     * application's socket calls proceed (the reference's app lcore runs
+     * beside its protocol lcore).  If the blocks changed meanwhile — by those
+     * calls, or by the first half's own segments (a SYN, a last ACK) — a half
+     * is delivered like verdicts of an older snapshot: frame by frame, every
+     * lookup made again on the live lists, which is the reference's sequential
+     * outcome. */
+    const uint32_t nh = g_half_min && n >= 2 * g_half_min ? n / 2 : n;
+    const uint32_t part_off[2] = {0, nh}, part_n[2] = {nh, n - nh};
+    const int parts = nh < n ? 2 : 1;
+    rxg_delivery d[2];
+    float gms[2][8];
+    memset(gms, 0, sizeof(gms));
+    int nsub = 0;
     const uint64_t gen0 = g_snap_gen;
-    if (rc == RXG_OK) rc = rxg_deliver_submit(g_ctx, m, n, s_v, &d);
-    if (rc == RXG_OK) {
-        rxg_ctx *ctx = g_ctx;
-        g_rx_in_flight = 1;
-        pthread_mutex_unlock(&g_lock);
-        rc = rxg_deliver_wait(ctx, &d, gms);
-        pthread_mutex_lock(&g_lock);
-        g_rx_in_flight = 0;
+    double lib_ms = 0;
+    for (int h = 0; rc == RXG_OK && h < parts; h++) {
+        const double a = mono_ms();
+        rc = rxg_deliver_submit(g_ctx, m + part_off[h], part_n[h], s_v + part_off[h], &d[h]);
+        lib_ms += mono_ms() - a;
+        if (rc == RXG_OK) nsub = h + 1;
     }
+    rxg_ctx *ctx = g_ctx;
     int delivered = 0;
-    if (rc == RXG_OK) {
+    double ph[3] = {0, 0, 0};
+    if (nsub) g_rx_in_flight = 1;
+    for (int h = 0; h < nsub; h++) { /* every submitted half is waited for */
+        const uint32_t o = part_off[h], k = part_n[h];
+        pthread_mutex_unlock(&g_lock);
+        const double a = mono_ms();
+        const int wrc = rxg_deliver_wait(ctx, &d[h], gms[h]);
+        lib_ms += mono_ms() - a;
+        proto_lock();
+        if (rc == RXG_OK) rc = wrc;
+        if (rc != RXG_OK) continue;
         const double t1 = mono_ms();
-        if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
+        int *rco = rc_out ? rc_out + o : NULL;
         g_burst_mutated = 0;
         g_burst_stale = gen0 != g_snap_gen;
-        if (g_burst_stale) d.first = NULL, d.nseg = 0; /* (ids may name other blocks now) */
-        if (d.first) {
-            delivered = deliver_udp_batches(m, d.dgram, d.first, d.udp_payload,
-                                            rxg_num_udp_ids(g_ctx));
+        if (g_burst_stale) { /* (ids may name other blocks now) */
+            d[h].first = NULL, d[h].nseg = 0;
+            g_stale_parts++;
+        }
+        if (d[h].first) {
+            delivered += deliver_udp_batches(m + o, d[h].dgram, d[h].first, d[h].udp_payload,
+                                             rxg_num_udp_ids(g_ctx));
             g_udp_done = 1; /* the per-frame loop leaves UDP alone */
         }
         const double t2 = mono_ms();
-        memset(s_handled, 0, n);
-        if (d.nseg)
-            deliver_tcp_sorted(d.seg, d.nseg, d.tcp_payload, d.tcp_payload_ref, m, s_handled,
-                               rc_out);
+        memset(s_handled + o, 0, k);
+        if (d[h].nseg)
+            deliver_tcp_sorted(d[h].seg, d[h].nseg, d[h].tcp_payload, d[h].tcp_payload_ref, m + o,
+                               s_handled + o, rco);
         const double t3 = mono_ms();
-        delivered += deliver_burst(m, n, s_v, rc_out, s_handled);
+        delivered += deliver_burst(m + o, k, s_v + o, rco, s_handled + o);
         g_udp_done = 0;
         g_burst_stale = 0;
         const double t4 = mono_ms();
-        for (int k = 0; k < 6; k++) g_phase_ms[k] = gms[k];
-        g_phase_ms[6] = (float)(t2 - t1); /* UDP batches to the sockets */
-        g_phase_ms[7] = (float)(t3 - t2); /* TCP connections from the segment sort */
-        g_phase_ms[8] = (float)(t4 - t3); /* the frame-by-frame loop (the rest) */
-        g_phase_ms[9] = (float)(t4 - t0); /* the whole call */
-        g_phase_ms[10] = (float)d.nseg;
-        g_phase_ms[11] = (float)d.ndgram;
+        ph[0] += t2 - t1, ph[1] += t3 - t2, ph[2] += t4 - t3;
+    }
+    g_rx_in_flight = 0;
+    if (rc == RXG_OK) {
+        if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
+        for (int j = 0; j < 5; j++) g_phase_ms[j] = gms[0][j] + gms[1][j];
+        g_phase_ms[5] = (float)lib_ms;   /* the library calls (host clock) */
+        g_phase_ms[6] = (float)ph[0];    /* UDP batches to the sockets */
+        g_phase_ms[7] = (float)ph[1];    /* TCP connections from the segment sort */
+        g_phase_ms[8] = (float)ph[2];    /* the frame-by-frame loop (the rest) */
+        g_phase_ms[9] = (float)(mono_ms() - t0); /* the whole call */
+        g_phase_ms[10] = (float)(d[0].nseg + (nsub > 1 ? d[1].nseg : 0));
+        g_phase_ms[11] = (float)(d[0].ndgram + (nsub > 1 ? d[1].ndgram : 0));
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
@@ -1769,6 +1821,7 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
     for (int kind = 0; kind < 2; kind++) {
         uint32_t id = 0;
         for (;;) {
+            app_yield();
             pthread_mutex_lock(&g_lock);
             const uint32_t ncap = kind ? s_tcb_cap : s_udp_cap;
             if (id >= ncap) {
@@ -1963,7 +2016,7 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
                     uint32_t max_frames, int cksum, uint64_t *span) {
     if (span) *span = 0;
     if (!pkts || !off || !len) return max_frames ? RXG_EINVAL : 0;
-    pthread_mutex_lock(&g_lock);
+    proto_lock();
     uint32_t n = 0;
     uint64_t pos = 0;
     int full = 0;
@@ -2057,9 +2110,9 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
 }
 
 uint64_t nstack_stat(int which) {
-    if (which < 0 || which > 4) return 0;
+    if (which < 0 || which > 5) return 0;
     pthread_mutex_lock(&g_lock);
-    uint64_t v = g_stat[which];
+    uint64_t v = which == 5 ? g_stale_parts : g_stat[which];
     pthread_mutex_unlock(&g_lock);
     return v;
 }

@@ -70,7 +70,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
                    (0, 0, 0, 60),  # heads taken out of the block stream
                    (0, 0, 0, 63), (0, 0, 0, 64),  # 60 with a 2 / 4-slot probe window
-                   (0, 0, 0, 66), (0, 0, 0, 67),  # 64 with 12-KiB / 8-KiB tiles
+                   (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 70),  # 64 with 12 / 8 / 4-KiB tiles
                    (0, 0, 0, 68), (0, 0, 0, 69),  # 67 / 66 with partial-chunk sums in the stream
                    (0, 0, 0, 65), (0, 0, 0, 61), (0, 0, 0, 62)]  # probes inside the stream (LDS-DMA)
 
@@ -117,7 +117,7 @@ class Delivery(C.Structure):
     _fields_ = [("dgram", C.c_void_p), ("first", C.c_void_p), ("udp_payload", C.c_void_p),
                 ("ndgram", C.c_uint32), ("nseg", C.c_uint32), ("udp_bytes", C.c_uint64),
                 ("seg", C.c_void_p), ("tcp_payload", C.c_void_p), ("tcp_bytes", C.c_uint64),
-                ("tcp_payload_ref", C.c_int32), ("_pad", C.c_uint32)]
+                ("tcp_payload_ref", C.c_int32), ("set", C.c_uint32)]
 
 
 class GenCfg(C.Structure):
@@ -168,6 +168,8 @@ _flows_rebuilds = _sig("rxg_flows_rebuilds", _u32, _vp)
 _tcp_compact_dev = _sig("rxg_tcp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp,
                         _u64, _vp, _vp)
 _process_mbufs_deliver = _sig("rxg_process_mbufs_deliver", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
+_deliver_submit = _sig("rxg_deliver_submit", _i32, _vp, _vp, _u32, _vp, _vp)
+_deliver_wait = _sig("rxg_deliver_wait", _i32, _vp, _vp, _vp)
 _register_host = _sig("rxg_register_host", _i32, _vp, _vp, _u64)
 _payload_hold = _sig("rxg_payload_hold", _i32, _vp, _i32)
 _payload_release = _sig("rxg_payload_release", _i32, _vp, _i32)
@@ -230,6 +232,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp", "rxg_tcp_compact_dev", "rxg_process_mbufs_deliver",
+            "rxg_deliver_submit", "rxg_deliver_wait",
             "rxg_register_host", "rxg_unregister_host", "rxg_payload_hold", "rxg_payload_release",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
@@ -486,7 +489,9 @@ class Context:
         ms = (C.c_float * 8)()
         _check(_process_mbufs_deliver(self._h, C.cast(arr, _vp), len(mbufs), _ptr(out),
                                       C.byref(d), ms), "rxg_process_mbufs_deliver")
+        return self._delivery_results(out, d, ms)
 
+    def _delivery_results(self, out, d, ms):
         def grab(ptr, nbytes, dtype):
             if not ptr or nbytes == 0:
                 return np.zeros(0, dtype)
@@ -498,6 +503,23 @@ class Context:
         seg = grab(d.seg, d.nseg * 32, SEGMENT_DTYPE)
         tp = grab(d.tcp_payload, d.tcp_bytes, np.uint8)
         return out, dg, first, up, seg, tp, list(ms)
+
+    def deliver_submit(self, mbufs):
+        """rxg_deliver_submit: a handle for deliver_wait (keeps the arrays alive)"""
+        if not isinstance(mbufs, C.Array):
+            mbufs = (C.POINTER(Mbuf) * len(mbufs))(*[C.pointer(m) for m in mbufs])
+        out = np.zeros(len(mbufs), VERDICT_DTYPE)
+        d = Delivery()
+        _check(_deliver_submit(self._h, C.cast(mbufs, _vp), len(mbufs), _ptr(out), C.byref(d)),
+               "rxg_deliver_submit")
+        return (mbufs, out, d)
+
+    def deliver_wait(self, handle):
+        """rxg_deliver_wait: the results as process_mbufs_deliver returns them"""
+        _, out, d = handle
+        ms = (C.c_float * 8)()
+        _check(_deliver_wait(self._h, C.byref(d), ms), "rxg_deliver_wait")
+        return self._delivery_results(out, d, ms)
 
     def tx_cksum(self, pkts: np.ndarray, off: np.ndarray, lens: np.ndarray,
                  off_unit_log2: int) -> np.ndarray:
@@ -743,6 +765,7 @@ class NStack:
                    ("nstack_lookup_tcp", _u32, [_u32, _u32, _u16, _u16]),
                    ("nstack_ctx", _vp, []),
                    ("nstack_register_host", _i32, [_vp, _u64]),
+                   ("nstack_set_halves", _i32, [_u32]),
                    ("nstack_stat", _u64, [_i32]),
                    ("nstack_set_local", _i32, [_u32, _vp]),
                    ("nstack_arp_insert", _i32, [_u32, _vp]),
@@ -827,6 +850,10 @@ class NStack:
     def lookup_tcp(self, sip: int, dip: int, sport: int, dport: int) -> int:
         """the flow id the library's tables give a TCP 4-tuple (raw), listener included"""
         return self.lib.nstack_lookup_tcp(sip, dip, sport, dport)
+
+    def set_halves(self, min_half: int):
+        """nstack_set_halves: bursts of >= 2 * min_half frames as two halves in flight (0 = off)"""
+        _check(self.lib.nstack_set_halves(min_half), "nstack_set_halves")
 
     def register_host(self, ptr: int, nbytes: int):
         """nstack_register_host: frames in this memory are pulled by the GPU"""

@@ -73,7 +73,8 @@ ssize_t nsendto(int sockfd, const void *buf, size_t len, int flags, const struct
 int nclose(int fd);
 
 /* Receive burst: the loop body of pkt_process (netfamily.c:152-200) for n
- * frames at once.  rc_out[i] (nullable) = what udp_process/tcp_process would
+ * frames at once (as two halves in flight together, see nstack_set_halves;
+ * the outcome is the same).  rc_out[i] (nullable) = what udp_process/tcp_process would
  * have returned (KNI frames: 1); v_out (nullable) = the verdicts.
  * Returns the number of UDP datagrams delivered, or a negative RXG_E* code.
  * Called by one protocol thread, which also runs nstack_tx_burst (as
@@ -158,23 +159,35 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * the receive buffer each call uses.  Returns the datagrams + fragments
  * received (EOF fragments are read and not counted, as oracle_drain_all does;
  * a negative RXG_E* code on error); *bytes = the bytes the calls returned.
- * Holds the stack's lock for the whole walk (a concurrent nstack_rx_burst
- * waits for it), so no block it reads can be freed under it. */
+ * Takes the stack's lock per chunk of 64 blocks, stepping aside between
+ * chunks while the protocol thread waits for it, so no block it reads can be
+ * freed under it and a concurrent nstack_rx_burst is not held up for a
+ * whole pass. */
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
 
 /* Where the last nstack_rx_burst's time went, in ms: [0] gather of the mbufs
  * into pinned staging (host), [1] copy in, [2] classify (K1), [3] UDP
  * compaction + TCP segment sort (K3 + K4), [4] copy out of their results
- * (device, HIP events), [5] the library call as a whole (host clock), then
- * host delivery: [6] UDP batches to the sockets, [7] TCP connections from
- * the segment sort, [8] the frame-by-frame loop over the rest, [9] the whole
- * nstack_rx_burst; [10] segments sorted, [11] datagrams compacted. */
+ * (device, HIP events), [5] the library calls (submit + wait, host clock),
+ * then host delivery: [6] UDP batches to the sockets, [7] TCP connections
+ * from the segment sort, [8] the frame-by-frame loop over the rest, [9] the
+ * whole nstack_rx_burst; [10] segments sorted, [11] datagrams compacted.  A
+ * burst run as two halves adds up both halves' phases, so [1]-[4] may exceed
+ * the wall time they took. */
 int nstack_last_burst_phases(float ms[12]);
+/* Bursts of at least 2 * min_half frames run as two halves, both on the GPU
+ * at once (rxg_deliver_submit twice: the second half's copy in overlaps the
+ * first half's copy out, and the host delivers the first half while the
+ * second is on the GPU); 0 (the default) = never.  Measured on MI355X: no
+ * gain for 16K-32K-frame bursts, hence off. */
+int nstack_set_halves(uint32_t min_half);
 
 /* counters: 0 = UDP datagrams delivered, 1 = dropped (a receive ring full),
  * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,
- * 4 = TCP fragments (payload or EOF) queued for nrecv.  Counter 1 also counts
- * TX items dropped (a send ring full, or a datagram too long for a frame). */
+ * 4 = TCP fragments (payload or EOF) queued for nrecv, 5 = bursts (or burst
+ * halves) delivered frame by frame because the lists changed while they were
+ * on the GPU.  Counter 1 also counts TX items dropped (a send ring full, or a
+ * datagram too long for a frame). */
 uint64_t nstack_stat(int which);
 
 #ifdef __cplusplus

@@ -388,7 +388,8 @@ int rxg_tcp_compact_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_o
  * most RXG_COMPACT_MAX_FLOWS; else dgram/first are NULL and ndgram 0) and
  * the TCP segment sort and gather, all in one pass over the staged burst.
  * Verdicts into `out`; the other results stay in pinned buffers the context
- * owns, valid until its next burst call.  `ms` (nullable, 8 floats): the
+ * owns (one set per burst in flight, RXG_DELIVER_DEPTH sets used in turn),
+ * valid until the set is reused: RXG_DELIVER_DEPTH delivery calls later.  `ms` (nullable, 8 floats): the
  * phases of this burst in ms — [0] host gather of the mbufs into pinned
  * staging; from HIP events on the device: [1] copy in, [2] classify (K1),
  * [3] the compactions (K3 + K4), [4] copy out of their results; [5] the
@@ -404,10 +405,10 @@ typedef struct rxg_delivery {
     const uint8_t *tcp_payload;
     uint64_t tcp_bytes;
     int32_t tcp_payload_ref;    /* >= 0: tcp_payload is pooled buffer `ref`, which the caller
-                                   may keep past the next call with rxg_payload_hold (and
-                                   must then rxg_payload_release); -1: valid until the next
-                                   call only */
-    uint32_t _pad;
+                                   may keep longer with rxg_payload_hold (and must then
+                                   rxg_payload_release); -1: valid while the set is (above) */
+    uint32_t set;               /* the context's delivery set holding this burst, 1-based
+                                   (written by rxg_deliver_submit, read by rxg_deliver_wait) */
 } rxg_delivery;
 int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
                               rxg_delivery *d, float ms[8]);
@@ -415,8 +416,12 @@ int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_
  * run while the burst is on the GPU: rxg_deliver_submit stages the burst and
  * queues every device step and copy (d gets its buffer pointers), and
  * rxg_deliver_wait(ctx, d, ms) waits for them and fills in d's counts and
- * the phase times.  One delivery burst in flight per context (a second
- * submit is RXG_EINVAL).  Between the two calls the context's control plane
+ * the phase times.  Up to RXG_DELIVER_DEPTH delivery bursts in flight per
+ * context, waited for in any order (a submit while the next set in turn is
+ * still in flight is RXG_EINVAL): burst k+1's frames cross PCIe while burst
+ * k's results come back and the host delivers burst k-1.  The verdicts of a
+ * burst submitted before an earlier one was delivered were classified against
+ * the flow tables of that submit.  Between the calls the context's control plane
  * (rxg_flows_add / remove / update / commit-free changes) may run from another
  * thread: rxg_deliver_wait reads none of the flow-table state; any other call
  * on the context waits for rxg_deliver_wait first. */
@@ -432,6 +437,7 @@ int rxg_deliver_wait(rxg_ctx *ctx, rxg_delivery *d, float ms[8]);
  * the context's own buffer (tcp_payload_ref -1) and must be copied.  Both
  * calls are safe from any thread (atomic counts). */
 #define RXG_PAYLOAD_BUFS 6
+#define RXG_DELIVER_DEPTH 2
 int rxg_payload_hold(rxg_ctx *ctx, int32_t ref);
 int rxg_payload_release(rxg_ctx *ctx, int32_t ref);
 
