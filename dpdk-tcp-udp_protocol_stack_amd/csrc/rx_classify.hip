@@ -1853,8 +1853,10 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 // the capture, from s_cp) into s_psum instead of storing the chunk in head
 // slot 0, so a head takes 48 B of LDS instead of 64 (with 8-KiB tiles the
 // block fits 6 per CU: 26.1 KiB).
+// FPB: frames per block (a multiple of 64; threads past it only stream), so
+// that larger frames still fit the head map (1500 B: 64 frames, 96 KiB).
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false>
+          bool PS = false, int FPB = 256>
 __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1893,8 +1895,9 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
         for (uint32_t i = tid; i < MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
-    const uint64_t p = (uint64_t)blockIdx.x * 256 + tid;
-    const bool valid = p < n;
+    static_assert(FPB % 64 == 0 && FPB <= 256, "whole waves of frames");
+    const uint64_t p = (uint64_t)blockIdx.x * FPB + tid;
+    const bool valid = tid < (uint32_t)FPB && p < n;
     const uint64_t q = valid ? p : 0;
     const uint64_t fpos = (uint64_t)off[q] << unit_log2;
     const int32_t cp = valid ? (int32_t)len[q] : 0;
@@ -2241,11 +2244,13 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         vd.y = (poff & 0xFFFFu) | (plen << 16);
         vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
-        if constexpr ((ABL & 32) != 0) put_count_idx_wave(ft, p, cidx, lane); // (diagnostic order)
+        if constexpr ((ABL & 32) != 0)
+            if (wvu * 64u < (uint32_t)FPB) put_count_idx_wave(ft, p, cidx, lane); // (diagnostic order)
         st_verdict(ft, out, p, vd);
         lane_count(cidx, counts, hist, lds_bins);
     }
-    if constexpr ((ABL & 48) == 0) put_count_idx_wave(ft, p, cidx, lane);
+    if constexpr ((ABL & 48) == 0)
+        if (wvu * 64u < (uint32_t)FPB) put_count_idx_wave(ft, p, cidx, lane); // (waves of frames)
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -2256,17 +2261,17 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
 }
 
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false>
+          bool PS = false, int FPB = 256>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                      const uint32_t *, const uint32_t *) {
-    const uint64_t blocks = ((uint64_t)n + 255) / 256;
+    const uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
         return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
                                               lds_bins, s, nullptr, nullptr);
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2641,6 +2646,12 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},
     // 70: 64 with 4-KiB tiles
     {0, 1, 1, 70, launch_sh<0, 4, SH_MAPC, false, 1>},
+    // 72 / 74 / 76: 67 / 64 / 66 with 64 frames per block (1500-B frames);
+    // 78: 67 with 128 frames per block
+    {0, 1, 1, 72, launch_sh<0, 4, SH_MAPC, false, 2, false, 64>},
+    {0, 1, 1, 74, launch_sh<0, 4, SH_MAPC, false, 4, false, 64>},
+    {0, 1, 1, 76, launch_sh<0, 4, SH_MAPC, false, 3, false, 64>},
+    {0, 1, 1, 78, launch_sh<0, 4, SH_MAPC, false, 2, false, 128>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2692,7 +2703,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70:
+    case 70: case 72: case 74: case 76: case 78:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";
