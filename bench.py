@@ -843,6 +843,30 @@ SOCK_CASES = {
 }
 
 
+def gpu_local_cpus(local):
+    """the CPUs this process may use on the GPU's NUMA node (sysfs), else all
+    of them: (cpus, node)"""
+    aff = sorted(os.sched_getaffinity(0))
+    try:
+        p = torch.cuda.get_device_properties(local)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+        if node >= 0:
+            with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+                cl = f.read().strip()
+            on = set()
+            for part in cl.split(","):
+                a, _, b = part.partition("-")
+                on.update(range(int(a), int(b or a) + 1))
+            loc = [c for c in aff if c in on]
+            if len(loc) >= 2:
+                return loc, node
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        pass
+    return aff, None
+
+
 def socket_api(local, name, budget_s, cores, with_cpu=True):
     """The kept socket API's rate: bursts through
     nstack_rx_burst — GPU classify (rxg_process_mbufs: staging, PCIe, K1) then
@@ -861,6 +885,16 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
     L = "192.168.100.77"
     ns = R.NStack(local, max_burst=B, max_bytes=B * cfg.slot_bytes + 4096)
     res = dict(workload=name, frames_per_burst=B)
+    # the protocol thread (this one) and the application thread on two
+    # neighbouring cores of the GPU's NUMA node, as a DPDK application pins
+    # its lcores (EAL -l): threads left to migrate across the two sockets of
+    # the box paid remote cache-line transfers on every socket ring
+    lcpus, node = gpu_local_cpus(local)
+    pair = (lcpus[0], lcpus[1]) if len(lcpus) >= 2 else None
+    res["lcores"] = dict(cpus=list(pair) if pair else None, numa_node=node)
+    old_aff = os.sched_getaffinity(0)
+    if pair:
+        os.sched_setaffinity(0, {pair[0]})
     try:
         setup = []  # (frames for the handshake), applied to both stacks
         if name == "cfg2":
@@ -942,35 +976,63 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # protocol thread runs the bursts (nstack_rx_burst releases the stack's
         # lock while a burst is on the GPU)
         import threading
-        stop = threading.Event()
-        ov = [0, 0]
 
-        def app_thread():
-            b2 = np.zeros(65536, np.uint8)
-            while not stop.is_set():
+        def overlapped(cpus=None, unpin=False):
+            stop = threading.Event()
+            ov = [0, 0]
+            app_t = [0.0, 0]  # time inside drain_all, passes
+
+            def app_thread():
+                if cpus:
+                    os.sched_setaffinity(0, {cpus[1]})
+                b2 = np.zeros(65536, np.uint8)
+                while not stop.is_set():
+                    a0 = time.perf_counter()
+                    g2, n2 = ns.drain_all(b2)
+                    app_t[0] += time.perf_counter() - a0
+                    app_t[1] += 1
+                    ov[0] += g2
+                    ov[1] += n2
+                    if g2 == 0:  # nothing queued: let the protocol thread take the lock
+                        time.sleep(0.0001)
                 g2, n2 = ns.drain_all(b2)
                 ov[0] += g2
                 ov[1] += n2
-                if g2 == 0:  # nothing queued: let the protocol thread take the lock
-                    time.sleep(0.0001)
-            g2, n2 = ns.drain_all(b2)
-            ov[0] += g2
-            ov[1] += n2
-        d0, s0 = int(ns.stat(1)), int(ns.stat(5))
-        th = threading.Thread(target=app_thread)
-        t0 = time.perf_counter()
-        th.start()
-        for _ in range(K):
-            ns.rx_burst_mbufs(arr, B)
-        stop.set()
-        th.join()
-        t_ov = time.perf_counter() - t0
-        res["overlapped"] = dict(mpps=round(B * K / t_ov / 1e6, 3), ms_per_burst=round(t_ov / K * 1e3, 3),
-                                 received=ov[0], payload_bytes=ov[1],
-                                 received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
-                                 stale_bursts=int(ns.stat(5)) - s0,
-                                 note="application thread draining while the protocol thread runs "
-                                      "the bursts")
+            main_aff = os.sched_getaffinity(0)
+            if cpus:
+                os.sched_setaffinity(0, {cpus[0]})
+            elif unpin:
+                os.sched_setaffinity(0, old_aff)
+            d0, s0 = int(ns.stat(1)), int(ns.stat(5))
+            th = threading.Thread(target=app_thread)
+            t0 = time.perf_counter()
+            th.start()
+            ov_rx, ov_ph = [], []
+            try:
+                for _ in range(K):
+                    a0 = time.perf_counter()
+                    ns.rx_burst_mbufs(arr, B)
+                    ov_rx.append(time.perf_counter() - a0)
+                    ov_ph.append(ns.last_burst_phases())
+            finally:
+                stop.set()
+                th.join()
+                os.sched_setaffinity(0, main_aff)
+            t_ov = time.perf_counter() - t0
+            return dict(mpps=round(B * K / t_ov / 1e6, 3), ms_per_burst=round(t_ov / K * 1e3, 3),
+                        received=ov[0], payload_bytes=ov[1],
+                        received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
+                        stale_bursts=int(ns.stat(5)) - s0,
+                        rx_burst_ms=round(float(np.median(ov_rx)) * 1e3, 3),
+                        rx_burst_phases_ms={k: round(float(np.median([p[k] for p in ov_ph])), 4)
+                                            for k in ov_ph[0]},
+                        app_drain_ms=round(app_t[0] * 1e3 / K, 3), app_passes=app_t[1],
+                        cpus=list(cpus) if cpus else None,
+                        note="application thread draining while the protocol thread runs "
+                             "the bursts" + ("; the two threads on the lcores above" if cpus else
+                                             "; threads not pinned"))
+        res["overlapped"] = overlapped(pair)
+        res["overlapped_unpinned"] = overlapped(None, unpin=True)
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
                    rx_burst_ms=round(t_rx / K * 1e3, 3), app_recv_ms=round(t_dr / K * 1e3, 3),
@@ -981,6 +1043,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                    dropped=int(ns.stat(1)))
     finally:
         ns.fini()
+        os.sched_setaffinity(0, old_aff)
     if with_cpu:  # the reference's path on one core: oracle/ref_stack.c
         O = _oracle()
         st = O.Stack()

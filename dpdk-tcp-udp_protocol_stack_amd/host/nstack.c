@@ -1807,6 +1807,34 @@ static inline void prefetch_next(const struct tcp_fragment *f, struct nring *r) 
     for (uint32_t o = 0; d && o < l; o += 64) __builtin_prefetch(d + o, 0, 0);
 }
 
+/* drain_all's look-ahead over the tcbs it visits next (g_lock held, so none
+ * is freed): the tcb 4 ids ahead, the ring of the one 2 ahead, the front
+ * fragment, its batch's fragment array and first payload lines of the next
+ * one, so the pointer chain a tcb's read walks is in cache when it gets
+ * there (the protocol thread wrote it on another core).  Prefetches only:
+ * the values read to form the addresses may be stale, which costs nothing. */
+static inline void drain_prefetch(uint32_t id, uint32_t end) {
+    if (id + 4 < end && s_tcb_cb[id + 4]) __builtin_prefetch(s_tcb_cb[id + 4], 0, 0);
+    if (id + 2 < end && s_tcb_cb[id + 2] && s_tcb_cb[id + 2]->rcvbuf)
+        __builtin_prefetch(s_tcb_cb[id + 2]->rcvbuf, 0, 0);
+    if (id + 1 >= end || !s_tcb_cb[id + 1]) return;
+    const struct nring *r = s_tcb_cb[id + 1]->rcvbuf;
+    if (!r || !r->count) return;
+    const struct tcp_fragment *it = r->slot[r->head];
+    if (!it) return;
+    __builtin_prefetch(it, 0, 0);
+    const struct frag_batch *b = it->batch;
+    if (b) {
+        const struct tcp_fragment *f = &b->frag[b->next];
+        __builtin_prefetch(f, 0, 0);
+        __builtin_prefetch((const char *)f + 64, 0, 0);
+        if (f->data) {
+            __builtin_prefetch(f->data, 0, 0);
+            __builtin_prefetch(f->data + 64, 0, 0);
+        }
+    }
+}
+
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
     /* The application side of the benchmark: every socket read until empty,
      * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
@@ -1839,6 +1867,7 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
                         got++, nb += (uint64_t)r;
                     continue;
                 }
+                drain_prefetch(id, end);
                 struct tcp_stream *s = s_tcb_cb[id];
                 if (!s) continue;
                 pthread_mutex_lock(&s->mutex);
