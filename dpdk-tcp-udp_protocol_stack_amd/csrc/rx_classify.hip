@@ -1855,8 +1855,9 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 // block fits 6 per CU: 26.1 KiB).
 // FPB: frames per block (a multiple of 64; threads past it only stream), so
 // that larger frames still fit the head map (1500 B: 64 frames, 96 KiB).
+// TT: stream tiles in flight per thread (2, or 3 with a period-3 rotation).
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256>
+          bool PS = false, int FPB = 256, int TT = 2>
 __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -2094,20 +2095,35 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
             }
         }
     };
+    static_assert(TT == 2 || (TT == 3 && !EP), "tiles in flight");
     uint32_t c0 = 0;
-    for (; c0 < span; c0 += 2 * TCH) {
-        tile_load(vb, c0 + TCH);
-        stile(va, c0, 0);
-        tile_load(va, c0 + 2 * TCH);
-        stile(vb, c0 + TCH, 1);
-        ep_issue(c0); // the heads completed in this pair of tiles
+    if constexpr (TT == 3) { // tile t in buffer t & 1, three tiles of loads in flight
+        uint4 vc[LPT];
+        tile_load(vb, TCH);
+        for (; c0 < span; c0 += 3 * TCH) {
+            const uint32_t t0 = c0 / TCH;
+            tile_load(vc, c0 + 2 * TCH);
+            stile(va, c0, t0 & 1u);
+            tile_load(va, c0 + 3 * TCH);
+            stile(vb, c0 + TCH, (t0 + 1u) & 1u);
+            tile_load(vb, c0 + 4 * TCH);
+            stile(vc, c0 + 2 * TCH, t0 & 1u);
+        }
+    } else {
+        for (; c0 < span; c0 += 2 * TCH) {
+            tile_load(vb, c0 + TCH);
+            stile(va, c0, 0);
+            tile_load(va, c0 + 2 * TCH);
+            stile(vb, c0 + TCH, 1);
+            ep_issue(c0); // the heads completed in this pair of tiles
+        }
     }
     __syncthreads(); // the last tile's prefixes and every head slot written
     if constexpr (EP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the windows landed
     if (streamed) {
-        const uint32_t p0 = c0 - TCH;
-        if (cs - p0 < TCH) es = s_pre[1][cs - p0];
-        if (ce - p0 < TCH) ee = s_pre[1][ce - p0];
+        const uint32_t p0 = c0 - TCH, lb = (p0 / TCH) & 1u; // the last tile, its buffer
+        if (cs - p0 < TCH) es = s_pre[lb][cs - p0];
+        if (ce - p0 < TCH) ee = s_pre[lb][ce - p0];
         if (ce == span) ee = carry;
     }
 
@@ -2261,7 +2277,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
 }
 
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256>
+          bool PS = false, int FPB = 256, int TT = 2>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -2271,7 +2287,8 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
         return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
                                               lds_bins, s, nullptr, nullptr);
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT>), dim3((uint32_t)blocks),
+                       dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
     return hipGetLastError();
@@ -2652,6 +2669,10 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 74, launch_sh<0, 4, SH_MAPC, false, 4, false, 64>},
     {0, 1, 1, 76, launch_sh<0, 4, SH_MAPC, false, 3, false, 64>},
     {0, 1, 1, 78, launch_sh<0, 4, SH_MAPC, false, 2, false, 128>},
+    // 71 / 73: 67 / 70 with three tiles in flight; 75: 67 with a two-slot window
+    {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
+    {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
+    {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2703,7 +2724,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70: case 72: case 74: case 76: case 78:
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 78:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";
