@@ -1643,28 +1643,40 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     rxg_delivery d[2];
     float gms[2][8];
     memset(gms, 0, sizeof(gms));
-    int nsub = 0;
+    int sub[2] = {0, 0};
     const uint64_t gen0 = g_snap_gen;
     double lib_ms = 0;
+    /* both halves go out before the first is waited for; a second half the
+     * library refused is submitted again once the first is delivered */
     for (int h = 0; rc == RXG_OK && h < parts; h++) {
         const double a = mono_ms();
-        rc = rxg_deliver_submit(g_ctx, m + part_off[h], part_n[h], s_v + part_off[h], &d[h]);
+        const int src = rxg_deliver_submit(g_ctx, m + part_off[h], part_n[h], s_v + part_off[h], &d[h]);
         lib_ms += mono_ms() - a;
-        if (rc == RXG_OK) nsub = h + 1;
+        if (src == RXG_OK)
+            sub[h] = 1;
+        else if (h == 0)
+            rc = src;
     }
     rxg_ctx *ctx = g_ctx;
     int delivered = 0;
     double ph[3] = {0, 0, 0};
-    if (nsub) g_rx_in_flight = 1;
-    for (int h = 0; h < nsub; h++) { /* every submitted half is waited for */
+    if (sub[0]) g_rx_in_flight = 1;
+    for (int h = 0; h < parts && (sub[h] || rc == RXG_OK); h++) {
         const uint32_t o = part_off[h], k = part_n[h];
+        if (!sub[h]) { /* (the lock is held here) */
+            const double a = mono_ms();
+            rc = rxg_deliver_submit(g_ctx, m + o, k, s_v + o, &d[h]);
+            lib_ms += mono_ms() - a;
+            if (rc != RXG_OK) break;
+            sub[h] = 1;
+        }
         pthread_mutex_unlock(&g_lock);
         const double a = mono_ms();
         const int wrc = rxg_deliver_wait(ctx, &d[h], gms[h]);
         lib_ms += mono_ms() - a;
         proto_lock();
         if (rc == RXG_OK) rc = wrc;
-        if (rc != RXG_OK) continue;
+        if (rc != RXG_OK) continue; /* (a submitted half is still waited for) */
         const double t1 = mono_ms();
         int *rco = rc_out ? rc_out + o : NULL;
         g_burst_mutated = 0;
@@ -1699,8 +1711,8 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         g_phase_ms[7] = (float)ph[1];    /* TCP connections from the segment sort */
         g_phase_ms[8] = (float)ph[2];    /* the frame-by-frame loop (the rest) */
         g_phase_ms[9] = (float)(mono_ms() - t0); /* the whole call */
-        g_phase_ms[10] = (float)(d[0].nseg + (nsub > 1 ? d[1].nseg : 0));
-        g_phase_ms[11] = (float)(d[0].ndgram + (nsub > 1 ? d[1].ndgram : 0));
+        g_phase_ms[10] = (float)(d[0].nseg + (parts > 1 ? d[1].nseg : 0));
+        g_phase_ms[11] = (float)(d[0].ndgram + (parts > 1 ? d[1].ndgram : 0));
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
