@@ -949,27 +949,35 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # delivery steps), median over the bursts
         res["rx_burst_phases_ms"] = {k: round(float(np.median([p[k] for p in phases])), 4)
                                      for k in phases[0]}
+        def ab_run():  # the sequential loop again, for an A/B
+            h_rx = h_dr = 0.0
+            h_items = 0
+            h_ph = []
+            for _ in range(K):
+                t0 = time.perf_counter()
+                ns.rx_burst_mbufs(arr, B)
+                t1 = time.perf_counter()
+                h_ph.append(ns.last_burst_phases())
+                g, _ = ns.drain_all(rbuf)
+                h_rx += t1 - t0
+                h_dr += time.perf_counter() - t1
+                h_items += g
+            return dict(mpps=round(B * K / (h_rx + h_dr) / 1e6, 3),
+                        rx_burst_ms=round(h_rx / K * 1e3, 3), app_recv_ms=round(h_dr / K * 1e3, 3),
+                        received_equal=h_items == items,
+                        rx_burst_phases_ms={k: round(float(np.median([p[k] for p in h_ph])), 4)
+                                            for k in h_ph[0]})
         # A/B: each burst as two halves, both on the GPU at once
         # (nstack_set_halves; off by default)
         ns.set_halves(B // 2)
-        h_rx = h_dr = 0.0
-        h_items = 0
-        h_ph = []
-        for _ in range(K):
-            t0 = time.perf_counter()
-            ns.rx_burst_mbufs(arr, B)
-            t1 = time.perf_counter()
-            h_ph.append(ns.last_burst_phases())
-            g, _ = ns.drain_all(rbuf)
-            h_rx += t1 - t0
-            h_dr += time.perf_counter() - t1
-            h_items += g
+        res["halves"] = ab_run()
         ns.set_halves(0)
-        res["halves"] = dict(mpps=round(B * K / (h_rx + h_dr) / 1e6, 3),
-                             rx_burst_ms=round(h_rx / K * 1e3, 3), app_recv_ms=round(h_dr / K * 1e3, 3),
-                             received_equal=h_items == items,
-                             rx_burst_phases_ms={k: round(float(np.median([p[k] for p in h_ph])), 4)
-                                                 for k in h_ph[0]})
+        # A/B: the registered pool pulled by the device frame by frame instead
+        # of copied as one span (rxg_tune_ingest)
+        if res.get("pool_registered") is True:
+            ns.tune_ingest(R.INGEST_PULL)
+            res["ingest_pull"] = ab_run()
+            ns.tune_ingest(R.INGEST_AUTO)
         # the same bursts with the application on its own thread, as the
         # reference runs it (app lcore beside the protocol lcore,
         # netfamily.c:424-430): the app drains every socket in a loop while the

@@ -181,6 +181,7 @@ struct rxg_ctx {
     rx_track *cur = nullptr; // the stream of the latest burst (its event not yet recorded)
     uint64_t use_clock = 0;
     uint32_t tune_tables = 0; // rxg_tune_tables flags
+    uint32_t tune_ingest = RXG_INGEST_AUTO; // rxg_tune_ingest
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
@@ -1119,6 +1120,12 @@ int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
     return RXG_OK;
 }
 
+int rxg_tune_ingest(rxg_ctx *c, uint32_t mode) {
+    if (!c || mode > RXG_INGEST_GATHER) return RXG_EINVAL;
+    c->tune_ingest = mode;
+    return RXG_OK;
+}
+
 int rxg_tune_flow_load(rxg_ctx *c, uint32_t load_log2) {
     if (!c || load_log2 > 4) return RXG_EINVAL;
     c->fs.load_log2 = load_log2 ? load_log2 : RX_FT_LOAD_LOG2;
@@ -1453,42 +1460,83 @@ static uint8_t *region_dev(rxg_ctx *c, const uint8_t *p, uint64_t bytes) {
     return nullptr;
 }
 
+// how an mbuf burst reaches a staging slot
+struct staged {
+    const uint8_t *src = nullptr; // host bytes copied in by DMA (the pinned gather, or a
+                                  // registered span); nullptr when the device pulls
+    uint64_t span = 0;            // bytes of the slot used
+    uint64_t bound = 0;           // bounds the 16-B padded payloads of the burst (results' copy out)
+    uint32_t ul = 6;              // descriptor unit (log2 bytes)
+    bool pulled = false;          // the device pulls each frame (rx_ingest_launch)
+};
+
 // an mbuf burst whose frames all lie in registered host memory, 16-B aligned:
-// descriptors and device source addresses only (the device pulls the frames,
-// rx_ingest_launch); false (nothing done) otherwise
-static int pull_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n, uint64_t *span,
-                      bool *pulled) {
-    *pulled = false;
-    if (c->regions.empty()) return RXG_OK;
+// descriptors only.  Dense in one region (the covering span at most 1.4x the
+// frames' 16-B rounded bytes, and it fits the slot): one DMA copy of the span,
+// descriptors in 16-B units from its start (the copy engine moves ~55 GB/s,
+// device loads of host memory ~38); else the device pulls frame by frame
+// (device source addresses).  st->src / pulled unset: the host gather takes it.
+static int pull_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n, staged *st) {
+    if (c->regions.empty() || c->tune_ingest == RXG_INGEST_GATHER) return RXG_OK;
+    if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_*
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    uint64_t dense = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
+        const uintptr_t f = (uintptr_t)m[i]->buf_addr + m[i]->data_off;
+        const uint64_t l16 = (m[i]->data_len + 15ull) & ~15ull;
+        if ((f & 15u) || !region_dev(c, (const uint8_t *)f, l16)) return RXG_OK; // (host gather)
+        lo = std::min(lo, f);
+        hi = std::max<uintptr_t>(hi, f + l16);
+        dense += l16;
+    }
+    if (n == 0) return RXG_OK;
+    const uint64_t span = hi - lo;
+    if (c->tune_ingest != RXG_INGEST_PULL && span <= c->max_bytes && span <= dense + dense / 5 * 2 &&
+        span >> 4 <= 0xFFFFFFFFull && region_dev(c, (const uint8_t *)lo, span)) {
+        // 64-B units when every frame sits on a 64-B boundary from the span's
+        // start (mbuf data rooms usually do), else 16-B units
+        uintptr_t mis = 0;
+        for (uint32_t i = 0; i < n; ++i) mis |= (uintptr_t)m[i]->buf_addr + m[i]->data_off - lo;
+        const uint32_t ul = (mis & 63u) ? 4u : 6u;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uintptr_t f = (uintptr_t)m[i]->buf_addr + m[i]->data_off;
+            sl.h_off[i] = (uint32_t)((f - lo) >> ul);
+            sl.h_len[i] = (uint16_t)m[i]->data_len;
+        }
+        st->src = (const uint8_t *)lo;
+        st->span = span;
+        st->bound = std::min<uint64_t>(std::max(span, dense), c->max_bytes); // (frames may overlap)
+        st->ul = ul;
+        return RXG_OK;
+    }
     if (!sl.h_src) {
         HIPCHK(hipMalloc(&sl.d_src, (size_t)c->max_pkts * 8));
         HIPCHK(hipHostMalloc((void **)&sl.h_src, (size_t)c->max_pkts * 8, 0));
     }
-    if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_src
     uint64_t pos = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
         const uint8_t *f = (const uint8_t *)m[i]->buf_addr + m[i]->data_off;
         const uint32_t l = m[i]->data_len;
-        uint8_t *d = ((uintptr_t)f & 15u) ? nullptr : region_dev(c, f, (l + 15ull) & ~15ull);
-        if (!d) return RXG_OK; // (the host gather takes the burst)
         const uint64_t step = std::max<uint64_t>((l + 63ull) & ~63ull, 64);
         if (pos + step > c->max_bytes) return RXG_ERANGE;
-        sl.h_src[i] = (unsigned long long)(uintptr_t)d;
+        sl.h_src[i] = (unsigned long long)(uintptr_t)region_dev(c, f, (l + 15ull) & ~15ull);
         sl.h_off[i] = (uint32_t)(pos >> 6);
         sl.h_len[i] = (uint16_t)l;
         pos += step;
     }
-    *span = pos;
-    *pulled = true;
+    st->span = st->bound = pos;
+    st->ul = 6;
+    st->pulled = true;
     return RXG_OK;
 }
 
-static int gather_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n,
-                        uint64_t *span, bool *pulled = nullptr) {
-    if (pulled) {
-        int rc = pull_mbufs(c, sl, m, n, span, pulled);
-        if (rc || *pulled) return rc;
+static int gather_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n, staged *st,
+                        bool registered) {
+    *st = staged();
+    if (registered) {
+        int rc = pull_mbufs(c, sl, m, n, st);
+        if (rc || st->pulled || st->src) return rc;
     }
     if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_stage
     uint64_t pos = 0;
@@ -1503,7 +1551,9 @@ static int gather_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint3
         sl.h_len[i] = (uint16_t)l;
         pos += step;
     }
-    *span = pos;
+    st->src = sl.h_stage;
+    st->span = st->bound = pos;
+    st->ul = 6;
     return RXG_OK;
 }
 
@@ -1516,11 +1566,10 @@ int rxg_process_mbufs(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *o
     DEVGUARD(c);
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
-    uint64_t pos = 0;
-    bool pulled = false;
-    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
+    staged st;
+    int rc = gather_mbufs(c, sl, m, n, &st, true);
     if (rc) return rc;
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
+    rc = submit_slot(c, sl, st.src, st.span, sl.h_off, sl.h_len, n, st.ul, out, t, st.pulled);
     return rc ? rc : rxg_wait(c, t);
 }
 
@@ -1592,15 +1641,14 @@ int rxg_process_mbufs_udp(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdic
     if (n == 0) return RXG_OK;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
-    uint64_t pos = 0;
-    bool pulled = false;
-    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
+    staged st;
+    int rc = gather_mbufs(c, sl, m, n, &st, true);
     if (rc) return rc;
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
+    rc = submit_slot(c, sl, st.src, st.span, sl.h_off, sl.h_len, n, st.ul, out, t, st.pulled);
     if (rc) return rc;
     // the compaction follows the classify on the context's stream (its inputs:
     // the staged frames and the device verdicts of this slot)
-    rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_cp_dg, c->d_cp_first,
+    rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_cp_dg, c->d_cp_first,
                       c->d_cp_payload, c->max_bytes, c->d_cp_totals, c->stream);
     if (rc) return rc;
     if (nf) {
@@ -1744,25 +1792,25 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
     if (n == 0) return RXG_OK;
     const uint64_t t = c->next_ticket++;
     rxg_ctx::slot &sl = c->slots[t % RXG_PIPE_DEPTH];
-    uint64_t pos = 0;
-    bool pulled = false;
-    int rc = gather_mbufs(c, sl, m, n, &pos, &pulled);
+    staged st;
+    int rc = gather_mbufs(c, sl, m, n, &st, true);
     if (rc) return rc;
+    const uint64_t pos = st.bound;
     const double t1 = now_ms();
     HIPCHK(hipEventRecord(ds.tev[0], c->s_h2d));
-    rc = submit_slot(c, sl, sl.h_stage, pos, sl.h_off, sl.h_len, n, 6, out, t, pulled);
+    rc = submit_slot(c, sl, st.src, st.span, sl.h_off, sl.h_len, n, st.ul, out, t, st.pulled);
     if (rc) return rc;
     HIPCHK(hipEventRecord(ds.tev[1], c->s_h2d)); // after the copy in
     HIPCHK(hipEventRecord(ds.tev[2], c->stream)); // after K1
     // the compactions follow the classify on the context's stream
     if (udp)
-        if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_cp_dg,
+        if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_cp_dg,
                                c->d_cp_first, c->d_cp_payload, c->max_bytes, c->d_cp_totals,
                                c->stream)))
             return rc;
     const bool tcp = c->fs.tcp.id_space() > 0;
     if (tcp)
-        if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, 6, sl.d_out, c->d_ss_seg,
+        if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_ss_seg,
                                c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
             return rc;
     HIPCHK(hipEventRecord(ds.tev[3], c->stream)); // after K3 / K4

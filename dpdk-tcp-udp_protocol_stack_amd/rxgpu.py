@@ -171,6 +171,8 @@ _tcp_compact_dev = _sig("rxg_tcp_compact_dev", _i32, _vp, _vp, _vp, _vp, _u32, _
                         _u64, _vp, _vp)
 _process_mbufs_deliver = _sig("rxg_process_mbufs_deliver", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
 _deliver_submit = _sig("rxg_deliver_submit", _i32, _vp, _vp, _u32, _vp, _vp)
+_tune_ingest = _sig("rxg_tune_ingest", _i32, _vp, _u32)
+INGEST_AUTO, INGEST_PULL, INGEST_GATHER = 0, 1, 2
 _deliver_wait = _sig("rxg_deliver_wait", _i32, _vp, _vp, _vp)
 _register_host = _sig("rxg_register_host", _i32, _vp, _vp, _u64)
 _payload_hold = _sig("rxg_payload_hold", _i32, _vp, _i32)
@@ -234,7 +236,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_flows_add", "rxg_flows_remove", "rxg_flows_update_udp", "rxg_flows_update_tcb",
             "rxg_flows_commit", "rxg_num_udp_ids", "rxg_flows_rebuilds", "rxg_udp_compact_dev",
             "rxg_process_mbufs_udp", "rxg_tcp_compact_dev", "rxg_process_mbufs_deliver",
-            "rxg_deliver_submit", "rxg_deliver_wait",
+            "rxg_deliver_submit", "rxg_deliver_wait", "rxg_tune_ingest",
             "rxg_register_host", "rxg_unregister_host", "rxg_payload_hold", "rxg_payload_release",
             "rxg_classify_dev", "rxg_classify_dev_cs", "rxg_classify_dev8", "rxg_classify", "rxg_classify_span", "rxg_process_mbufs", "rxg_flow_counts",
             "rxg_counts_reset", "rxg_num_flows", "rxg_tune", "rxg_kernel_variant", "rxg_tune_grid", "rxg_tune_tx", "rxg_tune_flow_load", "rxg_tune_tables", "rxg_ft_lookup_udp", "rxg_ft_lookup_tcp", "rxg_ft_dump",
@@ -505,6 +507,10 @@ class Context:
         seg = grab(d.seg, d.nseg * 32, SEGMENT_DTYPE)
         tp = grab(d.tcp_payload, d.tcp_bytes, np.uint8)
         return out, dg, first, up, seg, tp, list(ms)
+
+    def tune_ingest(self, mode: int):
+        """rxg_tune_ingest: INGEST_AUTO / INGEST_PULL / INGEST_GATHER"""
+        _check(_tune_ingest(self._h, mode), "rxg_tune_ingest")
 
     def deliver_submit(self, mbufs):
         """rxg_deliver_submit: a handle for deliver_wait (keeps the arrays alive)"""
@@ -852,6 +858,10 @@ class NStack:
     def lookup_tcp(self, sip: int, dip: int, sport: int, dport: int) -> int:
         """the flow id the library's tables give a TCP 4-tuple (raw), listener included"""
         return self.lib.nstack_lookup_tcp(sip, dip, sport, dport)
+
+    def tune_ingest(self, mode: int):
+        """rxg_tune_ingest on the stack's context (INGEST_AUTO / _PULL / _GATHER)"""
+        _check(_tune_ingest(self.lib.nstack_ctx(), mode), "rxg_tune_ingest")
 
     def set_halves(self, min_half: int):
         """nstack_set_halves: bursts of >= 2 * min_half frames as two halves in flight (0 = off)"""

@@ -502,6 +502,20 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
 
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 
+/* Tuning hook: how mbuf bursts whose frames lie in registered memory
+ * (rxg_register_host) reach the GPU.  RXG_INGEST_AUTO (the default): a burst
+ * dense in one region (its covering span at most 1.4x its frames' bytes and
+ * within the staging slot) is copied as that one span by the copy engine,
+ * any other registered burst is pulled by the device frame by frame;
+ * RXG_INGEST_PULL: always pulled; RXG_INGEST_GATHER: always gathered on the
+ * host.  Outputs do not depend on it.  In both registered forms the frames
+ * are read after the call returns: they must stay in place until the burst
+ * is waited for (rxg_deliver_wait; the synchronous calls return after it). */
+#define RXG_INGEST_AUTO 0u
+#define RXG_INGEST_PULL 1u
+#define RXG_INGEST_GATHER 2u
+int rxg_tune_ingest(rxg_ctx *ctx, uint32_t mode);
+
 /* Context-owned per-flow counts (accumulated by rxg_classify / rxg_process_mbufs). */
 int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);

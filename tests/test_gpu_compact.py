@@ -12,6 +12,8 @@ same grouping (every datagram, every byte), and the whole socket layer
 (nstack_rx_burst -> nrecvfrom) against the delivery oracle
 (oracle/ref_stack.c) on bursts with 1000 sockets, mixed sizes, captures that
 end inside the payload, unknown ports and split reads."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -332,7 +334,10 @@ def test_registered_pool_is_pulled_by_the_device(torch_dev):
         ctx.flows_sync(udp, tcb)
         host = ctx.process_mbufs_deliver(arr)
         ctx.register_host(buf.ctypes.data, buf.nbytes)
-        pulled = ctx.process_mbufs_deliver(arr)
+        pulled = ctx.process_mbufs_deliver(arr)  # dense: one span copied (RXG_INGEST_AUTO)
+        ctx.tune_ingest(R.INGEST_PULL)
+        pulled_frames = ctx.process_mbufs_deliver(arr)  # frame by frame by the device
+        ctx.tune_ingest(R.INGEST_AUTO)
         # one frame outside the registered memory: the burst is gathered on the host
         o5 = int(off[5]) << 6
         extra = np.zeros(2048, np.uint8)
@@ -341,7 +346,61 @@ def test_registered_pool_is_pulled_by_the_device(torch_dev):
         mixed = ctx.process_mbufs_deliver(arr)
         ctx.unregister_host(buf.ctypes.data)
     assert host[0].tobytes() == want_v.tobytes()
-    for got in (pulled, mixed):
+    for got in (pulled, pulled_frames, mixed):
         for a, b in zip(host[:6], got[:6]):
             assert (a is None and b is None) or a.tobytes() == b.tobytes()
     assert len(host[4]) > 500 and host[6][1] >= 0
+
+
+@pytest.mark.parametrize("layout", ["dense16", "sparse", "overlap"])
+def test_registered_layouts_match_host_gather(torch_dev, layout):
+    """rxg_tune_ingest's registered forms against the host gather on the same
+    mbufs: frames packed at 16-B (not 64-B) boundaries (one span, 16-B
+    descriptor units), frames 4 KiB apart (sparse: pulled frame by frame), and
+    mbufs sharing data (the span smaller than the frames' bytes: the results
+    copy-out bound); every output equal"""
+    rng = np.random.default_rng({"dense16": 41, "sparse": 42, "overlap": 43}[layout])
+    nsock = 200
+    udp = np.zeros(nsock, R.UDP_SOCK_DTYPE)
+    udp["localip"] = R.ip_raw(L)
+    udp["localport"] = [R.port_raw(30000 + k) for k in range(nsock)]
+    udp["protocol"] = 17
+    tcb = np.zeros(201, R.TCB_DTYPE)
+    tcb[0] = (0, R.ip_raw(L), 0, R.port_raw(9999), R.TCP_STATUS_LISTEN)
+    keys = []
+    for k in range(1, 201):
+        cip, cport = f"10.8.{k >> 8}.{k & 255}", 2000 + k
+        tcb[k] = (R.ip_raw(cip), R.ip_raw(L), R.port_raw(cport), R.port_raw(9999), 4)
+        keys.append((cip, cport))
+    uf, ucaps = _burst(rng, 700, nsock)
+    tf, tcaps = _tcp_burst(rng, 700, keys)
+    frames = [f[:c] for f, c in zip(uf + tf, ucaps + tcaps)]
+    frames = [frames[i] for i in rng.permutation(len(frames))]
+    n = len(frames)
+    stride = 4096 if layout == "sparse" else 0
+    pos, offs = 0, []
+    for f in frames:
+        offs.append(pos)
+        pos += stride or ((len(f) + 15) & ~15)
+    buf = np.zeros(pos + 8192, np.uint8)
+    for o, f in zip(offs, frames):
+        buf[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    ms = (R.Mbuf * n)()
+    for i in range(n):
+        o = offs[i] if layout != "overlap" else offs[i % (n // 3)]  # a third of the data, reused
+        f = frames[i] if layout != "overlap" else frames[i % (n // 3)]
+        ms[i].buf_addr = buf.ctypes.data + o
+        ms[i].data_len = len(f)
+    arr = (C.POINTER(R.Mbuf) * n)(*[C.pointer(ms[i]) for i in range(n)])
+    with R.Context(0, max_pkts=2048, max_bytes=(2048 * 1536 if layout != "sparse" else n * 4096 + 8192)) as ctx:
+        ctx.flows_sync(udp, tcb)
+        host = ctx.process_mbufs_deliver(arr)
+        ctx.register_host(buf.ctypes.data, buf.nbytes)
+        auto = ctx.process_mbufs_deliver(arr)
+        ctx.tune_ingest(R.INGEST_PULL)
+        pull = ctx.process_mbufs_deliver(arr)
+        ctx.unregister_host(buf.ctypes.data)
+    for got in (auto, pull):
+        for a, b in zip(host[:6], got[:6]):
+            assert (a is None and b is None) or a.tobytes() == b.tobytes(), layout
+    assert len(host[4]) > 100 and len(host[1]) > 100

@@ -13,7 +13,7 @@ for line in open(sys.argv[1]):
             print(name, v)
             continue
         print(f"{name}: seq {v['mpps']} Mpps (rx {v['rx_burst_ms']} + app {v['app_recv_ms']} ms)")
-        for k in ("halves", "overlapped", "overlapped_pinned"):
+        for k in ("halves", "ingest_pull", "overlapped", "overlapped_unpinned"):
             x = v.get(k)
             if not x:
                 continue
