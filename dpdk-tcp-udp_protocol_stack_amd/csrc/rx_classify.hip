@@ -1929,7 +1929,9 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
     // EP: the stream's last tile, the tile that completes this frame's head
     const uint32_t tlast = span ? (span - 1u) / TCH : 0u;
     const uint32_t thead = cp > 0 ? (rel + nh - 1u) / TCH : 0u;
-    const bool early = EP && streamed && cp >= 14 && tlast > 0 && thead == tlast;
+    // (tlast >= 2: the early parse runs after the first tile pair, which must
+    // not hold the last tile, whose partial chunks land in head slot 0)
+    const bool early = EP && streamed && cp >= 14 && tlast >= 2 && thead == tlast;
     const uint32_t relx = early ? 0x8000u : 0u; // (rel < MAPC < 0x8000)
     if (streamed) {
         if (!early)
@@ -1956,7 +1958,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
     }
     // EP: the frames whose probe goes out inside the stream (the rest, rare,
     // keep the after-stream path)
-    const bool inflight = EP && streamed && cp >= 14 && !direct && tlast > 0;
+    const bool inflight = EP && streamed && cp >= 14 && !direct && tlast > 0 && (early || thead < tlast);
     if constexpr (EP) {
         if (__ballot(early) != 0ull) { // the early heads, by LDS-DMA into slots 0..3
 #pragma unroll
