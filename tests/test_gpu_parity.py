@@ -716,3 +716,33 @@ def test_count_idx16_all_ones(ctx, torch_dev, nu):
     if nu == 65536:
         want[65535] = reps
     assert np.array_equal(cnt, want)
+
+
+@pytest.mark.parametrize("variant", [(0, 0, 0, 64), (0, 0, 0, 67), (0, 0, 0, 65), (0, 0, 0, 61),
+                                     (0, 0, 0, 62), (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 68)])
+@pytest.mark.parametrize("size", [90, "mixed"])
+def test_sh_short_spans(ctx, torch_dev, variant, size):
+    """SH blocks whose span is one to three stream tiles (small frames packed
+    at 16-B boundaries), frames with a partial last chunk (90 B: chunks 0-4
+    and 10 bytes of chunk 5), so the last tile holds heads and partial chunks
+    at once (the EP variants' early-head and in-stream probe paths, the tile
+    rotations of 71 / 73); against the oracle, with counts"""
+    rng = np.random.default_rng(90 if size == 90 else 91)
+    cfg = rxdist.gen_cfg("cfg4", n_udp=300, n_tcp=300)
+    udp, tcb = R.gen_flows(cfg)
+    pk, off, ln = R.gen_host(cfg, 5, 6000, 6)
+    frames = [pk[int(o) << 6:(int(o) << 6) + int(l)].tobytes() for o, l in zip(off, ln)]
+    if size == 90:
+        frames = [f[:90] if len(f) >= 90 else f for f in frames]
+    else:
+        frames = [f[:int(rng.integers(60, 260))] for f in frames]
+    buf, off, lens = F.pack_frames(frames, 4)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(buf, off, lens, 4, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 4, 354, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, size, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), (variant, size)
