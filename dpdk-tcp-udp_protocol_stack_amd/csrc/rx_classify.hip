@@ -1317,15 +1317,16 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // FPB: frames per block (256, or 128 / 64 / 32 / 16 with the other threads
 // streaming only: shorter blocks for jumbo frames, whose 256-frame blocks
 // stream 2.3 MB each and leave the last round of blocks a fraction of the chip)
+// L: 16-B chunks per thread per tail tile (4: 16-KiB tiles)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false, uint32_t FPB = 256>
+          bool HG = false, uint32_t FPB = 256, int L = 4>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    constexpr uint32_t LPT = 4;          // 16-B chunks per thread per tail tile
-    constexpr uint32_t TCH = 256u * LPT; // chunks per tail tile (16 KiB)
+    constexpr uint32_t LPT = L;          // 16-B chunks per thread per tail tile
+    constexpr uint32_t TCH = 256u * LPT; // chunks per tail tile
     __shared__ __attribute__((aligned(16))) uint32_t s_pre[2][TCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_wt[2][4 * LPT]; // [row j][wave w]
     __shared__ unsigned long long s_lo, s_hi;
@@ -1681,14 +1682,14 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
 }
 
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false, uint32_t FPB = 256>
+          bool HG = false, uint32_t FPB = 256, int L = 4>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG, FPB>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG, FPB, L>), dim3((uint32_t)blocks),
                        dim3(256), (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out,
                        counts, lds_bins);
     return hipGetLastError();
@@ -2649,6 +2650,9 @@ static const variant_entry k_variants[] = {
     // 938: 738 with 16 frames per block; 739: pipe 39 (probe consumed before the
     // stream) with 32
     {0, 1, 1, 938, launch_stream<true, 0, 3, 1, true, false, false, 16>},
+    // 2938 / 3938: 938 with 8-KiB / 12-KiB tail tiles
+    {0, 1, 1, 2938, launch_stream<true, 0, 3, 1, true, false, false, 16, 2>},
+    {0, 1, 1, 3938, launch_stream<true, 0, 3, 1, true, false, false, 16, 3>},
     {0, 1, 1, 739, launch_stream<true, 0, 0, 1, true, false, false, 32>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
