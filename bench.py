@@ -318,7 +318,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     kdisp = kernel_dispatches(ctx, pk, off, ln, n, ul, w["len_hint"], out, counts, stream, csh,
-                              dev, alg_bytes)
+                              dev, alg_bytes, cs if use_cs else None)
     # counts: every delivered verdict counted once per step, on every rank
     # after the all-reduce (the global histogram)
     v = out[:n * 16].view(n, 16)
@@ -417,20 +417,26 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
 KDISP = 20  # dispatches of the per-dispatch pass (roofline.kernel)
 
 
-def kernel_dispatches(ctx, pk, off, ln, n, ul, len_hint, out, counts, stream, csh, dev, alg_bytes):
+def kernel_dispatches(ctx, pk, off, ln, n, ul, len_hint, out, counts, stream, csh, dev, alg_bytes,
+                      cs=None):
     """roofline.kernel: the dominant kernel dispatch by dispatch, so that a
     kernel trace of the same run (rocprofv3 --kernel-trace) can confirm it.
     KDISP untimed classify dispatches after the timed steps, each between its
     own HIP event pair on the kernel's stream, counts on (into a scratch
-    vector: the run's counts stay exact).  A dispatch measured alone includes
-    its ramp-up and drain, which back-to-back steps overlap with the next
-    dispatch, so its mean can exceed ms_per_step."""
+    vector: the run's counts stay exact).  Where the counts are separate passes
+    on the count stream cs, each dispatch first waits for the previous one's
+    passes, so that no slab pass shares the GPU with the dispatch being timed
+    (in the steps they overlap the next classify; a kernel trace times each
+    kernel on its own).  A dispatch measured alone includes its ramp-up and
+    drain, which back-to-back steps overlap with the next dispatch."""
     name, variant = ctx.kernel_variant(len_hint)
     scratch = torch.zeros_like(counts) if COUNTS else None
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(KDISP)]
     torch.cuda.synchronize(dev)
     for a, b in evs:
+        if cs is not None:
+            stream.wait_stream(cs)
         a.record(stream)
         ctx.classify_dev(pk, off, ln, n, ul, len_hint, out, scratch, stream=stream.cuda_stream,
                          count_stream=csh)

@@ -1477,52 +1477,52 @@ struct staged {
 // device loads of host memory ~38); else the device pulls frame by frame
 // (device source addresses).  st->src / pulled unset: the host gather takes it.
 static int pull_mbufs(rxg_ctx *c, rxg_ctx::slot &sl, rxg_mbuf *const *m, uint32_t n, staged *st) {
-    if (c->regions.empty() || c->tune_ingest == RXG_INGEST_GATHER) return RXG_OK;
+    if (c->regions.empty() || c->tune_ingest == RXG_INGEST_GATHER || n == 0) return RXG_OK;
+    if (!sl.h_src) {
+        HIPCHK(hipMalloc(&sl.d_src, (size_t)c->max_pkts * 8));
+        HIPCHK(hipHostMalloc((void **)&sl.h_src, (size_t)c->max_pkts * 8, 0));
+    }
     if (sl.ticket) HIPCHK(hipEventSynchronize(sl.ev_in)); // the slot's last copy-in read h_*
-    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    // one pass over the mbufs: each frame's device address (h_src) and
+    // length, the covering span, and whether all frames share one 64-B phase
+    uintptr_t lo = UINTPTR_MAX, hi = 0, phase = 0;
+    const uintptr_t ph0 = m[0] ? ((uintptr_t)m[0]->buf_addr + m[0]->data_off) & 63u : 0;
     uint64_t dense = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (!m[i] || !m[i]->buf_addr) return RXG_EINVAL;
         const uintptr_t f = (uintptr_t)m[i]->buf_addr + m[i]->data_off;
-        const uint64_t l16 = (m[i]->data_len + 15ull) & ~15ull;
-        if ((f & 15u) || !region_dev(c, (const uint8_t *)f, l16)) return RXG_OK; // (host gather)
+        const uint32_t l = m[i]->data_len;
+        const uint64_t l16 = (l + 15ull) & ~15ull;
+        uint8_t *d = (f & 15u) ? nullptr : region_dev(c, (const uint8_t *)f, l16);
+        if (!d) return RXG_OK; // (the host gather takes the burst)
+        sl.h_src[i] = (unsigned long long)(uintptr_t)d;
+        sl.h_len[i] = (uint16_t)l;
         lo = std::min(lo, f);
         hi = std::max<uintptr_t>(hi, f + l16);
+        phase |= (f & 63u) ^ ph0;
         dense += l16;
     }
-    if (n == 0) return RXG_OK;
     const uint64_t span = hi - lo;
+    uint8_t *dlo = region_dev(c, (const uint8_t *)lo, 16);
     if (c->tune_ingest != RXG_INGEST_PULL && span <= c->max_bytes && span <= dense + dense / 5 * 2 &&
         span >> 4 <= 0xFFFFFFFFull && region_dev(c, (const uint8_t *)lo, span)) {
-        // 64-B units when every frame sits on a 64-B boundary from the span's
-        // start (mbuf data rooms usually do), else 16-B units
-        uintptr_t mis = 0;
-        for (uint32_t i = 0; i < n; ++i) mis |= (uintptr_t)m[i]->buf_addr + m[i]->data_off - lo;
-        const uint32_t ul = (mis & 63u) ? 4u : 6u;
-        for (uint32_t i = 0; i < n; ++i) {
-            const uintptr_t f = (uintptr_t)m[i]->buf_addr + m[i]->data_off;
-            sl.h_off[i] = (uint32_t)((f - lo) >> ul);
-            sl.h_len[i] = (uint16_t)m[i]->data_len;
-        }
+        // one span: 64-B units when every frame sits on a 64-B boundary from
+        // its start (mbuf data rooms usually do), else 16-B units; offsets
+        // from the device addresses (the same region, so the same distances)
+        const uint32_t ul = phase ? 4u : 6u;
+        const uintptr_t dbase = (uintptr_t)dlo;
+        for (uint32_t i = 0; i < n; ++i) sl.h_off[i] = (uint32_t)(((uintptr_t)sl.h_src[i] - dbase) >> ul);
         st->src = (const uint8_t *)lo;
         st->span = span;
         st->bound = std::min<uint64_t>(std::max(span, dense), c->max_bytes); // (frames may overlap)
         st->ul = ul;
         return RXG_OK;
     }
-    if (!sl.h_src) {
-        HIPCHK(hipMalloc(&sl.d_src, (size_t)c->max_pkts * 8));
-        HIPCHK(hipHostMalloc((void **)&sl.h_src, (size_t)c->max_pkts * 8, 0));
-    }
     uint64_t pos = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *f = (const uint8_t *)m[i]->buf_addr + m[i]->data_off;
-        const uint32_t l = m[i]->data_len;
-        const uint64_t step = std::max<uint64_t>((l + 63ull) & ~63ull, 64);
+        const uint64_t step = std::max<uint64_t>((sl.h_len[i] + 63ull) & ~63ull, 64);
         if (pos + step > c->max_bytes) return RXG_ERANGE;
-        sl.h_src[i] = (unsigned long long)(uintptr_t)region_dev(c, f, (l + 15ull) & ~15ull);
         sl.h_off[i] = (uint32_t)(pos >> 6);
-        sl.h_len[i] = (uint16_t)l;
         pos += step;
     }
     st->span = st->bound = pos;
