@@ -1857,8 +1857,12 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 // FPB: frames per block (a multiple of 64; threads past it only stream), so
 // that larger frames still fit the head map (1500 B: 64 frames, 96 KiB).
 // TT: stream tiles in flight per thread (2, or 3 with a period-3 rotation).
+// PERS: a resident grid; each block loops over block-tiles of FPB frames and
+// loads the next one's descriptors during the current one's stream, so no
+// block starts on a descriptor round trip (and the LDS histogram is flushed
+// once per block instead of once per 256 frames).
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false>
 __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1886,6 +1890,21 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         return EP ? k * 256u + m : (PS ? (k - 1u) * 256u + m : m * 4u + k);
     };
     for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+    static_assert(FPB % 64 == 0 && FPB <= 256, "whole waves of frames");
+    const uint32_t nblk = (uint32_t)(((uint64_t)n + FPB - 1) / FPB);
+    // PERS: this block-tile's descriptors, loaded during the previous one
+    uint32_t nx_off = 0;
+    int32_t nx_len = 0;
+    auto desc_load = [&](uint32_t blk) {
+        const uint64_t pp = (uint64_t)blk * FPB + tid;
+        const bool vv = blk < nblk && tid < (uint32_t)FPB && pp < n;
+        nx_off = off[vv ? pp : 0];
+        nx_len = vv ? (int32_t)len[vv ? pp : 0] : 0;
+    };
+    if constexpr (PERS) desc_load(blockIdx.x);
+    // (without PERS the loop is one trip the compiler sees as such)
+    const uint32_t bend = PERS ? nblk : blockIdx.x + 1u;
+    for (uint32_t blk = blockIdx.x; blk < bend; blk += PERS ? gridDim.x : 1u) {
     if (tid == 0) {
         s_lo = ~0ull;
         s_hi = 0;
@@ -1897,12 +1916,21 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         uint4 *m4 = reinterpret_cast<uint4 *>(s_map);
         for (uint32_t i = tid; i < MAPC / 16; i += 256) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
-    static_assert(FPB % 64 == 0 && FPB <= 256, "whole waves of frames");
-    const uint64_t p = (uint64_t)blockIdx.x * FPB + tid;
+    const uint64_t p = (uint64_t)blk * FPB + tid;
     const bool valid = tid < (uint32_t)FPB && p < n;
     const uint64_t q = valid ? p : 0;
-    const uint64_t fpos = (uint64_t)off[q] << unit_log2;
-    const int32_t cp = valid ? (int32_t)len[q] : 0;
+    uint32_t doff;
+    int32_t dlen;
+    if constexpr (PERS) {
+        doff = nx_off;
+        dlen = nx_len;
+        desc_load(blk + gridDim.x); // in flight through this block-tile's stream
+    } else {
+        doff = off[q];
+        dlen = valid ? (int32_t)len[q] : 0;
+    }
+    const uint64_t fpos = (uint64_t)doff << unit_log2;
+    const int32_t cp = dlen;
     const uint8_t *fb = pkts + fpos;
     const uint64_t fc = fpos >> 4;                  // first chunk (absolute)
     const uint32_t nch = ((uint32_t)cp + 15u) >> 4; // chunks of the capture
@@ -2270,6 +2298,8 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
     }
     if constexpr ((ABL & 48) == 0)
         if (wvu * 64u < (uint32_t)FPB) put_count_idx_wave(ft, p, cidx, lane); // (waves of frames)
+    if constexpr (PERS) __syncthreads(); // every LDS read of this block-tile done
+    } // block-tiles
     if (lds_bins) {
         __syncthreads();
         for (uint32_t i = tid; i < lds_bins; i += 256) {
@@ -2280,17 +2310,26 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
 }
 
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                      const uint32_t *, const uint32_t *) {
-    const uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
+    uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (PERS) { // one resident wave of blocks
+        int cu = 0, bpc = 0;
+        hipError_t e = rx_occupancy(
+            reinterpret_cast<const void *>(rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS>),
+            256, (size_t)lds_bins * 4u, &cu, &bpc);
+        if (e != hipSuccess) return e;
+        const uint64_t res = (uint64_t)cu * (uint64_t)(bpc > 0 ? bpc : 1);
+        if (blocks > res) blocks = res;
+    }
     if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
         return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
                                               lds_bins, s, nullptr, nullptr);
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS>), dim3((uint32_t)blocks),
                        dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
@@ -2679,6 +2718,9 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
     {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
     {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
+    // 77 / 79: 67 / 64 on a resident grid (descriptors one block-tile ahead)
+    {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
+    {0, 1, 1, 79, launch_sh<0, 4, SH_MAPC, false, 4, false, 256, 2, true>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2730,7 +2772,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 78:
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 79:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";
