@@ -2718,9 +2718,8 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
     {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
     {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
-    // 77 / 79: 67 / 64 on a resident grid (descriptors one block-tile ahead)
+    // 77: 67 on a resident grid (descriptors one block-tile ahead)
     {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
-    {0, 1, 1, 79, launch_sh<0, 4, SH_MAPC, false, 4, false, 256, 2, true>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
