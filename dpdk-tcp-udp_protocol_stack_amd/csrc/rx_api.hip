@@ -1797,47 +1797,59 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
     if (rc) return rc;
     const uint64_t pos = st.bound;
     const double t1 = now_ms();
-    HIPCHK(hipEventRecord(ds.tev[0], c->s_h2d));
-    rc = submit_slot(c, sl, st.src, st.span, sl.h_off, sl.h_len, n, st.ul, out, t, st.pulled);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(ds.tev[1], c->s_h2d)); // after the copy in
-    HIPCHK(hipEventRecord(ds.tev[2], c->stream)); // after K1
-    // the compactions follow the classify on the context's stream
-    if (udp)
-        if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_cp_dg,
-                               c->d_cp_first, c->d_cp_payload, c->max_bytes, c->d_cp_totals,
-                               c->stream)))
-            return rc;
-    const bool tcp = c->fs.tcp.id_space() > 0;
-    if (tcp)
-        if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_ss_seg,
-                               c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
-            return rc;
-    HIPCHK(hipEventRecord(ds.tev[3], c->stream)); // after K3 / K4
-    // every result in one round trip: the counts with upper-bound copies of
-    // the records (n of each) and payloads (the staged span bounds the sum of
-    // the 16-B padded payloads), so no synchronisation sits between the
-    // compactions and their copy out.  The next set's compactions reuse the
-    // device buffers after these copies, in stream order.
-    if (udp) {
-        HIPCHK(hipMemcpyAsync(ds.h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(ds.h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(ds.h_cp_dg, c->d_cp_dg, (size_t)n * sizeof(rxg_dgram),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(ds.h_cp_payload, c->d_cp_payload, pos, hipMemcpyDeviceToHost,
-                              c->stream));
+    bool tcp = false;
+    // every device step and copy of the burst; on an error after the first is
+    // queued, the streams are drained so nothing still writes into the set
+    auto enqueue = [&]() -> int {
+        HIPCHK(hipEventRecord(ds.tev[0], c->s_h2d));
+        rc = submit_slot(c, sl, st.src, st.span, sl.h_off, sl.h_len, n, st.ul, out, t, st.pulled);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(ds.tev[1], c->s_h2d)); // after the copy in
+        HIPCHK(hipEventRecord(ds.tev[2], c->stream)); // after K1
+        // the compactions follow the classify on the context's stream
+        if (udp)
+            if ((rc = compact_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_cp_dg,
+                                   c->d_cp_first, c->d_cp_payload, c->max_bytes, c->d_cp_totals,
+                                   c->stream)))
+                return rc;
+        tcp = c->fs.tcp.id_space() > 0;
+        if (tcp)
+            if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_ss_seg,
+                                   c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
+                return rc;
+        HIPCHK(hipEventRecord(ds.tev[3], c->stream)); // after K3 / K4
+        // every result in one round trip: the counts with upper-bound copies of
+        // the records (n of each) and payloads (the staged span bounds the sum of
+        // the 16-B padded payloads), so no synchronisation sits between the
+        // compactions and their copy out.  The next set's compactions reuse the
+        // device buffers after these copies, in stream order.
+        if (udp) {
+            HIPCHK(hipMemcpyAsync(ds.h_cp_totals, c->d_cp_totals, 3 * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(ds.h_cp_first, c->d_cp_first, (nf + 1) * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(ds.h_cp_dg, c->d_cp_dg, (size_t)n * sizeof(rxg_dgram),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(ds.h_cp_payload, c->d_cp_payload, pos, hipMemcpyDeviceToHost,
+                                  c->stream));
+        }
+        if (tcp) {
+            HIPCHK(hipMemcpyAsync(ds.h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(ds.h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
+                                  hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPCHK(hipEventRecord(ds.tev[4], c->stream)); // after the results' copy out
+        return RXG_OK;
+    };
+    if ((rc = enqueue())) {
+        (void)hipStreamSynchronize(c->s_h2d);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->s_d2h);
+        return rc;
     }
-    if (tcp) {
-        HIPCHK(hipMemcpyAsync(ds.h_ss_totals, c->d_ss_totals, 3 * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(ds.h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
-                              hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(hipEventRecord(ds.tev[4], c->stream)); // after the results' copy out
     ds.on = true;
     ds.udp = udp;
     ds.tcp = tcp;
