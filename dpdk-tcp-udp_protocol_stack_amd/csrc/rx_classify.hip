@@ -1319,7 +1319,7 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
 // stream 2.3 MB each and leave the last round of blocks a fraction of the chip)
 // L: 16-B chunks per thread per tail tile (4: 16-KiB tiles)
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false, uint32_t FPB = 256, int L = 4>
+          bool HG = false, uint32_t FPB = 256, int L = 4, bool WT = false>
 __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1666,7 +1666,7 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
             vd.y = vy;
             vd.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
             vd.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
-            st_verdict(ft, out, p, vd);
+            st_verdict<WT>(ft, out, p, vd);
             lane_count(cidx, counts, hist, lds_bins);
         }
         // (FPB < 64: the first FPB lanes of wave 0; its other lanes' pieces are the next block's)
@@ -1682,14 +1682,14 @@ __global__ __launch_bounds__(256, HO == 3 ? 5 : 6) void rx_classify_stream_kerne
 }
 
 template <bool NTS, int ABL = 0, int HO = 0, int PW = 1, bool B1 = false, bool DS = false,
-          bool HG = false, uint32_t FPB = 256, int L = 4>
+          bool HG = false, uint32_t FPB = 256, int L = 4, bool WT = false>
 hipError_t launch_stream(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                          uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                          unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                          const uint32_t *, const uint32_t *) {
     const uint64_t blocks = ((uint64_t)n + FPB - 1) / FPB;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG, FPB, L>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_stream_kernel<NTS, ABL, HO, PW, B1, DS, HG, FPB, L, WT>), dim3((uint32_t)blocks),
                        dim3(256), (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out,
                        counts, lds_bins);
     return hipGetLastError();
@@ -1861,8 +1861,9 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 // loads the next one's descriptors during the current one's stream, so no
 // block starts on a descriptor round trip (and the LDS histogram is flushed
 // once per block instead of once per 256 frames).
+// WT: write-through (sc1) verdict stores (the G=8 kernel's pipe 40).
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false>
 __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -2293,7 +2294,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
         if constexpr ((ABL & 32) != 0)
             if (wvu * 64u < (uint32_t)FPB) put_count_idx_wave(ft, p, cidx, lane); // (diagnostic order)
-        st_verdict(ft, out, p, vd);
+        st_verdict<WT>(ft, out, p, vd);
         lane_count(cidx, counts, hist, lds_bins);
     }
     if constexpr ((ABL & 48) == 0)
@@ -2310,7 +2311,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
 }
 
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -2320,7 +2321,7 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (PERS) { // one resident wave of blocks
         int cu = 0, bpc = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS>),
+            reinterpret_cast<const void *>(rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT>),
             256, (size_t)lds_bins * 4u, &cu, &bpc);
         if (e != hipSuccess) return e;
         const uint64_t res = (uint64_t)cu * (uint64_t)(bpc > 0 ? bpc : 1);
@@ -2329,7 +2330,7 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
         return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
                                               lds_bins, s, nullptr, nullptr);
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT>), dim3((uint32_t)blocks),
                        dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
@@ -2692,6 +2693,8 @@ static const variant_entry k_variants[] = {
     // 2938 / 3938: 938 with 8-KiB / 12-KiB tail tiles
     {0, 1, 1, 2938, launch_stream<true, 0, 3, 1, true, false, false, 16, 2>},
     {0, 1, 1, 3938, launch_stream<true, 0, 3, 1, true, false, false, 16, 3>},
+    // 4938: 938 with write-through verdict stores
+    {0, 1, 1, 4938, launch_stream<true, 0, 3, 1, true, false, false, 16, 4, true>},
     {0, 1, 1, 739, launch_stream<true, 0, 0, 1, true, false, false, 32>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
@@ -2718,8 +2721,10 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
     {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
     {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
-    // 77: 67 on a resident grid (descriptors one block-tile ahead)
+    // 77: 67 on a resident grid (descriptors one block-tile ahead); 81: 67
+    // with write-through verdict stores
     {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
+    {0, 1, 1, 81, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, false, true>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2771,7 +2776,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 79:
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 81:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";
