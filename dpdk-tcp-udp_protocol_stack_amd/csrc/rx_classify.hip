@@ -2693,8 +2693,7 @@ static const variant_entry k_variants[] = {
     // 2938 / 3938: 938 with 8-KiB / 12-KiB tail tiles
     {0, 1, 1, 2938, launch_stream<true, 0, 3, 1, true, false, false, 16, 2>},
     {0, 1, 1, 3938, launch_stream<true, 0, 3, 1, true, false, false, 16, 3>},
-    // 4938: 938 with write-through verdict stores
-    {0, 1, 1, 4938, launch_stream<true, 0, 3, 1, true, false, false, 16, 4, true>},
+
     {0, 1, 1, 739, launch_stream<true, 0, 0, 1, true, false, false, 32>},
     // 60: heads taken out of the block stream (SH kernel)
     // 63 / 64: 60 with a two / four-slot first probe window
@@ -2721,10 +2720,8 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
     {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
     {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
-    // 77: 67 on a resident grid (descriptors one block-tile ahead); 81: 67
-    // with write-through verdict stores
+    // 77: 67 on a resident grid (descriptors one block-tile ahead)
     {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
-    {0, 1, 1, 81, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, false, true>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2776,7 +2773,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 81:
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";
