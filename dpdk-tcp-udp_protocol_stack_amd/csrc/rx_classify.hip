@@ -1862,13 +1862,8 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 // block starts on a descriptor round trip (and the LDS histogram is flushed
 // once per block instead of once per 256 frames).
 // WT: write-through (sc1) verdict stores (the G=8 kernel's pipe 40).
-// SPEC: the first tile goes out with the descriptors' round trip, from the
-// span of the block's first and last frames (frames in buffer order, the
-// usual burst), instead of after the block's span reduction; loaded again
-// when the real span starts elsewhere.
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false,
-          bool SPEC = false>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false>
 __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) void rx_classify_sh_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -1938,21 +1933,6 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
     const uint64_t fpos = (uint64_t)doff << unit_log2;
     const int32_t cp = dlen;
     const uint8_t *fb = pkts + fpos;
-    uint4 va[LPT], vb[LPT];
-    uint64_t glo = 0;
-    uint32_t gspan = 0;
-    if constexpr (SPEC) { // [first frame's start, last frame's end): inside the buffer
-        const uint64_t b0 = (uint64_t)blk * FPB, bl = min(b0 + FPB, (uint64_t)n) - 1u;
-        const uint64_t o0 = (uint64_t)off[b0] << unit_log2, ol = (uint64_t)off[bl] << unit_log2;
-        const uint64_t ghi = (ol + len[bl] + 15u) >> 4;
-        glo = o0 >> 4;
-        gspan = ghi > glo ? (uint32_t)min<uint64_t>(ghi - glo, TCH) : 0u;
-#pragma unroll
-        for (int j = 0; j < LPT; ++j) {
-            const uint32_t k = j * 256 + tid;
-            va[j] = ldg16<true>(pkts + ((glo + (k < gspan ? k : 0u)) << 4));
-        }
-    }
     const uint64_t fc = fpos >> 4;                  // first chunk (absolute)
     const uint32_t nch = ((uint32_t)cp + 15u) >> 4; // chunks of the capture
     const int32_t cf = cp & ~15;                    // full chunks: [0, cf)
@@ -1972,9 +1952,8 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
             v[j] = ldg16<true>(sb + ((uint64_t)(k < span ? k : 0) << 4)); // masked at use
         }
     };
-    // the first tile: already loaded from the guessed span when it starts at
-    // the real one and covers the real one's first tile
-    if (!SPEC || !(lo == glo && gspan >= min<uint64_t>(span, TCH))) tile_load(va, 0);
+    uint4 va[LPT], vb[LPT];
+    tile_load(va, 0);
     const uint32_t rel = (streamed && cp > 0) ? (uint32_t)(fc - lo) : 0u;
     const uint32_t nh = nch < 4u ? nch : 4u;
     // EP: the stream's last tile, the tile that completes this frame's head
@@ -2332,8 +2311,7 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
 }
 
 template <int ABL = 0, int PW = 1, uint32_t MAPC = SH_MAPC, bool EP = false, int L = EP ? 3 : 4,
-          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false,
-          bool SPEC = false>
+          bool PS = false, int FPB = 256, int TT = 2, bool PERS = false, bool WT = false>
 hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                      uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                      unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
@@ -2343,8 +2321,7 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (PERS) { // one resident wave of blocks
         int cu = 0, bpc = 0;
         hipError_t e = rx_occupancy(
-            reinterpret_cast<const void *>(
-                rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT, SPEC>),
+            reinterpret_cast<const void *>(rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT>),
             256, (size_t)lds_bins * 4u, &cu, &bpc);
         if (e != hipSuccess) return e;
         const uint64_t res = (uint64_t)cu * (uint64_t)(bpc > 0 ? bpc : 1);
@@ -2353,8 +2330,7 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (EP && ((uintptr_t)pkts & 15u)) // LDS-DMA needs 16-B aligned frames: pipe 64 instead
         return launch_sh<ABL, 4, MAPC, false>(pkts, off, len, n, unit_log2, ft, out, counts,
                                               lds_bins, s, nullptr, nullptr);
-    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT, SPEC>),
-                       dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((rx_classify_sh_kernel<ABL, PW, MAPC, EP, L, PS, FPB, TT, PERS, WT>), dim3((uint32_t)blocks),
                        dim3(256),
                        (size_t)lds_bins * 4u, s, pkts, off, len, n, unit_log2, ft, out, counts,
                        lds_bins);
@@ -2744,11 +2720,8 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
     {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
     {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
-    // 77: 67 on a resident grid (descriptors one block-tile ahead); 83 / 85:
-    // 67 / 64 with the first tile loaded from the guessed span
+    // 77: 67 on a resident grid (descriptors one block-tile ahead)
     {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
-    {0, 1, 1, 83, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, false, false, true>},
-    {0, 1, 1, 85, launch_sh<0, 4, SH_MAPC, false, 4, false, 256, 2, false, false, true>},
     {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
     // 264: 64 with every partial last chunk loaded from HBM after the stream
     // (no partial marks; diagnostic)
@@ -2800,7 +2773,7 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     if (pipe == 20) return "rx_bin_kernel+rx_classify_lane_kernel+rx_classify_kernel";
     switch (pipe % 1000u % 100u) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 83: case 85:
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78:
         return "rx_classify_sh_kernel";
     default:
         return "rx_classify_stream_kernel";

@@ -74,7 +74,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4
                    (0, 0, 0, 72), (0, 0, 0, 74), (0, 0, 0, 76), (0, 0, 0, 78),  # 64 / 128 frames per block
                    (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),  # three tiles in flight, two-slot window
                    (0, 0, 0, 2938), (0, 0, 0, 3938),  # jumbo stream kernel with 8 / 12-KiB tiles
-                   (0, 0, 0, 77), (0, 0, 0, 83), (0, 0, 0, 85),  # resident grid; first tile from the guessed span
+                   (0, 0, 0, 77),  # 67 on a resident grid
                    (0, 0, 0, 68), (0, 0, 0, 69),  # 67 / 66 with partial-chunk sums in the stream
                    (0, 0, 0, 65), (0, 0, 0, 61), (0, 0, 0, 62)]  # probes inside the stream (LDS-DMA)
 

@@ -292,7 +292,7 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
                                      (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 60),
                                      (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65), (0, 0, 0, 61),
                                      (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
-                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78), (0, 0, 0, 83), (0, 0, 0, 85),
+                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78),
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
                                      (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
@@ -335,7 +335,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
                                      (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
                                      (0, 0, 0, 61), (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
-                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78), (0, 0, 0, 83), (0, 0, 0, 85),
+                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78),
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
                                      (4, 1, 2, 0),
                                      (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),
@@ -408,7 +408,7 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
 
 @pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
                                      (0, 0, 0, 61), (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
-                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78), (0, 0, 0, 83), (0, 0, 0, 85),
+                                     (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78),
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
                                      (0, 0, 0, 54)])
 @pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix", "dirty_gaps", "reversed",
@@ -719,8 +719,7 @@ def test_count_idx16_all_ones(ctx, torch_dev, nu):
 
 
 @pytest.mark.parametrize("variant", [(0, 0, 0, 64), (0, 0, 0, 67), (0, 0, 0, 65), (0, 0, 0, 61),
-                                     (0, 0, 0, 62), (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 68),
-                                     (0, 0, 0, 83), (0, 0, 0, 85)])
+                                     (0, 0, 0, 62), (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 68)])
 @pytest.mark.parametrize("size", [90, "mixed"])
 def test_sh_short_spans(ctx, torch_dev, variant, size):
     """SH blocks whose span is one to three stream tiles (small frames packed
