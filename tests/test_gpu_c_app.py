@@ -1,0 +1,24 @@
+"""The socket API from C (-m gpu): examples/udp_tcp_app.c, a UDP server and a
+TCP server written as the reference's are (netfamily.c:211-383) on
+include/nstack.h alone, linked against libnstack.so / librxgpu.so like an
+application; its own checks (every datagram and its source, the handshake and
+naccept, nrecv's data, a corrupted segment dropped with rc -3, the TX pass's
+SYN|ACK and data ACK) end in exit 0."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+APP = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "dpdk-tcp-udp_protocol_stack_amd", "examples", "udp_tcp_app")
+
+
+def test_c_application_on_the_socket_api():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a GPU (no fallback path exists)")
+    assert os.path.exists(APP), f"{APP} missing: run make -C dpdk-tcp-udp_protocol_stack_amd"
+    r = subprocess.run([APP], capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "udp_tcp_app ok" in r.stdout
