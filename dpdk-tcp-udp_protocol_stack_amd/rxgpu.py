@@ -19,7 +19,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RXGPU_LIB: another build of the same library (A/B of compile-time variants)
 LIB_PATH = os.environ.get("RXGPU_LIB") or os.path.join(_HERE, "librxgpu.so")
-NSTACK_PATH = os.path.join(_HERE, "libnstack.so")
+# NSTACK_LIB: another build of the socket layer (e.g. a sanitizer build, host code only)
+NSTACK_PATH = os.environ.get("NSTACK_LIB") or os.path.join(_HERE, "libnstack.so")
 
 # One HIP runtime per process: PyTorch (the plumbing for device memory, streams
 # and torch.distributed) ships its own libamdhip64.so.7 with the same SONAME as
