@@ -1453,7 +1453,10 @@ def main():
             "config": {"workload": f"{names[0]}: {head['desc']}",
                        "frames_per_step": head["frames_per_step"], "flows": head["nflows"],
                        "parallelism": f"rss-split x{world}" if world > 1 else "1 GPU",
-                       "collective": collective},
+                       "collective": collective,
+                       # ranks time-slicing one GPU (a rehearsal of the N-rank logic on a
+                       # one-GPU box): their step times measure the sharing, not the kernels
+                       "ranks_share_gpus": bool(world > max(ndev, 1))},
             "gb_per_s": round(head["gbps"], 2),
             "roofline": head["roofline"],
             "cpu_baseline": head.get("cpu_baseline"),
