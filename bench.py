@@ -1017,17 +1017,20 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                 os.sched_setaffinity(0, {cpus[0]})
             elif unpin:
                 os.sched_setaffinity(0, old_aff)
-            d0, s0 = int(ns.stat(1)), int(ns.stat(5))
+            d0, s0, c0 = int(ns.stat(1)), int(ns.stat(5)), int(ns.stat(6))
+            w0 = [int(ns.stat(8 + j)) for j in range(3)]
             th = threading.Thread(target=app_thread)
             t0 = time.perf_counter()
             th.start()
-            ov_rx, ov_ph = [], []
+            ov_rx, ov_ph, ov_cp, ov_tr = [], [], [], []
             try:
                 for _ in range(K):
                     a0 = time.perf_counter()
                     ns.rx_burst_mbufs(arr, B)
                     ov_rx.append(time.perf_counter() - a0)
                     ov_ph.append(ns.last_burst_phases())
+                    ov_cp.append(int(ns.stat(6)))
+                    ov_tr.append((ov[0], int(ns.stat(7))))
             finally:
                 stop.set()
                 th.join()
@@ -1037,6 +1040,11 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         received=ov[0], payload_bytes=ov[1],
                         received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
                         stale_bursts=int(ns.stat(5)) - s0,
+                        copied_payload_bytes=int(ns.stat(6)) - c0,
+                        copied_mb_by_burst=[round((b - a) / 1e6, 1) for a, b in zip([c0] + ov_cp, ov_cp)],
+                        drained_and_held_by_burst=ov_tr,
+                        app_ms_per_burst={k: round((int(ns.stat(8 + j)) - w0[j]) / 1e6 / K, 3) for j, k in
+                                          enumerate(("lock_wait", "yield", "read_out"))},
                         rx_burst_ms=round(float(np.median(ov_rx)) * 1e3, 3),
                         rx_burst_phases_ms={k: round(float(np.median([p[k] for p in ov_ph])), 4)
                                             for k in ov_ph[0]},

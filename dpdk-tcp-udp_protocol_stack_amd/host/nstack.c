@@ -187,9 +187,16 @@ struct frag_batch {
 
 /* ---- a tcb's fragment queues: logical fragments over ring items ---------- */
 static rxg_ctx *g_ctx;
+static atomic_llong g_pl_batches; /* batches holding a library payload buffer (stat 7) */
+/* drain_all's time, ns (stats 8-10): waiting for the stack's lock, stepping
+ * aside for the protocol thread, reading the taken-out fragments */
+static atomic_llong g_drain_ns[3];
 static void frag_item_free(struct tcp_fragment *f) {
     if (f->batch) {
-        if (f->batch->pl_ref >= 0) rxg_payload_release(g_ctx, f->batch->pl_ref);
+        if (f->batch->pl_ref >= 0) {
+            rxg_payload_release(g_ctx, f->batch->pl_ref);
+            atomic_fetch_sub_explicit(&g_pl_batches, 1, memory_order_relaxed);
+        }
         free(f->batch); /* (fragments and payloads live in the batch's allocation) */
     } else {
         free(f->data);
@@ -320,6 +327,7 @@ static void app_yield(void) {
  * (nstack_set_halves; 0 = never) */
 static uint32_t g_half_min;
 static uint64_t g_stale_parts; /* burst halves delivered against changed lists */
+static uint64_t g_copied_bytes; /* TCP payload bytes copied on the host (stat 6) */
 static int g_udp_done;          /* this burst's UDP datagrams went out as batches */
 
 /* the control block of each stable flow id (NULL: free id).  Blocks are
@@ -1489,6 +1497,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
                     if ((uint32_t)(PLEN) > (SEG)->ncopy)                                     \
                         memset(pp + (SEG)->ncopy, 0, (uint32_t)(PLEN) - (SEG)->ncopy);       \
                     pp += (uint32_t)(PLEN);                                                  \
+                    g_copied_bytes += (uint32_t)(PLEN);                                      \
                 }                                                                            \
                 g_stat[4]++;                                                                 \
             } else {                                                                         \
@@ -1531,7 +1540,10 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
     #undef PUT_FRAG
     #undef PUT_ACK
     if (rb) {
-        if (rb->pl_ref >= 0) rxg_payload_hold(g_ctx, rb->pl_ref); /* until the batch is freed */
+        if (rb->pl_ref >= 0) { /* until the batch is freed */
+            rxg_payload_hold(g_ctx, rb->pl_ref);
+            atomic_fetch_add_explicit(&g_pl_batches, 1, memory_order_relaxed);
+        }
         if (ring_enqueue(s->rcvbuf, &rb->item)) { /* (not reached: items <= fragments <= capacity) */
             frag_item_free(&rb->item);
             g_stat[4] -= rtake, g_stat[1] += rtake;
@@ -1720,7 +1732,9 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
 
 int nstack_last_burst_phases(float ms[12]) {
     if (!ms) return RXG_EINVAL;
-    pthread_mutex_lock(&g_lock);
+    /* read by the protocol thread between its bursts: it goes ahead of an
+     * application loop (drain_all) as rx_burst itself does */
+    proto_lock();
     memcpy(ms, g_phase_ms, sizeof(g_phase_ms));
     pthread_mutex_unlock(&g_lock);
     return RXG_OK;
@@ -1807,18 +1821,6 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
     return rc;
 }
 
-/* the next fragment's payload into the cache while this one is copied (a
- * batch's fragments sit one after the other in the pinned payload buffer) */
-static inline void prefetch_next(const struct tcp_fragment *f, struct nring *r) {
-    struct tcp_fragment *it;
-    if (ring_peek(r, (void **)&it) || !it->batch || f != &it->batch->frag[it->batch->next]) return;
-    const struct frag_batch *b = it->batch;
-    if (b->next + 1 >= b->n) return;
-    const unsigned char *d = b->frag[b->next + 1].data;
-    const uint32_t l = b->frag[b->next + 1].length;
-    for (uint32_t o = 0; d && o < l; o += 64) __builtin_prefetch(d + o, 0, 0);
-}
-
 /* drain_all's look-ahead over the tcbs it visits next (g_lock held, so none
  * is freed): the tcb 4 ids ahead, the ring of the one 2 ahead, the front
  * fragment, its batch's fragment array and first payload lines of the next
@@ -1847,22 +1849,60 @@ static inline void drain_prefetch(uint32_t id, uint32_t end) {
     }
 }
 
+/* the fragments of ring items drain_all took out of their tcbs, read after
+ * the stack's lock is released: counted (EOF fragments are read and not
+ * counted), copied into buf, and freed (a batch's hold on the library's
+ * payload buffer ends here) */
+static void drain_detached(void **it, uint32_t k, void *buf, uint64_t *got, uint64_t *nb) {
+    for (uint32_t i = 0; i < k; i++) {
+        struct tcp_fragment *f = it[i];
+        if (i + 1 < k) __builtin_prefetch(it[i + 1], 0, 0);
+        if (f->batch) {
+            const struct frag_batch *b = f->batch;
+            for (uint32_t j = b->next; j < b->n; j++) {
+                const struct tcp_fragment *g = &b->frag[j];
+                if (j + 1 < b->n && b->frag[j + 1].data)
+                    for (uint32_t o = 0; o < b->frag[j + 1].length; o += 64)
+                        __builtin_prefetch(b->frag[j + 1].data + o, 0, 0);
+                if (g->length) {
+                    memcpy(buf, g->data, g->length);
+                    (*got)++, *nb += g->length;
+                }
+            }
+        } else if (f->length) {
+            memcpy(buf, f->data, f->length);
+            (*got)++, *nb += f->length;
+        }
+        frag_item_free(f);
+    }
+}
+
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
     /* The application side of the benchmark: every socket read until empty,
      * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
      * visited by stable id, DRAIN_CHUNK of them per hold of the stack's lock:
      * a block is freed only under that lock (no block is read after
      * a concurrent nstack_rx_burst freed it), and between chunks the protocol
-     * thread can take the lock.  A tcb's receive ring is read under one hold
-     * of its mutex: nrecv's semantics call by call (a fragment longer than
-     * `cap` takes nrecv's split path). */
+     * thread can take the lock.  A tcb's receive ring is emptied under one
+     * hold of its mutex: its items are taken out (their fragments then belong
+     * to this call alone) and read after the chunk releases the stack's lock,
+     * so the copies do not hold up the protocol thread's next delivery; an
+     * item with a fragment longer than `cap` is read in place through nrecv's
+     * split path. */
     enum { DRAIN_CHUNK = 64 };
     uint64_t got = 0, nb = 0;
+    void **det = NULL;
+    uint32_t ndet = 0, det_cap = 0;
     for (int kind = 0; kind < 2; kind++) {
         uint32_t id = 0;
         for (;;) {
+            const double w0 = mono_ms();
             app_yield();
+            const double w1 = mono_ms();
             pthread_mutex_lock(&g_lock);
+            const double w2 = mono_ms();
+            atomic_fetch_add_explicit(&g_drain_ns[1], (long long)((w1 - w0) * 1e6), memory_order_relaxed);
+            atomic_fetch_add_explicit(&g_drain_ns[0], (long long)((w2 - w1) * 1e6), memory_order_relaxed);
             const uint32_t ncap = kind ? s_tcb_cap : s_udp_cap;
             if (id >= ncap) {
                 pthread_mutex_unlock(&g_lock);
@@ -1884,27 +1924,44 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
                 if (!s) continue;
                 pthread_mutex_lock(&s->mutex);
                 struct tcp_fragment *f;
-                while ((f = tq_front(s->rcvbuf)) != NULL) {
-                    if (f->length > cap) { /* nrecv's split path */
-                        pthread_mutex_unlock(&s->mutex);
-                        const ssize_t r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT);
-                        if (r > 0) got++, nb += (uint64_t)r;
-                        pthread_mutex_lock(&s->mutex);
+                while (ring_peek(s->rcvbuf, (void **)&f) == 0) {
+                    const uint32_t first = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
+                    uint32_t j = first;
+                    while (j < n && (f->batch ? f->batch->frag[j].length : f->length) <= cap) j++;
+                    if (j < n || (ndet == det_cap && grow((void **)&det, &det_cap, det_cap ? 2 * det_cap : 1024,
+                                                           sizeof(void *)))) {
+                        /* a fragment longer than cap (or no room to take the item
+                         * out): its head read in place, nrecv's way */
+                        struct tcp_fragment *h = tq_front(s->rcvbuf);
+                        if (h->length > cap) {
+                            pthread_mutex_unlock(&s->mutex);
+                            const ssize_t r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT);
+                            if (r > 0) got++, nb += (uint64_t)r;
+                            pthread_mutex_lock(&s->mutex);
+                            continue;
+                        }
+                        if (h->length) {
+                            memcpy(buf, h->data, h->length);
+                            got++, nb += h->length;
+                        }
+                        tq_pop(s->rcvbuf, &s->rq);
                         continue;
                     }
-                    if (f->length) {
-                        prefetch_next(f, s->rcvbuf);
-                        memcpy(buf, f->data, f->length);
-                        got++, nb += f->length;
-                    }
-                    tq_pop(s->rcvbuf, &s->rq);
+                    ring_dequeue(s->rcvbuf, (void **)&f);
+                    s->rq -= n - first;
+                    det[ndet++] = f;
                 }
                 tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
                 pthread_mutex_unlock(&s->mutex);
             }
             pthread_mutex_unlock(&g_lock);
+            const double c0 = mono_ms();
+            drain_detached(det, ndet, buf, &got, &nb);
+            atomic_fetch_add_explicit(&g_drain_ns[2], (long long)((mono_ms() - c0) * 1e6), memory_order_relaxed);
+            ndet = 0;
         }
     }
+    free(det);
     if (bytes) *bytes = nb;
     return (int64_t)got;
 }
@@ -2151,9 +2208,11 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
 }
 
 uint64_t nstack_stat(int which) {
-    if (which < 0 || which > 5) return 0;
+    if (which < 0 || which > 10) return 0;
+    if (which == 7) return (uint64_t)atomic_load_explicit(&g_pl_batches, memory_order_relaxed);
+    if (which >= 8) return (uint64_t)atomic_load_explicit(&g_drain_ns[which - 8], memory_order_relaxed);
     pthread_mutex_lock(&g_lock);
-    uint64_t v = which == 5 ? g_stale_parts : g_stat[which];
+    const uint64_t v = which == 6 ? g_copied_bytes : which == 5 ? g_stale_parts : g_stat[which];
     pthread_mutex_unlock(&g_lock);
     return v;
 }

@@ -173,7 +173,8 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
  * from the segment sort, [8] the frame-by-frame loop over the rest, [9] the
  * whole nstack_rx_burst; [10] segments sorted, [11] datagrams compacted.  A
  * burst run as two halves adds up both halves' phases, so [1]-[4] may exceed
- * the wall time they took. */
+ * the wall time they took.  A protocol-thread call: like nstack_rx_burst it
+ * takes the stack's lock ahead of an application loop (nstack_drain_all). */
 int nstack_last_burst_phases(float ms[12]);
 /* Bursts of at least 2 * min_half frames run as two halves, both on the GPU
  * at once (rxg_deliver_submit twice: the second half's copy in overlaps the
@@ -186,8 +187,16 @@ int nstack_set_halves(uint32_t min_half);
  * 2 = TCP segments dispatched to the state machine, 3 = frames handed to KNI,
  * 4 = TCP fragments (payload or EOF) queued for nrecv, 5 = bursts (or burst
  * halves) delivered frame by frame because the lists changed while they were
- * on the GPU.  Counter 1 also counts TX items dropped (a send ring full, or a
- * datagram too long for a frame). */
+ * on the GPU, 6 = TCP payload bytes copied on the host (the sorted segments'
+ * payloads are otherwise queued in place, in a pooled pinned buffer the
+ * library holds until the application has read them; copied when no pooled
+ * buffer was free, or for a segment cut short by its capture), 7 = fragment
+ * batches now queued that hold such a buffer (read without the lock); 8-10 =
+ * nstack_drain_all's time in ns (read without the lock): waiting for the
+ * stack's lock, stepping aside for the protocol thread, reading out the
+ * fragments it took from the tcbs (outside the lock).  Counter 1
+ * also counts TX items dropped (a send ring full, or a datagram too long for
+ * a frame). */
 uint64_t nstack_stat(int which);
 
 #ifdef __cplusplus
