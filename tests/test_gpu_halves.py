@@ -194,3 +194,46 @@ def test_socket_layer_halves_match_oracle(torch_dev):
         assert len(st.conns) >= 100
     finally:
         st.ns.fini()
+
+
+def _split_model(lens, cap):
+    """drain_all's count through nrecv's split path (common.c:483-496): a
+    fragment longer than cap gives cap bytes, re-queues the rest at the tail
+    and returns the REMAINING length; the last piece returns its length"""
+    got = nb = 0
+    for n in lens:
+        while n > cap:
+            n -= cap
+            got, nb = got + 1, nb + n
+        got, nb = got + 1, nb + n
+    return got, nb
+
+
+@pytest.mark.parametrize("cap", [256, 1000, 4096])
+def test_drain_all_reads_long_fragments_through_the_split_path(torch_dev, cap):
+    """drain_all takes whole ring items out of a tcb and reads them after the
+    stack's lock is released, except an item holding a fragment longer than
+    the buffer, which goes through nrecv's split path in place: the counts
+    must be those of nrecv called until empty"""
+    ns = R.NStack(0, max_burst=1024, max_bytes=1024 * 1536)
+    try:
+        conns = []
+        for k in range(3):
+            t = (R.ip_raw(f"10.9.0.{k + 1}"), R.ip_raw(L), R.port_raw(3000 + k), R.port_raw(9998))
+            assert ns.lib.nstack_tcb_add(*t, 4) == 0
+            conns.append((f"10.9.0.{k + 1}", 3000 + k))
+        rng = np.random.default_rng(33)
+        lens, frames = [], []
+        for i in range(60):
+            cip, cport = conns[i % 3]
+            n = int(rng.choice([1446, 9, 300, 1000, 257, 77]))
+            lens.append(n)
+            frames.append(F.tcp_frame(cip, cport, L, 9998, bytes(rng.integers(0, 256, n, np.uint8)),
+                                      flags=0x18, seq=1000 + i, ack=1))
+        _, rcs, _ = ns.rx_burst(frames)
+        assert (np.asarray(rcs) == 0).all()
+        buf = np.zeros(cap, np.uint8)
+        assert ns.drain_all(buf) == _split_model(lens, cap)
+        assert ns.drain_all(buf) == (0, 0)
+    finally:
+        ns.fini()
