@@ -1019,6 +1019,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                 os.sched_setaffinity(0, old_aff)
             d0, s0, c0 = int(ns.stat(1)), int(ns.stat(5)), int(ns.stat(6))
             w0 = [int(ns.stat(8 + j)) for j in range(3)]
+            pw0 = int(ns.stat(11))
             th = threading.Thread(target=app_thread)
             t0 = time.perf_counter()
             th.start()
@@ -1041,6 +1042,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
                         stale_bursts=int(ns.stat(5)) - s0,
                         copied_payload_bytes=int(ns.stat(6)) - c0,
+                        bursts_waited_for_buffer=int(ns.stat(11)) - pw0,
                         copied_mb_by_burst=[round((b - a) / 1e6, 1) for a, b in zip([c0] + ov_cp, ov_cp)],
                         drained_and_held_by_burst=ov_tr,
                         app_ms_per_burst={k: round((int(ns.stat(8 + j)) - w0[j]) / 1e6 / K, 3) for j, k in

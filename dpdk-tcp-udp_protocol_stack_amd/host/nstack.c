@@ -188,6 +188,19 @@ struct frag_batch {
 /* ---- a tcb's fragment queues: logical fragments over ring items ---------- */
 static rxg_ctx *g_ctx;
 static atomic_llong g_pl_batches; /* batches holding a library payload buffer (stat 7) */
+/* Backpressure for the two-thread arrangement: the batches queued per pooled
+ * payload buffer, the buffer each delivery set's last burst used (the library
+ * holds it until that set's next submit), and the drain_all calls running.
+ * While an application thread drains, nstack_rx_burst waits (the stack's lock
+ * released) for a pooled buffer to come free rather than have the library
+ * hand out the set's own buffer, whose payloads would then be copied. */
+static atomic_int g_pl_out[RXG_PAYLOAD_BUFS];
+static int32_t g_set_ref[RXG_DELIVER_DEPTH];
+static uint32_t g_next_set; /* the set the next submit takes (the library's round robin) */
+static atomic_int g_drainers;
+static pthread_mutex_t g_pl_mx = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_pl_cv = PTHREAD_COND_INITIALIZER;
+static uint64_t g_pl_waits; /* submits that waited for a buffer (stat 11) */
 /* drain_all's time, ns (stats 8-10): waiting for the stack's lock, stepping
  * aside for the protocol thread, reading the taken-out fragments */
 static atomic_llong g_drain_ns[3];
@@ -196,6 +209,12 @@ static void frag_item_free(struct tcp_fragment *f) {
         if (f->batch->pl_ref >= 0) {
             rxg_payload_release(g_ctx, f->batch->pl_ref);
             atomic_fetch_sub_explicit(&g_pl_batches, 1, memory_order_relaxed);
+            if (atomic_fetch_sub_explicit(&g_pl_out[f->batch->pl_ref], 1, memory_order_acq_rel) == 1 &&
+                atomic_load_explicit(&g_drainers, memory_order_relaxed)) {
+                pthread_mutex_lock(&g_pl_mx); /* the last batch on that buffer */
+                pthread_cond_broadcast(&g_pl_cv);
+                pthread_mutex_unlock(&g_pl_mx);
+            }
         }
         free(f->batch); /* (fragments and payloads live in the batch's allocation) */
     } else {
@@ -541,7 +560,12 @@ static void restate_tcb(struct tcp_stream *s, int lookup_moves) {
 int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
     pthread_mutex_lock(&g_lock);
     int rc = RXG_OK;
-    if (!g_ctx) rc = rxg_open(&g_ctx, device, max_burst, max_bytes);
+    if (!g_ctx) {
+        rc = rxg_open(&g_ctx, device, max_burst, max_bytes);
+        /* a new context: its delivery sets start again at set 0 */
+        for (uint32_t j = 0; j < RXG_DELIVER_DEPTH; j++) g_set_ref[j] = -1;
+        g_next_set = 0;
+    }
     g_dirty = 1;
     pthread_mutex_unlock(&g_lock);
     return rc;
@@ -1543,6 +1567,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
         if (rb->pl_ref >= 0) { /* until the batch is freed */
             rxg_payload_hold(g_ctx, rb->pl_ref);
             atomic_fetch_add_explicit(&g_pl_batches, 1, memory_order_relaxed);
+            atomic_fetch_add_explicit(&g_pl_out[rb->pl_ref], 1, memory_order_relaxed);
         }
         if (ring_enqueue(s->rcvbuf, &rb->item)) { /* (not reached: items <= fragments <= capacity) */
             frag_item_free(&rb->item);
@@ -1622,6 +1647,51 @@ static double mono_ms(void) {
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
+/* a pooled payload buffer the library can take for the next submit (set
+ * g_next_set releases its own previous one): none held by queued batches and
+ * none the other sets' last bursts used */
+static int pl_free(void) {
+    for (int k = 0; k < RXG_PAYLOAD_BUFS; k++) {
+        if (atomic_load_explicit(&g_pl_out[k], memory_order_acquire)) continue;
+        int held = 0;
+        for (uint32_t j = 0; j < RXG_DELIVER_DEPTH; j++)
+            if (j != g_next_set && g_set_ref[j] == k) held = 1;
+        if (!held) return 1;
+    }
+    return 0;
+}
+
+/* g_lock held by the protocol thread: while an application thread drains and
+ * every pooled buffer is still held by its unread batches, wait for one (the
+ * lock released, so the application can take fragments out), up to 20 ms;
+ * past that the library's set buffer is used and the payloads copied */
+static void pl_wait_free(void) {
+    if (!atomic_load_explicit(&g_drainers, memory_order_relaxed) || pl_free()) return;
+    const double t0 = mono_ms();
+    g_pl_waits++;
+    while (!pl_free() && atomic_load_explicit(&g_drainers, memory_order_relaxed) &&
+           mono_ms() - t0 < 20.0) {
+        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_lock(&g_pl_mx);
+        if (!pl_free()) {
+            struct timespec ts;
+            clock_gettime(CLOCK_REALTIME, &ts);
+            ts.tv_nsec += 1000000;
+            if (ts.tv_nsec >= 1000000000) ts.tv_sec++, ts.tv_nsec -= 1000000000;
+            pthread_cond_timedwait(&g_pl_cv, &g_pl_mx, &ts);
+        }
+        pthread_mutex_unlock(&g_pl_mx);
+        proto_lock();
+    }
+}
+
+/* after a submit: the set it took and the pooled buffer (or -1) it holds */
+static void pl_note_submit(const rxg_delivery *d) {
+    if (d->set < 1 || d->set > RXG_DELIVER_DEPTH) return;
+    g_set_ref[d->set - 1] = d->tcp_payload_ref;
+    g_next_set = d->set % RXG_DELIVER_DEPTH;
+}
+
 int nstack_set_halves(uint32_t min_half) {
     pthread_mutex_lock(&g_lock);
     g_half_min = min_half;
@@ -1632,6 +1702,7 @@ int nstack_set_halves(uint32_t min_half) {
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
     proto_lock();
+    pl_wait_free(); /* (two threads: the application frees the payload buffers) */
     const double t0 = mono_ms();
     /* one protocol thread (the reference's pkt_process lcore): a second
      * rx_burst while one waits for the GPU is refused */
@@ -1664,6 +1735,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         const double a = mono_ms();
         const int src = rxg_deliver_submit(g_ctx, m + part_off[h], part_n[h], s_v + part_off[h], &d[h]);
         lib_ms += mono_ms() - a;
+        pl_note_submit(&d[h]);
         if (src == RXG_OK)
             sub[h] = 1;
         else if (h == 0)
@@ -1679,6 +1751,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
             const double a = mono_ms();
             rc = rxg_deliver_submit(g_ctx, m + o, k, s_v + o, &d[h]);
             lib_ms += mono_ms() - a;
+            pl_note_submit(&d[h]);
             if (rc != RXG_OK) break;
             sub[h] = 1;
         }
@@ -1892,6 +1965,7 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
     enum { DRAIN_CHUNK = 64 };
     uint64_t got = 0, nb = 0;
     void **det = NULL;
+    atomic_fetch_add_explicit(&g_drainers, 1, memory_order_relaxed);
     uint32_t ndet = 0, det_cap = 0;
     for (int kind = 0; kind < 2; kind++) {
         uint32_t id = 0;
@@ -1962,6 +2036,10 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
         }
     }
     free(det);
+    atomic_fetch_sub_explicit(&g_drainers, 1, memory_order_relaxed);
+    pthread_mutex_lock(&g_pl_mx); /* a waiting protocol thread re-checks */
+    pthread_cond_broadcast(&g_pl_cv);
+    pthread_mutex_unlock(&g_pl_mx);
     if (bytes) *bytes = nb;
     return (int64_t)got;
 }
@@ -2208,11 +2286,14 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
 }
 
 uint64_t nstack_stat(int which) {
-    if (which < 0 || which > 10) return 0;
+    if (which < 0 || which > 11) return 0;
     if (which == 7) return (uint64_t)atomic_load_explicit(&g_pl_batches, memory_order_relaxed);
     if (which >= 8) return (uint64_t)atomic_load_explicit(&g_drain_ns[which - 8], memory_order_relaxed);
     pthread_mutex_lock(&g_lock);
-    const uint64_t v = which == 6 ? g_copied_bytes : which == 5 ? g_stale_parts : g_stat[which];
+    const uint64_t v = which == 11 ? g_pl_waits
+                       : which == 6 ? g_copied_bytes
+                       : which == 5 ? g_stale_parts
+                                    : g_stat[which];
     pthread_mutex_unlock(&g_lock);
     return v;
 }

@@ -194,7 +194,9 @@ int nstack_set_halves(uint32_t min_half);
  * batches now queued that hold such a buffer (read without the lock); 8-10 =
  * nstack_drain_all's time in ns (read without the lock): waiting for the
  * stack's lock, stepping aside for the protocol thread, reading out the
- * fragments it took from the tcbs (outside the lock).  Counter 1
+ * fragments it took from the tcbs (outside the lock); 11 = bursts that waited
+ * for a pooled payload buffer while an application thread was draining (at
+ * most 20 ms each; the stack's lock released meanwhile).  Counter 1
  * also counts TX items dropped (a send ring full, or a datagram too long for
  * a frame). */
 uint64_t nstack_stat(int which);

@@ -21,7 +21,8 @@ for line in open(sys.argv[1]):
             print(f"  {k}: {x['mpps']} Mpps, rx {x['rx_burst_ms']} ms, app "
                   f"{x.get('app_drain_ms', x.get('app_recv_ms'))} ms, tcp_deliver "
                   f"{ph.get('tcp_deliver')}, udp_deliver {ph.get('udp_deliver')}, cpus {x.get('cpus')}, "
-                  f"equal {x.get('received_equal')}, copied {x.get('copied_payload_bytes')}")
+                  f"equal {x.get('received_equal')}, copied {x.get('copied_payload_bytes')}, "
+                  f"waited {x.get('bursts_waited_for_buffer')}")
             if x.get("copied_mb_by_burst"):
                 print("    copied MB by burst", x["copied_mb_by_burst"])
                 print("    (items drained, batches holding a buffer) by burst", x.get("drained_and_held_by_burst"))
