@@ -237,3 +237,59 @@ def test_drain_all_reads_long_fragments_through_the_split_path(torch_dev, cap):
         assert ns.drain_all(buf) == (0, 0)
     finally:
         ns.fini()
+
+
+def test_two_threads_receive_every_byte(torch_dev):
+    """The reference's arrangement: the protocol loop on one thread
+    (nstack_rx_burst), the application on another draining every socket
+    (nstack_drain_all) at the same time.  drain_all takes fragments out under
+    the locks and reads them after; rx_burst waits for a pooled payload buffer
+    while the application still holds them all.  Every payload byte of every
+    burst must reach the application exactly once."""
+    import threading
+    ns = R.NStack(0, max_burst=4096, max_bytes=4096 * 1536)
+    try:
+        conns = []
+        for k in range(512):
+            cip, cport = f"10.8.{k >> 8}.{k & 255}", 4000 + k
+            t = (R.ip_raw(cip), R.ip_raw(L), R.port_raw(cport), R.port_raw(9998))
+            assert ns.lib.nstack_tcb_add(*t, 4) == 0
+            conns.append((cip, cport))
+        rng = np.random.default_rng(34)
+        bursts, want_items, want_bytes = [], 0, 0
+        for b in range(16):
+            frames = []
+            for i in range(4000):
+                cip, cport = conns[int(rng.integers(len(conns)))]
+                n = int(rng.choice([1446, 1446, 700, 33]))
+                frames.append(F.tcp_frame(cip, cport, L, 9998, bytes(rng.integers(0, 256, n, np.uint8)),
+                                          flags=0x18, seq=i, ack=1))
+                want_items, want_bytes = want_items + 1, want_bytes + n
+            buf, off, lens = F.pack_frames(frames, 6)
+            arr, keep = R.NStack.mbufs_over(buf, off, lens, 6)
+            bursts.append((arr, len(frames), keep, buf))
+        got = [0, 0]
+        stop = threading.Event()
+
+        def app():
+            buf = np.zeros(65536, np.uint8)
+            while not stop.is_set():
+                g, nb = ns.drain_all(buf)
+                got[0], got[1] = got[0] + g, got[1] + nb
+            g, nb = ns.drain_all(buf)
+            got[0], got[1] = got[0] + g, got[1] + nb
+
+        c0, w0 = ns.stat(6), ns.stat(11)
+        th = threading.Thread(target=app)
+        th.start()
+        try:
+            for arr, n, _keep, _buf in bursts:
+                assert ns.rx_burst_mbufs(arr, n) >= 0
+        finally:
+            stop.set()
+            th.join()
+        assert (got[0], got[1]) == (want_items, want_bytes)
+        assert ns.stat(7) == 0  # no batch left holding a payload buffer
+        print("copied bytes", ns.stat(6) - c0, "bursts that waited", ns.stat(11) - w0)
+    finally:
+        ns.fini()
