@@ -763,6 +763,9 @@ def cpu_baseline(name, budget_s, cores):
                f"(host: {cores['model']}, nproc {cores['nproc']}, affinity {cores['affinity']}, "
                f"cgroup quota {cores['cgroup_quota']}, threads capped at the box's CPU share; "
                f"nproc = {cores['nproc']} threads, bounded by the same cgroup quota)",
+        sample_short=f"{sampled}{sample} frames of {name} cycled ~{budget_s:g} s through "
+                     f"oracle/ref_cpu.c (-O2, list-scan lookups, printf off) on 1 core; "
+                     f"all_cores = {cores['threads']} threads over an RSS split",
         O2=res["O2"], O0=res["O0"], host=cores)
 
 
@@ -1100,23 +1103,23 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
     return res
 
 
-def hbm_copy_peak(dev, nbytes=4 << 30, reps=10):
-    """device-to-device copy rate on this box (read + write bytes / s): the
-    measured ceiling beside the 8 TB/s spec"""
-    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
-    del a, b
+def hbm_read_ceiling(local, nbytes=4 << 30, reps=9):
+    """this box's measured HBM read ceiling (GB/s) beside the 8 TB/s spec:
+    tools/libceiling.so's plain coalesced read (tools/ceiling.hip), the
+    fastest shape of tools/membw_large.hip; None if the tool is not built"""
+    import ctypes as C
+    p = os.path.join(ROOT, "tools", "libceiling.so")
+    if not os.path.exists(p):
+        log("bench: tools/libceiling.so not built; hbm_read_ceiling_gbs = null")
+        return None
     torch.cuda.empty_cache()
-    return round(2 * nbytes / ms / 1e6, 1)
+    g = C.c_double(0.0)
+    rc = C.CDLL(p).ceiling_read_gbs(C.c_int(local), C.c_ulonglong(nbytes), C.c_int(reps),
+                                    C.byref(g))
+    if rc != 0:
+        log(f"bench: ceiling_read_gbs failed (HIP error {rc})")
+        return None
+    return round(g.value, 1)
 
 
 # ---------------------------------------------------------------------------
@@ -1273,6 +1276,138 @@ def sweep(ctx, names, steps, warmup, dev, only="", with_counts=False):
         torch.cuda.empty_cache()
 
 
+# ---------------------------------------------------------------------------
+# The stdout line.  The driver parses a bounded tail of stdout (round 4's
+# 21-KB line was cut mid-object and read as unparsed), so stdout carries a
+# compact line of at most LINE_MAX bytes: the headline fields, roofline,
+# cpu_baseline, the parity / digest booleans and one scalar summary per extra
+# workload and socket mode.  The full result dict goes to the detail file.
+LINE_MAX = 4096
+DETAIL_PATH = os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+
+
+def write_detail(full):
+    """the full result dict (per-burst arrays, phase maps, O0 / nproc legs,
+    per_rank) as JSON in gpurun_out/ (BENCH_DETAIL overrides); returns the
+    path, or None if it could not be written (reported on stderr)"""
+    path = os.environ.get("BENCH_DETAIL", DETAIL_PATH)
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        log(f"bench: full detail in {path}")
+        return path
+    except OSError as e:
+        log(f"bench: detail file not written ({e}); full line follows on stderr")
+        log(json.dumps(full))
+        return None
+
+
+def _g(d, *ks):
+    """d[k0][k1]... or None"""
+    for k in ks:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return d
+
+
+def _wl_summary(r, peak=HBM_PEAK_GBS):
+    """one extra workload as scalars"""
+    s = dict(mpps=_g(r, "mpps"), gb_per_s=_g(r, "gbps"), ms_per_step=_g(r, "ms_per_step"),
+             frac=round(r["gbps"] / peak, 4) if isinstance(r.get("gbps"), (int, float)) else None,
+             kernel_median_ms=_g(r, "roofline", "kernel", "median_ms"),
+             kernel_frac=_g(r, "roofline", "kernel", "frac"),
+             traffic=_g(r, "roofline", "traffic"),
+             parity_ok=(_g(r, "parity", "mismatches") == 0) if _g(r, "parity") else None,
+             digest_ok=_g(r, "digest", "digest_ok"), counts_match=_g(r, "counts_match"),
+             cpu_mpps=_g(r, "cpu_baseline", "value"),
+             v8_frac=_g(r, "verdict8", "frac"), tx_frac=_g(r, "tx_cksum", "frac"))
+    return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.items()
+            if v is not None}
+
+
+def _sock_summary(s):
+    """one socket-API mode as scalars"""
+    if "error" in s:
+        return dict(error=str(s["error"])[:120])
+    out = dict(mpps=_g(s, "mpps"), overlapped_mpps=_g(s, "overlapped", "mpps"),
+               cpu_mpps=_g(s, "cpu_baseline", "mpps"),
+               d2h_ms=_g(s, "rx_burst_phases_ms", "d2h"),
+               app_lock_wait_ms=_g(s, "overlapped", "app_ms_per_burst", "lock_wait"),
+               received_equal=_g(s, "overlapped", "received_equal"))
+    return {k: v for k, v in out.items() if v is not None}
+
+
+def compact_line(full, limit=LINE_MAX):
+    """the stdout line from the full result dict (see LINE_MAX)"""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "gb_per_s",
+            "ramp_ms")
+    out = {k: full[k] for k in keep if k in full}
+    rf = full.get("roofline") or {}
+    out["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
+                                               "traffic")}
+    if rf.get("kernel"):
+        out["roofline"]["kernel"] = {k: rf["kernel"].get(k) for k in ("name", "median_ms",
+                                                                     "frac")}
+    cb = full.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = dict(
+            value=cb.get("value"), unit=cb.get("unit"), cores=cb.get("cores"),
+            kind=cb.get("kind"),
+            sample=(cb.get("sample_short") or cb.get("sample") or "")[:200],
+            all_cores_mpps=_g(cb, "O2", "all_cores", "mpps"),
+            all_cores_threads=_g(cb, "O2", "all_cores", "threads"),
+            O0_mpps=_g(cb, "O0", "one_core", "mpps"), model=_g(cb, "host", "model"))
+    else:
+        out["cpu_baseline"] = None
+    par = full.get("parity") or {}
+    out["parity"] = dict(checked=par.get("checked"), mismatches=par.get("mismatches"))
+    out["digest_ok"] = _g(full, "digest", "digest_ok")
+    out["counts_match"] = full.get("counts_match")
+    out["hbm_read_ceiling_gbs"] = full.get("hbm_read_ceiling_gbs")
+    if "per_rank" in full:
+        pr = full["per_rank"] or []
+        ms = [p["ms_per_step"] for p in pr]
+        out["ranks"] = dict(n=len(pr), ms_per_step_max=max(ms) if ms else None,
+                            ms_per_step_min=min(ms) if ms else None,
+                            frames_min=min((p["frames"] for p in pr), default=None),
+                            frames_max=max((p["frames"] for p in pr), default=None),
+                            allreduce_ms=full.get("allreduce_ms"),
+                            allreduce_bytes=full.get("allreduce_bytes"))
+    if full.get("verdict8"):
+        v8 = full["verdict8"]
+        out["verdict8"] = dict(mpps=v8.get("mpps"), frac=v8.get("frac"),
+                               ok=bool(v8.get("equals_projection")) and v8.get("digest_ok")
+                               is not False)
+    if full.get("tx_cksum"):
+        out["tx_cksum"] = {k: full["tx_cksum"].get(k) for k in ("mpps", "frac")}
+    if full.get("e2e_pcie"):
+        out["e2e_pcie_mpps"] = full["e2e_pcie"].get("mpps")
+    c1 = full.get("cfg1")
+    if c1:
+        out["cfg1"] = dict(pcie_mpps=_g(c1, "pcie_inclusive", "mpps"),
+                           device_mpps=_g(c1, "device_resident", "mpps"),
+                           cpu_mpps=_g(c1, "cpu_baseline", "value"),
+                           parity_ok=_g(c1, "parity", "mismatches") == 0)
+    for k, v in full.items():
+        if k.startswith("cfg") and k != "cfg1" and isinstance(v, dict):
+            out[k] = _wl_summary(v)
+    if full.get("socket_api"):
+        out["socket_api"] = {m: _sock_summary(s) for m, s in full["socket_api"].items()}
+    # over the limit (never expected): drop the optional parts, least
+    # important first, and say so
+    extra = [k for k in out if k.startswith("cfg") and k != "cfg1"]
+    for drop in ["socket_api", "cfg1", "verdict8", "tx_cksum"] + extra[::-1]:
+        if len(json.dumps(out, separators=(",", ":"))) < limit - 200:
+            break
+        if drop in out:
+            out.pop(drop)
+            out.setdefault("dropped", []).append(drop)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1427,7 +1562,7 @@ def main():
             except Exception as e:  # reported in the line, never silent
                 sock[nm] = dict(error=repr(e))
                 log(f"socket_api {nm} failed: {e!r}")
-    copy_peak = hbm_copy_peak(dev) if rank == 0 and world == 1 else None
+    ceiling = hbm_read_ceiling(local) if rank == 0 and world == 1 else None
 
     if a.e2e and rank == 0:
         pk = pcie_peaks(local)
@@ -1475,7 +1610,7 @@ def main():
             "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
             "counts_ok": head["counts_ok"],
             "counts_match": head["counts_match"],
-            "hbm_copy_peak_gbs": copy_peak,
+            "hbm_read_ceiling_gbs": ceiling,
             "librxgpu_sha256": lib_sha256()[:16],
         }
         if world > 1:
@@ -1496,7 +1631,12 @@ def main():
         for nm in names[1:]:
             r = results[nm]
             line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
-        print(json.dumps(line), file=JSON_OUT, flush=True)
+        # stdout: the compact line (the driver parses a bounded tail of
+        # stdout); every measured detail goes to the detail file
+        path = write_detail(line)
+        short = compact_line(line)
+        short["detail"] = os.path.relpath(path, ROOT) if path else None
+        print(json.dumps(short, separators=(",", ":")), file=JSON_OUT, flush=True)
     ctx.close()
     if group is not None:
         group.close()
