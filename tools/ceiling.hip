@@ -19,7 +19,48 @@ __global__ __launch_bounds__(256) void ceiling_read_kernel(const u32x4 *__restri
     if (acc == 0x9e3779b9u) sink[0] = acc; // keeps the loads; never true for the fill
 }
 
+// one wave spinning for `ticks` of the constant-rate wall clock
+// (s_memrealtime), counting the shader clock (s_memtime) meanwhile
+__global__ void clock_probe_kernel(unsigned long long ticks, unsigned long long *out) {
+    const unsigned long long w0 = wall_clock64(), c0 = clock64();
+    unsigned long long w1 = w0, c1 = c0;
+    while (w1 - w0 < ticks) {
+        __builtin_amdgcn_s_sleep(2);
+        w1 = wall_clock64();
+        c1 = clock64();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = w1 - w0;
+    }
+}
+
 extern "C" {
+
+// the shader clock while the probe runs: launch on `stream` (a HIP stream
+// handle, or null), spinning for `ms`; *state is a device buffer of 2 u64
+// (allocated here when *state is null); read the result with clock_probe_read
+int clock_probe_launch(int device, void *stream, double ms, void **state) {
+    int rate_khz = 0;
+    hipError_t e = hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device);
+    if (e != hipSuccess) return (int)e;
+    if (!*state && (e = hipMalloc(state, 16)) != hipSuccess) return (int)e;
+    const unsigned long long ticks = (unsigned long long)(ms * rate_khz);
+    clock_probe_kernel<<<1, 64, 0, (hipStream_t)stream>>>(ticks, (unsigned long long *)*state);
+    return (int)hipGetLastError();
+}
+
+// after the probe's stream is synchronized: shader-clock MHz (s_memtime
+// ticks per wall microsecond)
+int clock_probe_read(int device, void *state, double *mhz) {
+    int rate_khz = 0;
+    unsigned long long h[2] = {0, 0};
+    hipError_t e = hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device);
+    if (e == hipSuccess) e = hipMemcpy(h, state, 16, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return (int)e;
+    *mhz = h[1] ? (double)h[0] / ((double)h[1] / (rate_khz * 1e-3)) : 0.0;
+    return 0;
+}
 
 // read rate of `nbytes` of HBM on `device` in GB/s (1e9 B/s), median of
 // `reps` timed passes per grid, best grid; 0 on success, else the HIP error

@@ -1,0 +1,59 @@
+#!/bin/bash
+# Round-5 GPU session: parity suite, smoke, the bench exactly as the driver
+# runs it (compact stdout line + the full detail file), rocprofv3
+# --kernel-trace --stats of the bench on the SAME box, and the table tying
+# each workload's roofline.kernel to the trace.  Optional: SWING=1 the cfg2
+# placement / clock probe (tools/cfg2_swing.py) first thing and again after
+# the tests; PMC=1 HBM bytes; N2=1 the N = 2 spawn rehearsal.  Each GPU step
+# has its own time limit; a failing step ends the script.
+#     TAG=r05a bash tools/gpu_r05.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+TAG=${TAG:-r05}
+step() { local name=$1 t=$2; shift 2; echo "== $name: $*"; date +%T; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n 4 "$OUT/$name.log"; return $rc; }
+bench() {  # name limit args...: the line and its detail file kept under the name
+  local name=$1 t=$2; shift 2
+  BENCH_DETAIL=$OUT/detail_${name}_$TAG.json step $name $t python bench.py "$@" || return $?
+  grep '^{' $OUT/$name.log > $OUT/${name}_$TAG.json || true
+}
+if [ "${SWING:-0}" = 1 ]; then
+  step swing_first 240 python tools/cfg2_swing.py || exit $?
+  grep '^{' $OUT/swing_first.log > $OUT/swing_first_$TAG.json || true
+  bench bench_cfg2_first 240 --workload cfg2 --no-cfg1 --no-sockrate --no-tx --no-v8 || exit $?
+fi
+if [ "${TESTS:-1}" = 1 ]; then
+  # plain test failures (rc 1) still let the bench run; anything else (a
+  # timeout, an abort, a fault) ends the session
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 170 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+  rc=$?; [ $rc -le 1 ] || exit $rc
+  step smoke 150 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+fi
+if [ "${SWING:-0}" = 1 ]; then
+  step swing_after 240 python tools/cfg2_swing.py || exit $?
+  grep '^{' $OUT/swing_after.log > $OUT/swing_after_$TAG.json || true
+fi
+export TMPDIR=/tmp
+if [ "${PMC:-0}" = 1 ]; then
+  step pmc 900 python tools/pmc_traffic.py $TAG cfg2,cfg3,cfg4,cfg5 || exit $?
+  cp $OUT/pmc_$TAG.json profiles/pmc_$TAG.json || exit 1
+fi
+if [ "${BENCH:-1}" = 1 ]; then
+  bench bench 420 ${BENCH_ARGS:-} || exit $?
+  BENCH_DETAIL=$OUT/detail_rocprof_$TAG.json step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
+      -- python3 bench.py --no-cpu --no-sockrate --no-v8 --no-cfg1 --no-tx || exit $?
+  grep '^{' $OUT/rocprof.log > $OUT/bench_profiled_$TAG.json || true
+  f=$(find $OUT/prof_$TAG -name '*kernel_trace.csv' | head -1)
+  s=$(find $OUT/prof_$TAG -name '*kernel_stats.csv' | head -1)
+  [ -n "$s" ] && cp "$s" $OUT/kernel_stats_$TAG.csv
+  if [ -n "$f" ]; then
+    python tools/trace_durations.py "$f" > $OUT/trace_durations_$TAG.txt
+    python tools/roofline_check.py $OUT/detail_rocprof_$TAG.json "$f" $OUT/detail_bench_$TAG.json \
+        > $OUT/roofline_check_$TAG.txt 2>&1
+    cat $OUT/roofline_check_$TAG.txt
+  fi
+fi
+if [ "${N2:-0}" = 1 ]; then
+  bench n2 400 --gpus 2 --steps 5 --warmup 2 || exit $?
+fi
+echo ALLDONE

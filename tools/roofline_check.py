@@ -32,9 +32,19 @@ def workloads(line):
     return out
 
 
+def load(path):
+    """a bench detail file (the full dict, bench.py write_detail) or a file
+    whose last line is a full (round <= 4) bench line"""
+    t = open(path).read().strip()
+    try:
+        return json.loads(t)
+    except ValueError:
+        return json.loads(t.splitlines()[-1])
+
+
 def main():
-    line = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-    plain = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1]) if len(sys.argv) > 3 else None
+    line = load(sys.argv[1])
+    plain = load(sys.argv[3]) if len(sys.argv) > 3 else None
     rows = defaultdict(list)
     for r in csv.DictReader(open(sys.argv[2])):
         name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
