@@ -18,7 +18,7 @@
 #include "rx_flows.h"
 
 void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
-bool rx_variant_exists(uint32_t g, uint32_t pipe);
+bool rx_variant_exists(uint32_t g, uint32_t p, uint32_t fpg, uint32_t pipe);
 const char *rx_variant_kernel(uint32_t g, uint32_t pipe);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
                               uint32_t n, uint32_t unit_log2, uint32_t g, uint32_t p, uint32_t fpg,
@@ -1030,7 +1030,7 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
         // size-class binned path (20) / stream kernel variants: anything else
         // would silently run the automatic choice (r02o measured "ablations"
         // that were the default kernel), so it is refused
-        if (pipeline != 20 && !rx_variant_exists(0, pipeline)) return RXG_EINVAL;
+        if (!rx_variant_exists(0, 0, 0, pipeline)) return RXG_EINVAL;
         c->tune_g = 0;
         c->tune_p = c->tune_fpg = 0;
         c->tune_pipe = pipeline;
@@ -1038,6 +1038,11 @@ int rxg_tune(rxg_ctx *c, uint32_t lanes_per_frame, uint32_t passes, uint32_t fra
     }
     if (lanes_per_frame && (lanes_per_frame == 2 || lanes_per_frame > 64 ||
                             (lanes_per_frame & (lanes_per_frame - 1))))
+        return RXG_EINVAL;
+    // a combination that is not compiled in (in the product library: every
+    // tuning shape and ablation of the RX_DIAG build) is refused here, not at
+    // the next burst
+    if (lanes_per_frame && !rx_variant_exists(lanes_per_frame, passes, frames_per_group, pipeline))
         return RXG_EINVAL;
     c->tune_g = lanes_per_frame;
     c->tune_p = lanes_per_frame ? passes : 0;

@@ -11,9 +11,9 @@
 //   stream kernel (rx_classify_stream_kernel) heads per thread, tails streamed
 //                 by the block as one contiguous span with prefix sums: mixed
 //                 sizes (IMIX) and jumbo frames.
-// The variant table (k_variants) also holds tuning shapes and diagnostic
-// ablations (pipe >= 100, wrong verdicts by construction), reachable only
-// through rxg_tune.
+// The variant table (k_variants) holds the defaults and a few measured
+// alternatives; tuning shapes and diagnostic ablations (wrong verdicts by
+// construction) compile only into the RX_DIAG build (librxgpu_diag.so).
 //
 // Group kernel work decomposition
 //   A frame is owned by a lane GROUP of G lanes (G = 4..64, power of two).
@@ -2605,130 +2605,85 @@ struct variant_entry {
 // one-trip pipeline, 2/3 = 0/1 with plain frame loads; pipe >= 100 are
 // diagnostic ablations (wrong verdicts by construction, tuning only).
 static const variant_entry k_variants[] = {
-    // defaults first (measured on MI355X, bench.py --sweep)
+    // The product table: the four defaults (rx_pick_variant) and the measured
+    // alternatives next to them, every one parity-tested (tests/
+    // test_gpu_parity.py runs each).  Experiment variants whose sweeps are
+    // recorded in profiles/ and DESIGN.md were removed from the code;
+    // diagnostic ablations (wrong verdicts or counts by construction) and the
+    // shapes kept for tuning compile only into the RX_DIAG build
+    // (librxgpu_diag.so, Makefile), so no public call on the product library
+    // can return a verdict that differs from the reference's (common.c:97-108,
+    // tcp.c:345-371: the contract every entry keeps).
     // pipe 12 at 4 blocks/CU: with per-flow counts its LDS (stage + UDP table +
     // histogram) allows 4 anyway; without counts 5 fit and ran 36% slower
     // (r01g: 0.255 vs 0.346 ms on cfg2, profiles/r01g/sweep_lane_bpc_counts.txt)
     {1, 4, 1, 12, launch_lane_udpc<12, 0, true, false>, 4},
+    // 5: per-lane head loads, LDS UDP table (the binned path's small-frame kernel)
     {1, 4, 1, 5, launch_lane_udpc<0, 0, true, false>, 6},
-    {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
-    {1, 4, 1, 0, launch_lane<0>},          {1, 4, 1, 1, launch_lane<1>},
-    {1, 4, 1, 2, launch_lane<2>},          {1, 4, 1, 3, launch_lane<3>},
-    {1, 4, 1, 4, launch_lane<0, 0, false>},
-    {1, 4, 1, 6, launch_lane<0, 0, false, false>},
-    {1, 4, 1, 7, launch_lane<1, 0, true, false>}, {1, 4, 1, 8, launch_lane<2, 0, true, false>},
-    {1, 4, 1, 9, launch_lane<9, 0, true, false>}, {1, 4, 1, 10, launch_lane<9, 0, false, false>},
-    {1, 4, 1, 11, launch_lane<0, 0, true, false>, 6}, // 5 without the LDS UDP table
-    // 12 (first entry): 5 with coalesced LDS-staged head loads; 13: 12 without the LDS UDP table
-    {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6},
-    // 14: 12 software-pipelined (descriptors two trips, frame bytes one trip ahead)
+    // 14 (the 64-B default): 12 software-pipelined (descriptors two trips,
+    // frame bytes one trip ahead)
     {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 2},
+    {1, 4, 1, 0, launch_lane<0>},
+    // group kernels, one per G (the first entry per g is its default)
+    {4, 1, 1, 1, launch_v<4, 1, 1, 1>},
+    {8, 2, 2, 0, launch_v<8, 2, 2, 0>},
+    // 40 (the 1500-B default): G=8 with write-through verdict stores (sc1:
+    // the lines leave the L2 instead of staying in it)
+    {8, 2, 2, 40, launch_v<8, 2, 2, 0, true, 0, 1, true>},
+    {8, 2, 1, 0, launch_v<8, 2, 1, 0>},
+    {16, 2, 2, 0, launch_v<16, 2, 2, 0>},
+    {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
+    {64, 4, 1, 0, launch_v<64, 4, 1, 0>},
+    // g = 0: stream kernel (head per lane, tails streamed per block); 30: nt
+    // tail loads; 38: probe after the stream, one barrier per tail tile (B1);
+    // 738 / 938 (the jumbo default): 38 with 32 / 16 frames per block
+    {0, 1, 1, 30, launch_stream<true>},
+    {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>},
+    {0, 1, 1, 738, launch_stream<true, 0, 3, 1, true, false, false, 32>},
+    {0, 1, 1, 938, launch_stream<true, 0, 3, 1, true, false, false, 16>},
+    // SH kernel (heads taken out of the block stream): 60; 64: a four-slot
+    // first probe window; 67 (the IMIX default): 64 with 8-KiB tiles
+    {0, 1, 1, 60, launch_sh<0>},
+    {0, 1, 1, 64, launch_sh<0, 4>},
+    {0, 1, 1, 67, launch_sh<0, 4, SH_MAPC, false, 2>},
+#if RX_DIAG
+    // ---- tuning shapes (correct verdicts; sweeps in profiles/) ----
+    {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6}, // 12 without the LDS UDP table
+    {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
+    {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
+    {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>}, // heads gathered 4 lanes/head
+    {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>},              // 12-KiB tiles
+    {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},        // partial sums in the stream
+    {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},              // two-slot window
+    {0, 1, 1, 65, launch_sh<0, 2, SH_MAPC, true>},                  // probes inside the stream
+    // ---- ablations: wrong verdicts (or counts) by construction ----
+    // lane kernel (ABL bits: 1 = no bucket probe, 4 = no verdict store, 8 = no
+    // checksum arithmetic): 101, 104, 108, 113 = 1|4|8; 2xx: the same with
+    // plain frame loads at 6 blocks/CU
     {1, 4, 1, 101, launch_lane<0, 1>},     {1, 4, 1, 104, launch_lane<0, 4>},
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},
     {1, 4, 1, 213, launch_lane<0, 13, true, false>, 6},
-    {4, 1, 1, 1, launch_v<4, 1, 1, 1>},    {4, 1, 1, 0, launch_v<4, 1, 1, 0>},
-    {4, 1, 1, 3, launch_v<4, 1, 1, 1, false>}, {4, 1, 2, 2, launch_v<4, 1, 2, 0, false>},
-    {4, 1, 2, 0, launch_v<4, 1, 2, 0>},    {4, 1, 2, 1, launch_v<4, 1, 2, 1>},
-    {4, 1, 4, 0, launch_v<4, 1, 4, 0>},
-    {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
-    // 40: the cfg3 default with write-through verdict stores (sc1: the lines
-    // leave the L2 instead of staying in it)
-    {8, 2, 2, 40, launch_v<8, 2, 2, 0, true, 0, 1, true>},
-    {8, 2, 1, 0, launch_v<8, 2, 1, 0>},    {8, 2, 1, 1, launch_v<8, 2, 1, 1>},
-    {16, 2, 2, 0, launch_v<16, 2, 2, 0>},  {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
-    {16, 2, 1, 1, launch_v<16, 2, 1, 1>},  {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
-    {32, 3, 1, 0, launch_v<32, 3, 1, 0>},  {32, 2, 1, 1, launch_v<32, 2, 1, 1>},
-    {64, 4, 1, 0, launch_v<64, 4, 1, 0>},  {64, 2, 1, 0, launch_v<64, 2, 1, 0>},
-    {64, 2, 1, 1, launch_v<64, 2, 1, 1>},
-    // pipe 10 + RI: interleaved remainder, RI passes of every frame per batch
-    {8, 2, 2, 15, launch_v<8, 2, 2, 0, true, 5>},   {8, 2, 2, 14, launch_v<8, 2, 2, 0, true, 4>},
-    {8, 4, 2, 18, launch_v<8, 4, 2, 0, true, 8>},   {8, 4, 1, 18, launch_v<8, 4, 1, 0, true, 8>},
-    {16, 2, 2, 14, launch_v<16, 2, 2, 0, true, 4>}, {16, 2, 2, 18, launch_v<16, 2, 2, 0, true, 8>},
-    {32, 2, 2, 18, launch_v<32, 2, 2, 0, true, 8>}, {32, 2, 1, 18, launch_v<32, 2, 1, 0, true, 8>},
-    {64, 1, 2, 18, launch_v<64, 1, 2, 0, true, 8>}, {64, 1, 1, 18, launch_v<64, 1, 1, 0, true, 8>},
-    // pipe 20 + W: register budget capped for W waves per SIMD; 2 = plain frame loads
-    {8, 2, 2, 26, launch_v<8, 2, 2, 0, true, 0, 6>}, {8, 2, 2, 28, launch_v<8, 2, 2, 0, true, 0, 8>},
-    {8, 2, 1, 28, launch_v<8, 2, 1, 0, true, 0, 8>}, {8, 1, 2, 28, launch_v<8, 1, 2, 0, true, 0, 8>},
-    {8, 2, 2, 2, launch_v<8, 2, 2, 0, false>},
-    {16, 2, 2, 26, launch_v<16, 2, 2, 0, true, 0, 6>}, {16, 2, 2, 28, launch_v<16, 2, 2, 0, true, 0, 8>},
-    // g = 0: stream kernel (head per lane, tails streamed per block); pipe 30 nt
-    // tail loads, 31 plain
-    {0, 1, 1, 30, launch_stream<true>},    {0, 1, 1, 31, launch_stream<false>},
+    // stream kernel: no flow probe (130); pipe 46 (span from the descriptors)
+    // and its ablations: no probe (146), no tail stream (246), no head loads
+    // (446), neither heads nor stream (646); pipe 38: no head loads (438), no
+    // partial-chunk load (838), neither (1238)
     {0, 1, 1, 130, launch_stream<true, 1>},
-    // 32/33/34: pipe 30 with the stream kernel's HO = 1/2/3 (first tile issued
-    // before the probe / the probe after the stream / same at 5 blocks per CU)
-    {0, 1, 1, 32, launch_stream<true, 0, 1>}, {0, 1, 1, 33, launch_stream<true, 0, 2>},
-    {0, 1, 1, 34, launch_stream<true, 0, 3>},
-    // 35/36/37: HO = 0/1/3 with the two-slot first probe (PW = 2)
-    {0, 1, 1, 35, launch_stream<true, 0, 0, 2>}, {0, 1, 1, 36, launch_stream<true, 0, 1, 2>},
-    {0, 1, 1, 37, launch_stream<true, 0, 3, 2>},
-    // 38/39: pipes 34/30 with one barrier per tail tile (B1)
-    {0, 1, 1, 38, launch_stream<true, 0, 3, 1, true>}, {0, 1, 1, 39, launch_stream<true, 0, 0, 1, true>},
-    // 46: pipe 38 with the span from the descriptors (DS: the first tiles
-    // issued while the heads are in flight); the base of the ablations below
     {0, 1, 1, 46, launch_stream<true, 0, 3, 1, true, true>},
-    // diagnostic ablations of pipe 46 (wrong verdicts by construction): no
-    // flow probe (146), no tail stream (246), no head loads (446), neither
-    // heads nor stream (646)
-    // 54: pipe 38 with the heads gathered four lanes per head (HG).  (54 with
-    // a four-slot first probe window, PW = 4, ran 8% slower: 96 VGPRs and the
-    // window held across the stream, profiles/r02ab)
-    {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>},
     {0, 1, 1, 146, launch_stream<true, 1, 3, 1, true, true>},
     {0, 1, 1, 246, launch_stream<true, 2, 3, 1, true, true>},
     {0, 1, 1, 446, launch_stream<true, 4, 3, 1, true, true>},
     {0, 1, 1, 646, launch_stream<true, 6, 3, 1, true, true>},
-    // ablations of pipe 38 (the jumbo default): no head loads (438), no
-    // partial-chunk load (838), neither (1238)
     {0, 1, 1, 438, launch_stream<true, 4, 3, 1, true>}, {0, 1, 1, 838, launch_stream<true, 8, 3, 1, true>},
     {0, 1, 1, 1238, launch_stream<true, 12, 3, 1, true>},
-    // 338 / 538: pipe 38 with 128 / 64 frames per block
-    {0, 1, 1, 338, launch_stream<true, 0, 3, 1, true, false, false, 128>},
-    {0, 1, 1, 538, launch_stream<true, 0, 3, 1, true, false, false, 64>},
-    {0, 1, 1, 738, launch_stream<true, 0, 3, 1, true, false, false, 32>},
-    // 938: 738 with 16 frames per block; 739: pipe 39 (probe consumed before the
-    // stream) with 32
-    {0, 1, 1, 938, launch_stream<true, 0, 3, 1, true, false, false, 16>},
-    // 2938 / 3938: 938 with 8-KiB / 12-KiB tail tiles
-    {0, 1, 1, 2938, launch_stream<true, 0, 3, 1, true, false, false, 16, 2>},
-    {0, 1, 1, 3938, launch_stream<true, 0, 3, 1, true, false, false, 16, 3>},
-
-    {0, 1, 1, 739, launch_stream<true, 0, 0, 1, true, false, false, 32>},
-    // 60: heads taken out of the block stream (SH kernel)
-    // 63 / 64: 60 with a two / four-slot first probe window
-    {0, 1, 1, 60, launch_sh<0>}, {0, 1, 1, 160, launch_sh<1>},
-    {0, 1, 1, 63, launch_sh<0, 2>}, {0, 1, 1, 64, launch_sh<0, 4>},
-    // 65 / 61: probes issued inside the stream (early heads and windows by
-    // LDS-DMA), a two / one-slot window
-    {0, 1, 1, 65, launch_sh<0, 2, SH_MAPC, true>}, {0, 1, 1, 61, launch_sh<0, 1, SH_MAPC, true>},
-    // 66 / 67: 64 with 12-KiB / 8-KiB tiles; 62: 65 with 8-KiB tiles
-    {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>}, {0, 1, 1, 67, launch_sh<0, 4, SH_MAPC, false, 2>},
-    {0, 1, 1, 62, launch_sh<0, 2, SH_MAPC, true, 2>},
-    // 68 / 69: 67 / 66 with partial-chunk sums in the stream (48-B heads:
-    // 68 fits 6 blocks per CU)
-    {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},
-    // 70: 64 with 4-KiB tiles
-    {0, 1, 1, 70, launch_sh<0, 4, SH_MAPC, false, 1>},
-    // 72 / 74 / 76: 67 / 64 / 66 with 64 frames per block (1500-B frames);
-    // 78: 67 with 128 frames per block
-    {0, 1, 1, 72, launch_sh<0, 4, SH_MAPC, false, 2, false, 64>},
-    {0, 1, 1, 74, launch_sh<0, 4, SH_MAPC, false, 4, false, 64>},
-    {0, 1, 1, 76, launch_sh<0, 4, SH_MAPC, false, 3, false, 64>},
-    {0, 1, 1, 78, launch_sh<0, 4, SH_MAPC, false, 2, false, 128>},
-    // 71 / 73: 67 / 70 with three tiles in flight; 75: 67 with a two-slot window
-    {0, 1, 1, 71, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 3>},
-    {0, 1, 1, 73, launch_sh<0, 4, SH_MAPC, false, 1, false, 256, 3>},
-    {0, 1, 1, 75, launch_sh<0, 2, SH_MAPC, false, 2>},
-    // 77: 67 on a resident grid (descriptors one block-tile ahead)
-    {0, 1, 1, 77, launch_sh<0, 4, SH_MAPC, false, 2, false, 256, 2, true>},
-    {0, 1, 1, 69, launch_sh<0, 4, SH_MAPC, false, 3, true>},
-    // 264: 64 with every partial last chunk loaded from HBM after the stream
-    // (no partial marks; diagnostic)
-    {0, 1, 1, 264, launch_sh<2, 4>},
-    // 1064: 64 without the count-index store; 2064: 64 with the count index
-    // stored before the verdict (diagnostics; the counts of 1064 are wrong)
+    // SH kernel: no flow probe (160); every partial last chunk from HBM after
+    // the stream (264); no count-index store (1064: counts wrong); the count
+    // index stored before the verdict (2064)
+    {0, 1, 1, 160, launch_sh<1>}, {0, 1, 1, 264, launch_sh<2, 4>},
     {0, 1, 1, 1064, launch_sh<16, 4>}, {0, 1, 1, 2064, launch_sh<32, 4>},
+    // 167: 67 without the flow probe
+    {0, 1, 1, 167, launch_sh<1, 4, SH_MAPC, false, 2>},
+#endif
 };
 
 } // namespace
@@ -2785,10 +2740,14 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
 
 #if !RX_V8
 
-// a compiled variant with this lanes-per-frame and pipeline id (rxg_tune)
-bool rx_variant_exists(uint32_t g, uint32_t pipe) {
+// a compiled variant matching (g, p, fpg, pipe) as rx_classify_launch
+// matches it (p, fpg = 0: any; pipe = ~0: any) (rxg_tune)
+bool rx_variant_exists(uint32_t g, uint32_t p, uint32_t fpg, uint32_t pipe) {
+    if (g == 0 && pipe == 20) return true; // size-class binned path
     for (const variant_entry &v : k_variants)
-        if (v.g == g && v.pipe == pipe) return true;
+        if (v.g == g && (p == 0 || v.p == p) && (fpg == 0 || v.fpg == fpg) &&
+            (pipe == 0xFFFFFFFFu || v.pipe == pipe))
+            return true;
     return false;
 }
 #endif

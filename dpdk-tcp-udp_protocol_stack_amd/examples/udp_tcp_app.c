@@ -12,7 +12,7 @@
  *     source (offload.length = dgram_len, udp.c:37);
  *   - a SYN, its handshake ACK and PSH data in later bursts establish a
  *     connection that naccept returns and whose nrecv reads the data;
- *   - a frame with a corrupted TCP checksum is dropped (rc -3, tcp.c:349-351);
+ *   - a frame with a corrupted TCP checksum is dropped (rc -1, RXG_RC_TCP_BAD_CKSUM: tcp.c:349-357);
  *   - the TX pass encodes the SYN|ACK and the data ACK with GPU checksums.
  * Exit 0 and "udp_tcp_app ok" on success.  Needs a GPU (device 0).
  */

@@ -604,6 +604,9 @@ void nstack_fini(void) {
     s_tcb_id = NULL, s_handled = NULL;
     s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = s_udp_xcap = s_tcb_xcap = s_handled_cap = 0;
     memset(g_stat, 0, sizeof(g_stat));
+    /* every counter nstack_stat reports describes the current stack */
+    g_stale_parts = g_copied_bytes = g_pl_waits = 0;
+    for (int j = 0; j < 3; j++) atomic_store_explicit(&g_drain_ns[j], 0, memory_order_relaxed);
     g_isn_seed = 0;
     while (g_arp) {
         struct arp_entry *e = g_arp;

@@ -47,37 +47,25 @@ TCP_STATUS_LISTEN, TCP_STATUS_ESTABLISHED = 1, 4
 HOST_ONLY = -1
 # (lanes per frame, passes up front, frames per group, pipeline) compiled in
 # rx_classify.hip (verdict-exact ones; the >= 100 pipeline ids are ablations)
-KERNEL_VARIANTS = [(1, 4, 1, 0), (1, 4, 1, 1), (1, 4, 1, 2), (1, 4, 1, 3), (1, 4, 1, 4),
-                   (1, 4, 1, 5), (1, 4, 1, 6), (1, 4, 1, 7), (1, 4, 1, 8), (1, 4, 1, 9), (1, 4, 1, 10),
-                   (1, 4, 1, 11), (1, 4, 1, 12), (1, 4, 1, 13), (1, 4, 1, 14),
-                   (4, 1, 1, 1), (4, 1, 1, 0), (4, 1, 1, 3), (4, 1, 2, 2), (4, 1, 2, 0), (4, 1, 2, 1), (4, 1, 4, 0),
-                   (8, 2, 2, 0), (8, 2, 2, 1), (8, 2, 2, 40), (8, 2, 1, 0), (8, 2, 1, 1), (16, 2, 2, 0),
-                   (16, 2, 1, 0), (16, 2, 1, 1), (32, 3, 2, 0), (32, 3, 1, 0), (32, 2, 1, 1),
-                   (64, 4, 1, 0), (64, 2, 1, 0), (64, 2, 1, 1),
-                   # pipeline 10 + RI: interleaved remainder passes (RI per frame per batch)
-                   (8, 2, 2, 15), (8, 2, 2, 14), (8, 4, 2, 18), (8, 4, 1, 18), (16, 2, 2, 14),
-                   (16, 2, 2, 18), (32, 2, 2, 18), (32, 2, 1, 18), (64, 1, 2, 18), (64, 1, 1, 18),
-                   # pipeline 20 + W: capped at W waves per SIMD; (8, 2, 2, 2): plain loads
-                   (8, 2, 2, 26), (8, 2, 2, 28), (8, 2, 1, 28), (8, 1, 2, 28), (8, 2, 2, 2),
-                   (16, 2, 2, 26), (16, 2, 2, 28),
+# the product library's classify variants (csrc/rx_classify.hip k_variants):
+# (lanes per frame, passes, frames per group, pipeline); every one gives the
+# reference's verdicts (tests/test_gpu_parity.py runs each)
+KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 0),
+                   (4, 1, 1, 1), (8, 2, 2, 0), (8, 2, 2, 40), (8, 2, 1, 0), (16, 2, 2, 0),
+                   (32, 3, 2, 0), (64, 4, 1, 0),
                    (0, 0, 0, 20),  # size-class binned: lane kernel + G=8 kernel
-                   (0, 0, 0, 30), (0, 0, 0, 31),  # stream kernel
-                   (0, 0, 0, 32), (0, 0, 0, 33), (0, 0, 0, 34),  # stream kernel, probe order HO=1/2/3
-                   (0, 0, 0, 35), (0, 0, 0, 36), (0, 0, 0, 37),  # two-slot first probe
-                   (0, 0, 0, 38), (0, 0, 0, 39),  # one barrier per tail tile
-                   (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),  # 38: 128 / 64 / 32 / 16 frames per block
-                   (0, 0, 0, 739),  # 39 with 32 frames per block
-                   (0, 0, 0, 46),  # 38 with the span from the descriptors
-                   (0, 0, 0, 54),  # 38 with heads gathered four lanes per head
-                   (0, 0, 0, 60),  # heads taken out of the block stream
-                   (0, 0, 0, 63), (0, 0, 0, 64),  # 60 with a 2 / 4-slot probe window
-                   (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 70),  # 64 with 12 / 8 / 4-KiB tiles
-                   (0, 0, 0, 72), (0, 0, 0, 74), (0, 0, 0, 76), (0, 0, 0, 78),  # 64 / 128 frames per block
-                   (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),  # three tiles in flight, two-slot window
-                   (0, 0, 0, 2938), (0, 0, 0, 3938),  # jumbo stream kernel with 8 / 12-KiB tiles
-                   (0, 0, 0, 77),  # 67 on a resident grid
-                   (0, 0, 0, 68), (0, 0, 0, 69),  # 67 / 66 with partial-chunk sums in the stream
-                   (0, 0, 0, 65), (0, 0, 0, 61), (0, 0, 0, 62)]  # probes inside the stream (LDS-DMA)
+                   (0, 0, 0, 30), (0, 0, 0, 38), (0, 0, 0, 738), (0, 0, 0, 938),  # stream kernel
+                   (0, 0, 0, 60), (0, 0, 0, 64), (0, 0, 0, 67)]  # SH kernel
+# compiled only into the RX_DIAG build (librxgpu_diag.so, RXGPU_LIB=...):
+# tuning shapes with correct verdicts ...
+DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (8, 2, 2, 1), (16, 2, 1, 0), (0, 0, 0, 54), (0, 0, 0, 66),
+                        (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65)]
+# ... and ablations, wrong verdicts (or counts) by construction
+DIAG_ABLATIONS = [(1, 4, 1, 101), (1, 4, 1, 104), (1, 4, 1, 108), (1, 4, 1, 113), (1, 4, 1, 201),
+                  (1, 4, 1, 204), (1, 4, 1, 213), (0, 0, 0, 130), (0, 0, 0, 46), (0, 0, 0, 146),
+                  (0, 0, 0, 246), (0, 0, 0, 446), (0, 0, 0, 646), (0, 0, 0, 438), (0, 0, 0, 838),
+                  (0, 0, 0, 1238), (0, 0, 0, 160), (0, 0, 0, 264), (0, 0, 0, 1064),
+                  (0, 0, 0, 2064), (0, 0, 0, 167)]
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
@@ -1004,3 +992,26 @@ class NStack:
         if r < 0:
             _check(r, "nstack_tx_burst")
         return [pk[int(o) << 6:(int(o) << 6) + int(n)].tobytes() for o, n in zip(off[:r], ln[:r])]
+
+
+_COMPILED = {}
+
+
+def compiled_variants(vs):
+    """the variants of `vs` the loaded library has compiled in, in order
+    (the product library: KERNEL_VARIANTS; the RX_DIAG build, RXGPU_LIB=
+    .../librxgpu_diag.so: also its tuning shapes and ablations)"""
+    out = []
+    with Context(HOST_ONLY) as c:
+        for v in vs:
+            v = tuple(v)
+            if v not in _COMPILED:
+                try:
+                    c.tune(*v)
+                    _COMPILED[v] = True
+                except RxgError:
+                    _COMPILED[v] = False
+            if _COMPILED[v]:
+                out.append(v)
+        c.tune(0)
+    return out

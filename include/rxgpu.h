@@ -461,9 +461,11 @@ int rxg_tx_cksum(rxg_ctx *ctx, uint8_t *pkts, uint64_t span_bytes, const uint32_
  * default pipeline); lanes_per_frame = 0 with pipeline 0xFFFFFFFF =
  * automatic from len_hint; lanes_per_frame = 0 with any other pipeline =
  * that frame-size-independent variant (20: size-class binned path; 30 and
- * up: stream kernel variants, >= 100 diagnostic ablations; csrc/
- * rx_classify.hip k_variants), RXG_EINVAL if it is not compiled in.  Unknown
- * lanes_per_frame > 0 combinations make the next burst fail with RXG_EHIP. */
+ * up: stream and SH kernel variants; csrc/rx_classify.hip k_variants).  A
+ * combination that is not compiled in returns RXG_EINVAL.  Every variant of
+ * the product library gives the same verdicts; diagnostic ablations (wrong
+ * verdicts by construction) exist only in the RX_DIAG tuning build
+ * (librxgpu_diag.so), never in librxgpu.so. */
 int rxg_tune(rxg_ctx *ctx, uint32_t lanes_per_frame, uint32_t passes, uint32_t frames_per_group,
              uint32_t pipeline);
 

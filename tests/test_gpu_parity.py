@@ -203,7 +203,7 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got8.tobytes() == want8.tobytes(), (variant, "v8", _mismatch_report(got8, want8))
 
 
-@pytest.mark.parametrize("variant", [(1, 4, 1, 12), (1, 4, 1, 14)])
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
@@ -233,8 +233,8 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
-@pytest.mark.parametrize("variant", [(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
-                                     (0, 0, 0, 20)])
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
+                                     (0, 0, 0, 20)]))
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("far", [False, True])
 def test_udp_port_window(ctx, torch_dev, variant, tables, far):
@@ -288,13 +288,13 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
 
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("load_log2", [1, 4])
-@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
+@pytest.mark.parametrize("variant", R.compiled_variants([(0, 0, 0, 30), (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 38),
                                      (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 60),
                                      (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65), (0, 0, 0, 61),
                                      (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
                                      (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78),
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
-                                     (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)])
+                                     (8, 2, 2, 0), (1, 4, 1, 0), (4, 1, 2, 0)]))
 def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
     """verdicts and counts do not depend on the flow-table layout: load factor
     (rxg_tune_flow_load: longer probe chains at <= 1/2, sparse tables at
@@ -330,7 +330,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
 
 
 @pytest.mark.parametrize("layout", ["packed", "block_shuffled", "scattered", "gapped"])
-@pytest.mark.parametrize("variant", [(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
+@pytest.mark.parametrize("variant", R.compiled_variants([(0, 0, 0, 30), (0, 0, 0, 31), (0, 0, 0, 32), (0, 0, 0, 33),
                                      (0, 0, 0, 34), (0, 0, 0, 35), (0, 0, 0, 37), (0, 0, 0, 38),
                                      (0, 0, 0, 39), (0, 0, 0, 46), (0, 0, 0, 54), (0, 0, 0, 20),
                                      (0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
@@ -339,7 +339,7 @@ def test_flow_table_load_factor(ctx, torch_dev, variant, load_log2, tables):
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
                                      (4, 1, 2, 0),
                                      (0, 0, 0, 338), (0, 0, 0, 538), (0, 0, 0, 738), (0, 0, 0, 938),
-                                     (0, 0, 0, 739), (0, 0, 0, 2938), (0, 0, 0, 3938), (0, 0, 0, 77)])
+                                     (0, 0, 0, 739), (0, 0, 0, 2938), (0, 0, 0, 3938), (0, 0, 0, 77)]))
 def test_layouts_match_oracle(ctx, torch_dev, layout, variant):
     """Descriptor orders the stream kernel must handle: packed (streamed),
     frames shuffled inside each 256-frame block (streamed, unordered
@@ -406,11 +406,11 @@ def test_count_paths_accumulate(ctx, torch_dev, nu, nt):
     assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), len(hints) * wcnt)
 
 
-@pytest.mark.parametrize("variant", [(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
+@pytest.mark.parametrize("variant", R.compiled_variants([(0, 0, 0, 60), (0, 0, 0, 63), (0, 0, 0, 64), (0, 0, 0, 65),
                                      (0, 0, 0, 61), (0, 0, 0, 66), (0, 0, 0, 67), (0, 0, 0, 62), (0, 0, 0, 68), (0, 0, 0, 69),
                                      (0, 0, 0, 70), (0, 0, 0, 72), (0, 0, 0, 76), (0, 0, 0, 78),
                                      (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 75),
-                                     (0, 0, 0, 54)])
+                                     (0, 0, 0, 54)]))
 @pytest.mark.parametrize("case", ["padded", "overlap", "jumbo_mix", "dirty_gaps", "reversed",
                                   "empty"])
 def test_stream_head_fallbacks(ctx, torch_dev, variant, case):
@@ -636,18 +636,16 @@ def test_single_hip_runtime_loaded(ctx):
 
 
 def test_unknown_variant_fails_loudly(ctx, torch_dev):
-    """a tuned combination that is not compiled in fails the burst (RXG_EHIP),
-    never falls back to another kernel silently"""
+    """a tuned combination that is not compiled in is refused (RXG_EINVAL at
+    rxg_tune), never run as another kernel silently; the next burst runs the
+    automatic choice"""
     cfg = rxdist.gen_cfg("cfg4", n_udp=64, n_tcp=64)
     pk, off, ln = R.gen_host(cfg, 0, 256, 6)
     udp, tcb = R.gen_flows(cfg)
     ctx.flows_sync(udp, tcb)
-    ctx.tune(8, 3, 2, 0)
-    try:
-        with pytest.raises(R.RxgError):
-            _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0)
-    finally:
-        ctx.tune(0)
+    with pytest.raises(R.RxgError):  # refused at rxg_tune: not compiled in
+        ctx.tune(8, 3, 2, 0)
+    ctx.tune(0)
     got = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0)
     assert got.tobytes() == O.Tables(udp, tcb).classify(pk, off, ln, 6).tobytes()
 
@@ -718,8 +716,8 @@ def test_count_idx16_all_ones(ctx, torch_dev, nu):
     assert np.array_equal(cnt, want)
 
 
-@pytest.mark.parametrize("variant", [(0, 0, 0, 64), (0, 0, 0, 67), (0, 0, 0, 65), (0, 0, 0, 61),
-                                     (0, 0, 0, 62), (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 68)])
+@pytest.mark.parametrize("variant", R.compiled_variants([(0, 0, 0, 64), (0, 0, 0, 67), (0, 0, 0, 65), (0, 0, 0, 61),
+                                     (0, 0, 0, 62), (0, 0, 0, 71), (0, 0, 0, 73), (0, 0, 0, 68)]))
 @pytest.mark.parametrize("size", [90, "mixed"])
 def test_sh_short_spans(ctx, torch_dev, variant, size):
     """SH blocks whose span is one to three stream tiles (small frames packed

@@ -5,6 +5,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -118,6 +119,39 @@ def test_tune_refuses_variants_not_compiled_in():
         for v in R.KERNEL_VARIANTS:
             c.tune(*v)
         c.tune(0)
+
+
+def test_product_library_refuses_diagnostic_variants():
+    """wrong-by-construction ablations and the tuning shapes compile only into
+    the RX_DIAG build: the product librxgpu.so refuses every one at rxg_tune,
+    so no public call can return a verdict that differs from the oracle's"""
+    if os.environ.get("RXGPU_LIB"):
+        pytest.skip("another library build is loaded")
+    with R.Context(R.HOST_ONLY) as c:
+        for v in R.DIAG_ABLATIONS + R.DIAG_TUNING_VARIANTS:
+            with pytest.raises(R.RxgError):
+                c.tune(*v)
+        for v in ((1, 4, 1, 99), (8, 2, 2, 26), (16, 2, 2, 14), (4, 1, 4, 0)):
+            with pytest.raises(R.RxgError):
+                c.tune(*v)
+        c.tune(0)
+
+
+def test_diag_library_has_the_ablations():
+    """the RX_DIAG build (make diag) accepts what the product refuses"""
+    import subprocess
+    lib = os.path.join(R._HERE, "librxgpu_diag.so")
+    if not os.path.exists(lib):
+        pytest.skip("librxgpu_diag.so not built (make -C dpdk-tcp-udp_protocol_stack_amd diag)")
+    code = ("import rxgpu as R\n"
+            "with R.Context(R.HOST_ONLY) as c:\n"
+            "    for v in R.KERNEL_VARIANTS + R.DIAG_ABLATIONS + R.DIAG_TUNING_VARIANTS:\n"
+            "        c.tune(*v)\n"
+            "print('ok')\n")
+    env = dict(os.environ, RXGPU_LIB=lib, PYTHONPATH=R._HERE)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
 
 
 def test_flow_load_rejects_out_of_range():
