@@ -927,22 +927,56 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                     ns.rx_burst(fr)
             res["established"] = int(ns.tcb_count()) - 1
         pk, off, ln = R.gen_host(cfg, 0, B, ul)
-        arr, keep = R.NStack.mbufs_over(pk, off, ln, ul)
-        # the frames' memory registered with the stack, as a DPDK application
-        # registers its mbuf pool once (rte_mempool_mem_iter): the GPU pulls
-        # each burst's frames over PCIe instead of a host gather + copy
+        # the mbuf pool: NSET bursts' worth of frames in distinct memory (the
+        # same bytes in each), registered with the stack once, as a DPDK
+        # application registers its mempool (rte_mempool_mem_iter): the GPU
+        # pulls each burst's frames over PCIe instead of a host gather + copy.
+        # In place (the default here, nstack_set_rx_inplace), a connection's
+        # receive fragments point into these frames and hold their mbufs
+        # (refcnt) until the application has read them, so a set is reused
+        # only once every one of its counts is back to 0 (the NIC refilling
+        # its ring from free mbufs)
+        NSET = 4
+        span = len(pk)
+        pool = np.empty(NSET * span, np.uint8)
+        sets = []
+        for j in range(NSET):
+            seg = pool[j * span:(j + 1) * span]
+            seg[:] = pk
+            a_j, k_j = R.NStack.mbufs_over(seg, off, ln, ul)
+            rc_j = np.frombuffer(k_j, np.uint8).reshape(B, 128)[:, 18:20].view(np.uint16)
+            rc_j[:] = 0  # the pool keeps no reference of its own: free at count 0
+            sets.append((a_j, k_j, rc_j))
         try:
-            ns.register_host(pk.ctypes.data, pk.nbytes)
+            ns.register_host(pool.ctypes.data, pool.nbytes)
             res["pool_registered"] = True
         except R.RxgError as e:  # reported, and the host gather carries the bursts
             res["pool_registered"] = repr(e)
+        ns.set_rx_inplace(True)
+        res["tcp_inplace"] = True
+        kset = [0]
+        pool_waits = [0]
+
+        def next_set():
+            """the next mbuf set whose frames no fragment holds any more"""
+            a_j, _, rc_j = sets[kset[0] % NSET]
+            kset[0] += 1
+            if rc_j.any():
+                pool_waits[0] += 1
+                t_end = time.perf_counter() + 5.0
+                while rc_j.any():
+                    if time.perf_counter() > t_end:
+                        raise RuntimeError("mbuf set still held after 5 s")
+                    time.sleep(0)
+            return a_j
         rbuf = np.zeros(65536, np.uint8)
-        ns.rx_burst_mbufs(arr, B)  # warm (staging, tables committed)
+        ns.rx_burst_mbufs(next_set(), B)  # warm (staging, tables committed)
         ns.drain_all(rbuf)
         t_rx = t_dr = 0.0
         items = nbytes = delivered = 0
         phases = []
         for _ in range(K):
+            arr = next_set()
             t0 = time.perf_counter()
             delivered += ns.rx_burst_mbufs(arr, B)
             t1 = time.perf_counter()
@@ -963,6 +997,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             h_items = 0
             h_ph = []
             for _ in range(K):
+                arr = next_set()
                 t0 = time.perf_counter()
                 ns.rx_burst_mbufs(arr, B)
                 t1 = time.perf_counter()
@@ -976,6 +1011,11 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         received_equal=h_items == items,
                         rx_burst_phases_ms={k: round(float(np.median([p[k] for p in h_ph])), 4)
                                             for k in h_ph[0]})
+        # A/B: payloads gathered on the GPU and copied back into pooled pinned
+        # buffers (the round-4 default)
+        ns.set_rx_inplace(False)
+        res["pooled_payload"] = ab_run()
+        ns.set_rx_inplace(True)
         # A/B: each burst as two halves, both on the GPU at once
         # (nstack_set_halves; off by default)
         ns.set_halves(B // 2)
@@ -1027,8 +1067,10 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             t0 = time.perf_counter()
             th.start()
             ov_rx, ov_ph, ov_cp, ov_tr = [], [], [], []
+            w_pool0 = pool_waits[0]
             try:
                 for _ in range(K):
+                    arr = next_set()
                     a0 = time.perf_counter()
                     ns.rx_burst_mbufs(arr, B)
                     ov_rx.append(time.perf_counter() - a0)
@@ -1046,6 +1088,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         stale_bursts=int(ns.stat(5)) - s0,
                         copied_payload_bytes=int(ns.stat(6)) - c0,
                         bursts_waited_for_buffer=int(ns.stat(11)) - pw0,
+                        bursts_waited_for_mbufs=pool_waits[0] - w_pool0,
                         copied_mb_by_burst=[round((b - a) / 1e6, 1) for a, b in zip([c0] + ov_cp, ov_cp)],
                         drained_and_held_by_burst=ov_tr,
                         app_ms_per_burst={k: round((int(ns.stat(8 + j)) - w0[j]) / 1e6 / K, 3) for j, k in
@@ -1099,7 +1142,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                                           f"oracle_rx per frame + every socket read; host "
                                           f"{cores['model']}")
         res["vs_cpu"] = round(res["mpps"] / max(res["cpu_baseline"]["mpps"], 1e-9), 2)
-    del keep
+    del sets, pool
     return res
 
 
@@ -1333,6 +1376,7 @@ def _sock_summary(s):
         return dict(error=str(s["error"])[:120])
     out = dict(mpps=_g(s, "mpps"), overlapped_mpps=_g(s, "overlapped", "mpps"),
                cpu_mpps=_g(s, "cpu_baseline", "mpps"),
+               pooled_mpps=_g(s, "pooled_payload", "mpps"),
                d2h_ms=_g(s, "rx_burst_phases_ms", "d2h"),
                app_lock_wait_ms=_g(s, "overlapped", "app_ms_per_burst", "lock_wait"),
                received_equal=_g(s, "overlapped", "received_equal"))

@@ -182,6 +182,7 @@ struct rxg_ctx {
     uint64_t use_clock = 0;
     uint32_t tune_tables = 0; // rxg_tune_tables flags
     uint32_t tune_ingest = RXG_INGEST_AUTO; // rxg_tune_ingest
+    uint32_t deliver_flags = 0;             // rxg_tune_deliver (RXG_DLV_*)
     rx_ft_dev ft{};
     uint32_t tune_g = 0, tune_p = 0, tune_fpg = 0, tune_pipe = ~0u; // rxg_tune override
     uint32_t tune_bpc = 0; // rxg_tune_grid: resident blocks per CU cap (0 = occupancy)
@@ -1125,6 +1126,12 @@ int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
     return RXG_OK;
 }
 
+int rxg_tune_deliver(rxg_ctx *c, uint32_t flags) {
+    if (!c || (flags & ~RXG_DLV_TCP_IN_PLACE)) return RXG_EINVAL;
+    c->deliver_flags = flags;
+    return RXG_OK;
+}
+
 int rxg_tune_ingest(rxg_ctx *c, uint32_t mode) {
     if (!c || mode > RXG_INGEST_GATHER) return RXG_EINVAL;
     c->tune_ingest = mode;
@@ -1708,8 +1715,8 @@ int rxg_tcp_compact_dev(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d_off
                         uint64_t payload_cap, uint32_t *d_totals, void *stream) {
     if (!c) return RXG_EINVAL;
     if (c->device == RXG_HOST_ONLY) return RXG_ENODEV;
-    if (!d_totals || (n && (!d_pkts || !d_off || !d_len || !d_v || !d_seg || !d_payload)))
-        return RXG_EINVAL;
+    if (!d_totals || (n && (!d_pkts || !d_off || !d_len || !d_v || !d_seg)))
+        return RXG_EINVAL; // (d_payload null: records only, RXG_DLV_TCP_IN_PLACE)
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     DEVGUARD(c);
     return segsort_impl(c, d_pkts, d_off, d_len, n, off_unit_log2, reinterpret_cast<const uint4 *>(d_v),
@@ -1765,10 +1772,13 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
     // the TCP payloads of this burst: a free pooled buffer (a hold the caller
     // can take, rxg_payload_hold), else the set's own one (valid until the
     // set is reused: tcp_payload_ref = -1).  The library's hold on the
-    // buffer of this set's previous burst ends here.
+    // buffer of this set's previous burst ends here.  In place
+    // (RXG_DLV_TCP_IN_PLACE): no payload is gathered or copied back; the
+    // payloads stay in the caller's frames.
+    const bool inplace = (c->deliver_flags & RXG_DLV_TCP_IN_PLACE) != 0;
     if (ds.pl >= 0) c->pl[ds.pl].refs.fetch_sub(1, std::memory_order_acq_rel);
     ds.pl = -1;
-    for (int k = 0; k < RXG_PAYLOAD_BUFS && ds.pl < 0; ++k) {
+    for (int k = 0; k < RXG_PAYLOAD_BUFS && ds.pl < 0 && !inplace; ++k) {
         rxg_ctx::pl_buf &b = c->pl[k];
         if (b.refs.load(std::memory_order_acquire) != 0) continue;
         if (!b.h && hipHostMalloc((void **)&b.h, c->max_bytes, 0) != hipSuccess) {
@@ -1779,10 +1789,11 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
         b.refs.store(1, std::memory_order_release);
         ds.pl = k;
     }
-    if (ds.pl < 0 && !ds.h_ss_payload) HIPCHK(hipHostMalloc((void **)&ds.h_ss_payload, c->max_bytes, 0));
+    if (ds.pl < 0 && !inplace && !ds.h_ss_payload)
+        HIPCHK(hipHostMalloc((void **)&ds.h_ss_payload, c->max_bytes, 0));
     d->seg = ds.h_ss_seg;
     d->tcp_payload_ref = ds.pl;
-    d->tcp_payload = ds.pl >= 0 ? c->pl[ds.pl].h : ds.h_ss_payload;
+    d->tcp_payload = inplace ? nullptr : ds.pl >= 0 ? c->pl[ds.pl].h : ds.h_ss_payload;
     d->set = si + 1;
     if (udp) {
         d->dgram = ds.h_cp_dg;
@@ -1820,7 +1831,8 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
         tcp = c->fs.tcp.id_space() > 0;
         if (tcp)
             if ((rc = segsort_impl(c, sl.d_pkts, sl.d_off, sl.d_len, n, st.ul, sl.d_out, c->d_ss_seg,
-                                   c->d_ss_payload, c->max_bytes, c->d_ss_totals, c->stream)))
+                                   inplace ? nullptr : c->d_ss_payload, c->max_bytes,
+                                   c->d_ss_totals, c->stream)))
                 return rc;
         HIPCHK(hipEventRecord(ds.tev[3], c->stream)); // after K3 / K4
         // every result in one round trip: the counts with upper-bound copies of
@@ -1843,8 +1855,9 @@ int rxg_deliver_submit(rxg_ctx *c, rxg_mbuf *const *m, uint32_t n, rxg_verdict *
                                   hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(ds.h_ss_seg, c->d_ss_seg, (size_t)n * sizeof(rxg_segment),
                                   hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
-                                  hipMemcpyDeviceToHost, c->stream));
+            if (!inplace)
+                HIPCHK(hipMemcpyAsync(const_cast<uint8_t *>(d->tcp_payload), c->d_ss_payload, pos,
+                                      hipMemcpyDeviceToHost, c->stream));
         }
         HIPCHK(hipEventRecord(ds.tev[4], c->stream)); // after the results' copy out
         return RXG_OK;

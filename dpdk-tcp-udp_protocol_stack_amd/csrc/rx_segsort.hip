@@ -165,6 +165,7 @@ __global__ __launch_bounds__(SS_THREADS) void ss_scatter_kernel(
 // tcp.c:153-166; the captured part); the block's exclusive scan of the
 // 16-B-padded payload sizes gives each its offset inside the block's slice,
 // tsum[block] the slice's size (0 for blocks past the count)
+template <bool INPLACE>
 __global__ __launch_bounds__(SS_THREADS) void ss_record_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t unit_log2, const uint32_t *__restrict__ keys,
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(SS_THREADS) void ss_record_kernel(
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t j = blockIdx.x * SS_THREADS + t;
     if (blockIdx.x * SS_THREADS >= nseg) { // (uniform)
-        if (t == 0u) tsum[blockIdx.x] = 0u;
+        if (t == 0u && !INPLACE) tsum[blockIdx.x] = 0u;
         return;
     }
     rxg_segment s;
@@ -200,6 +201,13 @@ __global__ __launch_bounds__(SS_THREADS) void ss_record_kernel(
         const uint32_t keep = ((s.flags & 0x08u) && s.plen > 0) ? min((uint32_t)s.plen, avail) : 0u;
         s.ncopy = (uint16_t)keep;
         padded = (keep + 15u) & ~15u;
+    }
+    if constexpr (INPLACE) { // the payload stays in the frame: bytes [34 + 4*hl, + ncopy)
+        if (j < nseg) {
+            s.offset = 34u + 4u * s.hl;
+            seg[j] = s;
+        }
+        return;
     }
     const uint32_t inc = ss_wave_scan(padded);
     if (lane == 63u) ws[w] = inc;
@@ -310,7 +318,12 @@ hipError_t rx_segsort_launch(const uint8_t *pkts, const uint32_t *off, const uin
         kout = (kout == ka) ? kb : ka;
         vout = (vout == va) ? vb : va;
     }
-    hipLaunchKernelGGL(ss_record_kernel, dim3(nblk), dim3(SS_THREADS), 0, s, pkts, off, len,
+    if (!payload) { // in place: records only, offset = the payload's offset in its frame
+        hipLaunchKernelGGL(ss_record_kernel<true>, dim3(nblk), dim3(SS_THREADS), 0, s, pkts, off,
+                           len, unit_log2, kin, vin, totals, seg, tsum);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(ss_record_kernel<false>, dim3(nblk), dim3(SS_THREADS), 0, s, pkts, off, len,
                        unit_log2, kin, vin, totals, seg, tsum);
     hipLaunchKernelGGL(ss_scan_kernel, dim3(1), dim3(1024), 0, s, tsum, nblk, totals + 1);
     hipLaunchKernelGGL(ss_copy_kernel, dim3((uint32_t)(((uint64_t)n + 3) / 4)), dim3(SS_THREADS), 0,

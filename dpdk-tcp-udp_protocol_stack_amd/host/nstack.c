@@ -101,6 +101,8 @@ struct localhost {
     pthread_mutex_t mutex;
     uint32_t flow_id; /* stable id in the GPU flow tables (verdict flow_id) */
     uint32_t queued;  /* datagrams in rcvbuf (a batch item holds several) */
+    atomic_int ref;   /* the lists' reference + one per reader (cb_get / udp_put) */
+    int dead;         /* unlinked (nclose): readers return, the last put frees */
 };
 
 struct dgram_batch;
@@ -155,6 +157,9 @@ struct tcp_stream {
     pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
     uint32_t flow_id;           /* stable id in the GPU flow tables (verdict flow_id) */
     uint32_t rq, sq;            /* fragments in rcvbuf / sndbuf (a batch item holds several) */
+    atomic_int ref;             /* the lists' reference + one per reader (cb_get / tcb_put) */
+    int dead;                   /* unlinked (last ACK, nclose): readers return, the last
+                                   put frees */
 };
 
 struct frag_batch;
@@ -169,6 +174,8 @@ struct tcp_fragment {
     uint32_t length;
     struct frag_batch *batch; /* non-NULL: this ring item is a burst's fragments for the
                                  tcb, in one allocation (GPU segment sort) */
+    rxg_mbuf *mb;             /* in-place delivery: data points into this mbuf's frame,
+                                 held (refcnt) until the fragment's item is freed */
 };
 
 /* The fragments one burst queues on one tcb (its receive fragments, or the
@@ -204,8 +211,23 @@ static uint64_t g_pl_waits; /* submits that waited for a buffer (stat 11) */
 /* drain_all's time, ns (stats 8-10): waiting for the stack's lock, stepping
  * aside for the protocol thread, reading the taken-out fragments */
 static atomic_llong g_drain_ns[3];
+/* In-place TCP delivery (nstack_set_rx_inplace): a receive fragment whose
+ * payload was captured whole points into its frame and holds the frame's mbuf
+ * (refcnt@18, as rte_mbuf_refcnt_update) until the application has read it;
+ * the put that drops the count to 0 hands the mbuf to g_mb_release (the
+ * mempool's free, rte_pktmbuf_free). */
+static int g_inplace;
+static void (*g_mb_release)(rxg_mbuf *m, void *arg);
+static void *g_mb_arg;
+static inline void mb_get(rxg_mbuf *m) { __atomic_fetch_add(&m->refcnt, 1, __ATOMIC_RELAXED); }
+static inline void mb_put(rxg_mbuf *m) {
+    if (__atomic_fetch_sub(&m->refcnt, 1, __ATOMIC_ACQ_REL) == 1 && g_mb_release)
+        g_mb_release(m, g_mb_arg);
+}
 static void frag_item_free(struct tcp_fragment *f) {
     if (f->batch) {
+        for (uint32_t j = 0; j < f->batch->n; j++)
+            if (f->batch->frag[j].mb) mb_put(f->batch->frag[j].mb);
         if (f->batch->pl_ref >= 0) {
             rxg_payload_release(g_ctx, f->batch->pl_ref);
             atomic_fetch_sub_explicit(&g_pl_batches, 1, memory_order_relaxed);
@@ -218,7 +240,10 @@ static void frag_item_free(struct tcp_fragment *f) {
         }
         free(f->batch); /* (fragments and payloads live in the batch's allocation) */
     } else {
-        free(f->data);
+        if (f->mb)
+            mb_put(f->mb);
+        else
+            free(f->data);
         free(f);
     }
 }
@@ -270,6 +295,7 @@ static struct tcp_fragment *tq_detach(struct nring *r, uint32_t *cnt) {
     *c = *m;
     c->batch = NULL;
     c->data = NULL;
+    c->mb = NULL; /* (a copy: the batch keeps its hold on the frame until it is freed) */
     if (m->data) {
         c->data = malloc((size_t)m->length + 1);
         if (!c->data) {
@@ -303,6 +329,74 @@ static void tq_clear(struct nring *r, uint32_t *cnt) {
         if ((list) == (item)) (list) = (item)->next;                                               \
         (item)->prev = (item)->next = NULL;                                                        \
     } while (0)
+
+/* ---- control-block lifetime ----------------------------------------------
+ * A block carries a reference count: one for being linked (lists, id and fd
+ * maps, flow tables) and one per application call that uses it after the
+ * stack's lock is released (nrecv / nrecvfrom / nsendto / naccept /
+ * drain_all take theirs under the lock, where the block is still linked).
+ * Freeing a block (nclose, the last ACK of LAST_ACK) unlinks it under the
+ * lock, marks it dead and wakes its waiters, then drops the linked reference;
+ * whoever drops the last one frees the memory.  So a reader blocked in nrecv
+ * on a connection another thread closes wakes up and returns instead of
+ * waiting on freed memory (the reference has that race: tcp.c:312-331
+ * frees the tcb under a concurrent nrecv, common.c:476-481). */
+static void udp_destroy(struct localhost *h) {
+    void *p;
+    while (ring_dequeue(h->rcvbuf, &p) == 0) offload_free(p);
+    while (ring_dequeue(h->sndbuf, &p) == 0) {
+        free(((struct offload *)p)->data);
+        free(p);
+    }
+    ring_free(h->rcvbuf);
+    ring_free(h->sndbuf);
+    pthread_cond_destroy(&h->cond);
+    pthread_mutex_destroy(&h->mutex);
+    free(h);
+}
+static void tcb_destroy(struct tcp_stream *s) {
+    tq_clear(s->rcvbuf, &s->rq);
+    tq_clear(s->sndbuf, &s->sq);
+    ring_free(s->rcvbuf);
+    ring_free(s->sndbuf);
+    pthread_cond_destroy(&s->cond);
+    pthread_cond_destroy(&s->accept_cond);
+    pthread_mutex_destroy(&s->mutex);
+    free(s);
+}
+static inline void cb_ref_init(atomic_int *ref) { atomic_init(ref, 1); }
+static inline void cb_get(atomic_int *ref) { atomic_fetch_add_explicit(ref, 1, memory_order_relaxed); }
+static void udp_put(struct localhost *h) {
+    if (atomic_fetch_sub_explicit(&h->ref, 1, memory_order_acq_rel) == 1) udp_destroy(h);
+}
+static void tcb_put(struct tcp_stream *s) {
+    if (atomic_fetch_sub_explicit(&s->ref, 1, memory_order_acq_rel) == 1) tcb_destroy(s);
+}
+/* a block of either kind (the protocol byte sits at the same offset in both,
+ * as get_hostinfo_fromfd assumes, common.c:111-143) */
+static void cb_put(void *cb) {
+    if (((struct localhost *)cb)->protocol == IPPROTO_UDP)
+        udp_put(cb);
+    else
+        tcb_put(cb);
+}
+/* the block is unlinked (g_lock held): readers wake and return; the linked
+ * reference goes */
+static void udp_kill(struct localhost *h) {
+    pthread_mutex_lock(&h->mutex);
+    h->dead = 1;
+    pthread_cond_broadcast(&h->cond);
+    pthread_mutex_unlock(&h->mutex);
+    udp_put(h);
+}
+static void tcb_kill(struct tcp_stream *s) {
+    pthread_mutex_lock(&s->mutex);
+    s->dead = 1;
+    pthread_cond_broadcast(&s->cond);
+    pthread_mutex_unlock(&s->mutex);
+    pthread_cond_broadcast(&s->accept_cond); /* (naccept waits with g_lock, held here) */
+    tcb_put(s);
+}
 
 /* ---- process-wide state (netfamily.c:16-18) ----------------------------- */
 static struct localhost *g_pstHost;
@@ -562,6 +656,7 @@ int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
     int rc = RXG_OK;
     if (!g_ctx) {
         rc = rxg_open(&g_ctx, device, max_burst, max_bytes);
+        if (rc == RXG_OK && g_inplace) rxg_tune_deliver(g_ctx, RXG_DLV_TCP_IN_PLACE);
         /* a new context: its delivery sets start again at set 0 */
         for (uint32_t j = 0; j < RXG_DELIVER_DEPTH; j++) g_set_ref[j] = -1;
         g_next_set = 0;
@@ -576,24 +671,12 @@ void nstack_fini(void) {
     while (g_pstHost) {
         struct localhost *h = g_pstHost;
         LL_REMOVE(h, g_pstHost);
-        void *p;
-        while (ring_dequeue(h->rcvbuf, &p) == 0) offload_free(p);
-        while (ring_dequeue(h->sndbuf, &p) == 0) {
-            free(((struct offload *)p)->data);
-            free(p);
-        }
-        ring_free(h->rcvbuf);
-        ring_free(h->sndbuf);
-        free(h);
+        udp_kill(h);
     }
     while (g_tcb_set) {
         struct tcp_stream *s = g_tcb_set;
         LL_REMOVE(s, g_tcb_set);
-        tq_clear(s->rcvbuf, &s->rq);
-        tq_clear(s->sndbuf, &s->sq);
-        ring_free(s->rcvbuf);
-        ring_free(s->sndbuf);
-        free(s);
+        tcb_kill(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
     memset(g_fd_cb, 0, sizeof(g_fd_cb));
@@ -615,6 +698,9 @@ void nstack_fini(void) {
     }
     g_local_ip = 0;
     memset(g_local_mac, 0, sizeof(g_local_mac));
+    g_inplace = 0; /* (options last one stack) */
+    g_mb_release = NULL;
+    g_mb_arg = NULL;
     if (g_ctx) rxg_close(g_ctx);
     g_ctx = NULL;
     g_dirty = 1;
@@ -649,6 +735,7 @@ int nsocket(int domain, int type, int protocol) {
         }
         pthread_cond_init(&h->cond, NULL);
         pthread_mutex_init(&h->mutex, NULL);
+        cb_ref_init(&h->ref);
         if (reg_udp(h)) {
             ring_free(h->rcvbuf);
             ring_free(h->sndbuf);
@@ -673,6 +760,7 @@ int nsocket(int domain, int type, int protocol) {
         pthread_cond_init(&s->cond, NULL);
         pthread_cond_init(&s->accept_cond, NULL);
         pthread_mutex_init(&s->mutex, NULL);
+        cb_ref_init(&s->ref);
         if (reg_tcb(s)) {
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
@@ -743,11 +831,19 @@ int naccept(int sockfd, struct sockaddr *addr, socklen_t *addrlen) { /* :388-416
         return -1;
     }
     struct tcp_stream *apt;
-    while ((apt = get_accept_tcb(s->dport)) == NULL) {
+    cb_get(&s->ref); /* (the listener may be closed while this call waits) */
+    while (!s->dead && (apt = get_accept_tcb(s->dport)) == NULL) {
         /* wait on the listener's cond; g_lock doubles as its mutex here so a
          * tcb added between the check and the wait cannot be missed */
         pthread_cond_wait(&s->accept_cond, &g_lock);
     }
+    if (s->dead) {
+        tcb_put(s);
+        pthread_mutex_unlock(&g_lock);
+        errno = EBADF;
+        return -1;
+    }
+    tcb_put(s);
     apt->fd = get_fd_frombitmap();
     fd_add(apt->fd, apt);
     if (addr) {
@@ -806,16 +902,24 @@ static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags)
 ssize_t nrecv(int sockfd, void *buf, size_t len, int flags) { /* :462-515 */
     pthread_mutex_lock(&g_lock);
     struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
+    if (s) cb_get(&s->ref); /* (linked: the block lives until our put) */
     pthread_mutex_unlock(&g_lock);
     if (!s) return -1;
-    if (s->protocol != IPPROTO_TCP) return 0;
-    return nrecv_tcb(s, buf, len, flags);
+    ssize_t r = 0;
+    if (s->protocol == IPPROTO_TCP) r = nrecv_tcb(s, buf, len, flags);
+    cb_put(s);
+    return r;
 }
 
 static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags) {
     struct tcp_fragment *f;
     pthread_mutex_lock(&s->mutex);
-    while ((f = tq_front(s->rcvbuf)) == NULL) {
+    while (s->dead || (f = tq_front(s->rcvbuf)) == NULL) {
+        if (s->dead) { /* freed (last ACK after nclose) while this call waited */
+            pthread_mutex_unlock(&s->mutex);
+            errno = EBADF;
+            return -1;
+        }
         if (flags & MSG_DONTWAIT) {
             pthread_mutex_unlock(&s->mutex);
             errno = EAGAIN;
@@ -852,9 +956,12 @@ ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr 
     (void)addrlen;
     pthread_mutex_lock(&g_lock);
     struct localhost *h = get_hostinfo_fromfd(sockfd);
+    if (h) cb_get(&h->ref);
     pthread_mutex_unlock(&g_lock);
     if (!h) return -1;
-    return udp_recv(h, buf, len, flags, src_addr);
+    const ssize_t r = udp_recv(h, buf, len, flags, src_addr);
+    cb_put(h);
+    return r;
 }
 
 /* nrecvfrom after the descriptor lookup (common.c:526-565) */
@@ -862,7 +969,12 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
                         struct sockaddr *src_addr) {
     struct offload *o = NULL;
     pthread_mutex_lock(&h->mutex);
-    while (ring_peek(h->rcvbuf, (void **)&o) < 0) {
+    while (h->dead || ring_peek(h->rcvbuf, (void **)&o) < 0) {
+        if (h->dead) { /* closed by another thread while this call waited */
+            pthread_mutex_unlock(&h->mutex);
+            errno = EBADF;
+            return -1;
+        }
         if (flags & MSG_DONTWAIT) {
             pthread_mutex_unlock(&h->mutex);
             errno = EAGAIN;
@@ -933,14 +1045,27 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
     return n;
 }
 
+static ssize_t udp_send(struct localhost *h, const void *buf, size_t len,
+                        const struct sockaddr_in *a);
+
 ssize_t nsendto(int sockfd, const void *buf, size_t len, int flags,
                 const struct sockaddr *dest_addr, socklen_t addrlen) { /* :567-607 */
     (void)flags, (void)addrlen;
     const struct sockaddr_in *a = (const struct sockaddr_in *)dest_addr;
+    if (!a) return -1;
     pthread_mutex_lock(&g_lock);
     struct localhost *h = get_hostinfo_fromfd(sockfd);
+    if (h) cb_get(&h->ref);
     pthread_mutex_unlock(&g_lock);
-    if (!h || !a) return -1;
+    if (!h) return -1;
+    const ssize_t r = udp_send(h, buf, len, a);
+    cb_put(h);
+    return r;
+}
+
+/* nsendto after the descriptor lookup (common.c:576-607) */
+static ssize_t udp_send(struct localhost *h, const void *buf, size_t len,
+                        const struct sockaddr_in *a) {
     struct offload *o = calloc(1, sizeof(*o));
     if (!o) return -1;
     o->dip = a->sin_addr.s_addr;
@@ -976,16 +1101,8 @@ int nclose(int fd) { /* :609-666 */
     if (h->protocol == IPPROTO_UDP) {
         unreg_udp(h);
         LL_REMOVE(h, g_pstHost);
-        void *p;
-        while (ring_dequeue(h->rcvbuf, &p) == 0) offload_free(p);
-        while (ring_dequeue(h->sndbuf, &p) == 0) {
-            free(((struct offload *)p)->data);
-            free(p);
-        }
-        ring_free(h->rcvbuf);
-        ring_free(h->sndbuf);
         fd_del(fd, h);
-        free(h);
+        udp_kill(h); /* (freed now, or by the last reader's put) */
         set_fd_frombitmap(fd);
     } else {
         struct tcp_stream *s = info;
@@ -1009,12 +1126,8 @@ int nclose(int fd) { /* :609-666 */
         } else {
             unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
-            tq_clear(s->rcvbuf, &s->rq);
-            tq_clear(s->sndbuf, &s->sq);
-            ring_free(s->rcvbuf);
-            ring_free(s->sndbuf);
             fd_del(fd, s);
-            free(s);
+            tcb_kill(s);
             /* the reference leaves the listener's fd set in the bitmap here */
         }
     }
@@ -1076,6 +1189,7 @@ static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, ui
     pthread_cond_init(&s->cond, NULL);
     pthread_cond_init(&s->accept_cond, NULL);
     pthread_mutex_init(&s->mutex, NULL);
+    cb_ref_init(&s->ref);
     return s;
 }
 
@@ -1194,12 +1308,8 @@ static void tcp_dispatch(struct tcp_stream *s, const uint8_t *f, uint32_t cap) {
             s->status = TCP_STATUS_CLOSED;
             unreg_tcb(s);
             LL_REMOVE(s, g_tcb_set);
-            tq_clear(s->rcvbuf, &s->rq);
-            tq_clear(s->sndbuf, &s->sq);
-            ring_free(s->rcvbuf);
-            ring_free(s->sndbuf);
             fd_del(s->fd, s);
-            free(s);
+            tcb_kill(s); /* (a reader blocked in nrecv wakes and returns) */
             g_burst_mutated = 1;
         }
         break;
@@ -1459,13 +1569,16 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
     uint32_t nfr = 0, nack = 0;
     uint64_t pbytes = 0;
     int st = s->status;
+    const int inpl = g_inplace; /* payloads captured whole stay in their frames */
     for (uint32_t j = 0; j < k; j++) {
         handled[sg[j].frame] = 1;
         if (rc_out) rc_out[sg[j].frame] = RXG_RC_OK;
         if (st != TCP_STATUS_ESTABLISHED) continue;
         if (sg[j].flags & TCP_PSH) {
             nfr++, nack++;
-            if (sg[j].plen > 0 && (pl_ref < 0 || sg[j].ncopy != (uint32_t)sg[j].plen))
+            if (sg[j].plen > 0 && sg[j].ncopy != (uint32_t)sg[j].plen) /* cut short: copied */
+                pbytes += (uint64_t)sg[j].plen;
+            else if (sg[j].plen > 0 && !inpl && pl_ref < 0)
                 pbytes += (uint64_t)sg[j].plen; /* (copied) */
         }
         if (sg[j].flags & TCP_FIN) nfr++, nack++, st = TCP_STATUS_CLOSE_WAIT;
@@ -1510,7 +1623,14 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
                 memset(fr, 0, sizeof(*fr));                                                  \
                 fr->dport = ntohs((SEG)->dport);                                             \
                 fr->sport = ntohs((SEG)->sport);                                             \
-                if ((PLEN) > 0 && pl_ref >= 0 && (SEG)->ncopy == (uint32_t)(PLEN)) {         \
+                if ((PLEN) > 0 && inpl && (SEG)->ncopy == (uint32_t)(PLEN)) {                \
+                    rxg_mbuf *mb_ = m[(SEG)->frame]; /* in its frame, the mbuf held */       \
+                    fr->data = (unsigned char *)mb_->buf_addr + mb_->data_off + 34u +        \
+                               4u * (SEG)->hl;                                               \
+                    fr->length = (uint32_t)(PLEN);                                           \
+                    fr->mb = mb_;                                                            \
+                    mb_get(mb_);                                                             \
+                } else if ((PLEN) > 0 && pl_ref >= 0 && (SEG)->ncopy == (uint32_t)(PLEN)) {  \
                     fr->data = (unsigned char *)payload + (SEG)->offset; /* (no copy) */     \
                     fr->length = (uint32_t)(PLEN);                                           \
                     rb->pl_ref = pl_ref;                                                     \
@@ -1746,6 +1866,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     }
     rxg_ctx *ctx = g_ctx;
     int delivered = 0;
+    int done[2] = {0, 0}; /* half delivered */
     double ph[3] = {0, 0, 0};
     if (sub[0]) g_rx_in_flight = 1;
     for (int h = 0; h < parts && (sub[h] || rc == RXG_OK); h++) {
@@ -1787,12 +1908,21 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         delivered += deliver_burst(m + o, k, s_v + o, rco, s_handled + o);
         g_udp_done = 0;
         g_burst_stale = 0;
+        done[h] = 1;
         const double t4 = mono_ms();
         ph[0] += t2 - t1, ph[1] += t3 - t2, ph[2] += t4 - t3;
     }
     g_rx_in_flight = 0;
-    if (rc == RXG_OK) {
-        if (v_out) memcpy(v_out, s_v, (size_t)n * sizeof(rxg_verdict));
+    /* the first half delivered, the second not put through the GPU (a failed
+     * second submit or wait): its frames are reported, not delivered */
+    const int partial = rc != RXG_OK && parts > 1 && done[0] && !done[1];
+    if (partial) {
+        if (rc_out)
+            for (uint32_t i = nh; i < n; i++) rc_out[i] = rc;
+        if (v_out) memset(v_out + nh, 0, (size_t)(n - nh) * sizeof(rxg_verdict));
+    }
+    if (rc == RXG_OK || partial) {
+        if (v_out) memcpy(v_out, s_v, (size_t)(partial ? nh : n) * sizeof(rxg_verdict));
         for (int j = 0; j < 5; j++) g_phase_ms[j] = gms[0][j] + gms[1][j];
         g_phase_ms[5] = (float)lib_ms;   /* the library calls (host clock) */
         g_phase_ms[6] = (float)ph[0];    /* UDP batches to the sockets */
@@ -1803,7 +1933,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         g_phase_ms[11] = (float)(d[0].ndgram + (parts > 1 ? d[1].ndgram : 0));
     }
     pthread_mutex_unlock(&g_lock);
-    return rc == RXG_OK ? delivered : rc;
+    return rc == RXG_OK || partial ? delivered : rc;
 }
 
 int nstack_last_burst_phases(float ms[12]) {
@@ -1897,39 +2027,21 @@ int nstack_flows(rxg_udp_sock *u, uint32_t cap_u, uint32_t *nu, rxg_tcb *t, uint
     return rc;
 }
 
-/* drain_all's look-ahead over the tcbs it visits next (g_lock held, so none
- * is freed): the tcb 4 ids ahead, the ring of the one 2 ahead, the front
- * fragment, its batch's fragment array and first payload lines of the next
- * one, so the pointer chain a tcb's read walks is in cache when it gets
- * there (the protocol thread wrote it on another core).  Prefetches only:
- * the values read to form the addresses may be stale, which costs nothing. */
-static inline void drain_prefetch(uint32_t id, uint32_t end) {
-    if (id + 4 < end && s_tcb_cb[id + 4]) __builtin_prefetch(s_tcb_cb[id + 4], 0, 0);
-    if (id + 2 < end && s_tcb_cb[id + 2] && s_tcb_cb[id + 2]->rcvbuf)
-        __builtin_prefetch(s_tcb_cb[id + 2]->rcvbuf, 0, 0);
-    if (id + 1 >= end || !s_tcb_cb[id + 1]) return;
-    const struct nring *r = s_tcb_cb[id + 1]->rcvbuf;
-    if (!r || !r->count) return;
-    const struct tcp_fragment *it = r->slot[r->head];
-    if (!it) return;
-    __builtin_prefetch(it, 0, 0);
-    const struct frag_batch *b = it->batch;
-    if (b) {
-        const struct tcp_fragment *f = &b->frag[b->next];
-        __builtin_prefetch(f, 0, 0);
-        __builtin_prefetch((const char *)f + 64, 0, 0);
-        if (f->data) {
-            __builtin_prefetch(f->data, 0, 0);
-            __builtin_prefetch(f->data + 64, 0, 0);
-        }
-    }
+/* FNV-1a 64 of a fragment's bytes: nstack_drain_all_sum adds them up, an
+ * order-free check of what the application read (tests) */
+static uint64_t fnv64(const void *p, size_t n) {
+    const unsigned char *c = p;
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 0x100000001b3ull;
+    return h;
 }
 
-/* the fragments of ring items drain_all took out of their tcbs, read after
- * the stack's lock is released: counted (EOF fragments are read and not
- * counted), copied into buf, and freed (a batch's hold on the library's
- * payload buffer ends here) */
-static void drain_detached(void **it, uint32_t k, void *buf, uint64_t *got, uint64_t *nb) {
+/* the fragments of ring items drain_tcb took out of a tcb, read after its
+ * mutex is released: counted (EOF fragments are read and not counted),
+ * copied into buf, and freed (a batch's hold on a payload buffer or on its
+ * frames' mbufs ends here) */
+static void drain_detached(void **it, uint32_t k, void *buf, uint64_t *got, uint64_t *nb,
+                           uint64_t *hs) {
     for (uint32_t i = 0; i < k; i++) {
         struct tcp_fragment *f = it[i];
         if (i + 1 < k) __builtin_prefetch(it[i + 1], 0, 0);
@@ -1943,36 +2055,82 @@ static void drain_detached(void **it, uint32_t k, void *buf, uint64_t *got, uint
                 if (g->length) {
                     memcpy(buf, g->data, g->length);
                     (*got)++, *nb += g->length;
+                    if (hs) *hs += fnv64(buf, g->length);
                 }
             }
         } else if (f->length) {
             memcpy(buf, f->data, f->length);
             (*got)++, *nb += f->length;
+            if (hs) *hs += fnv64(buf, f->length);
         }
         frag_item_free(f);
     }
 }
 
-int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
+/* one tcb's receive ring emptied (its reference held): its items are taken
+ * out under one hold of its mutex and read after it is released; an item
+ * with a fragment longer than `cap` is read in place through nrecv's split
+ * path */
+static void drain_tcb(struct tcp_stream *s, void *buf, size_t cap, uint64_t *got, uint64_t *nb,
+                      uint64_t *hs, void ***det, uint32_t *det_cap) {
+    uint32_t nd = 0;
+    struct tcp_fragment *f;
+    pthread_mutex_lock(&s->mutex);
+    while (!s->dead && ring_peek(s->rcvbuf, (void **)&f) == 0) {
+        const uint32_t first = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
+        uint32_t j = first;
+        while (j < n && (f->batch ? f->batch->frag[j].length : f->length) <= cap) j++;
+        if (j < n || (nd == *det_cap && grow((void **)det, det_cap, *det_cap ? 2 * *det_cap : 256,
+                                             sizeof(void *)))) {
+            struct tcp_fragment *h = tq_front(s->rcvbuf);
+            if (h->length > cap) {
+                pthread_mutex_unlock(&s->mutex);
+                const ssize_t r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT);
+                if (r > 0) {
+                    (*got)++, *nb += (uint64_t)r;
+                    if (hs) *hs += fnv64(buf, cap);
+                }
+                pthread_mutex_lock(&s->mutex);
+                continue;
+            }
+            if (h->length) {
+                memcpy(buf, h->data, h->length);
+                (*got)++, *nb += h->length;
+                if (hs) *hs += fnv64(buf, h->length);
+            }
+            tq_pop(s->rcvbuf, &s->rq);
+            continue;
+        }
+        ring_dequeue(s->rcvbuf, (void **)&f);
+        s->rq -= n - first;
+        (*det)[nd++] = f;
+    }
+    tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
+    pthread_mutex_unlock(&s->mutex);
+    drain_detached(*det, nd, buf, got, nb, hs);
+}
+
+static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum) {
     /* The application side of the benchmark: every socket read until empty,
      * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
-     * visited by stable id, DRAIN_CHUNK of them per hold of the stack's lock:
-     * a block is freed only under that lock (no block is read after
-     * a concurrent nstack_rx_burst freed it), and between chunks the protocol
-     * thread can take the lock.  A tcb's receive ring is emptied under one
-     * hold of its mutex: its items are taken out (their fragments then belong
-     * to this call alone) and read after the chunk releases the stack's lock,
-     * so the copies do not hold up the protocol thread's next delivery; an
-     * item with a fragment longer than `cap` is read in place through nrecv's
-     * split path. */
-    enum { DRAIN_CHUNK = 64 };
-    uint64_t got = 0, nb = 0;
+     * visited by stable id.  The stack's lock is held only to take a
+     * reference on the next DRAIN_CHUNK live blocks (a block stays valid
+     * while referenced, even if the protocol thread frees it meanwhile: its
+     * memory goes with the last reference); everything else — the rings, the
+     * copies — runs under each block's own mutex, beside the protocol
+     * thread's deliveries (the reference's app lcore reads its socket rings
+     * beside the protocol lcore, netfamily.c:424-430, udp.c:48,
+     * common.c:531-536). */
+    enum { DRAIN_CHUNK = 1024 };
+    void *blk[DRAIN_CHUNK];
+    uint64_t got = 0, nb = 0, hs = 0;
+    uint64_t *hp = sum ? &hs : NULL;
     void **det = NULL;
+    uint32_t det_cap = 0;
     atomic_fetch_add_explicit(&g_drainers, 1, memory_order_relaxed);
-    uint32_t ndet = 0, det_cap = 0;
     for (int kind = 0; kind < 2; kind++) {
         uint32_t id = 0;
-        for (;;) {
+        for (int more = 1; more;) {
             const double w0 = mono_ms();
             app_yield();
             const double w1 = mono_ms();
@@ -1981,61 +2139,46 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
             atomic_fetch_add_explicit(&g_drain_ns[1], (long long)((w1 - w0) * 1e6), memory_order_relaxed);
             atomic_fetch_add_explicit(&g_drain_ns[0], (long long)((w2 - w1) * 1e6), memory_order_relaxed);
             const uint32_t ncap = kind ? s_tcb_cap : s_udp_cap;
-            if (id >= ncap) {
-                pthread_mutex_unlock(&g_lock);
-                break;
-            }
-            const uint32_t end = id + DRAIN_CHUNK < ncap ? id + DRAIN_CHUNK : ncap;
-            for (; id < end; id++) {
-                if (!kind) {
+            uint32_t k = 0;
+            for (; id < ncap && k < DRAIN_CHUNK; id++) {
+                if (kind) {
+                    struct tcp_stream *t = s_tcb_cb[id];
+                    if (!t) continue;
+                    cb_get(&t->ref);
+                    blk[k++] = t;
+                } else {
                     struct localhost *h = s_udp_cb[id];
                     if (!h) continue;
-                    ssize_t r;
-                    struct sockaddr_in a;
-                    while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0)
-                        got++, nb += (uint64_t)r;
-                    continue;
+                    cb_get(&h->ref);
+                    blk[k++] = h;
                 }
-                drain_prefetch(id, end);
-                struct tcp_stream *s = s_tcb_cb[id];
-                if (!s) continue;
-                pthread_mutex_lock(&s->mutex);
-                struct tcp_fragment *f;
-                while (ring_peek(s->rcvbuf, (void **)&f) == 0) {
-                    const uint32_t first = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
-                    uint32_t j = first;
-                    while (j < n && (f->batch ? f->batch->frag[j].length : f->length) <= cap) j++;
-                    if (j < n || (ndet == det_cap && grow((void **)&det, &det_cap, det_cap ? 2 * det_cap : 1024,
-                                                           sizeof(void *)))) {
-                        /* a fragment longer than cap (or no room to take the item
-                         * out): its head read in place, nrecv's way */
-                        struct tcp_fragment *h = tq_front(s->rcvbuf);
-                        if (h->length > cap) {
-                            pthread_mutex_unlock(&s->mutex);
-                            const ssize_t r = nrecv_tcb(s, buf, cap, MSG_DONTWAIT);
-                            if (r > 0) got++, nb += (uint64_t)r;
-                            pthread_mutex_lock(&s->mutex);
-                            continue;
-                        }
-                        if (h->length) {
-                            memcpy(buf, h->data, h->length);
-                            got++, nb += h->length;
-                        }
-                        tq_pop(s->rcvbuf, &s->rq);
-                        continue;
-                    }
-                    ring_dequeue(s->rcvbuf, (void **)&f);
-                    s->rq -= n - first;
-                    det[ndet++] = f;
-                }
-                tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
-                pthread_mutex_unlock(&s->mutex);
             }
+            more = id < ncap;
             pthread_mutex_unlock(&g_lock);
             const double c0 = mono_ms();
-            drain_detached(det, ndet, buf, &got, &nb);
+            for (uint32_t i = 0; i < k; i++) {
+                /* look-ahead: the blocks 2-4 ahead and their receive rings
+                 * (referenced, so valid; no ring item is dereferenced) */
+                if (i + 4 < k) __builtin_prefetch(blk[i + 4], 0, 0);
+                if (i + 2 < k)
+                    __builtin_prefetch(kind ? (void *)((struct tcp_stream *)blk[i + 2])->rcvbuf
+                                            : (void *)((struct localhost *)blk[i + 2])->rcvbuf,
+                                       0, 0);
+                if (kind) {
+                    drain_tcb(blk[i], buf, cap, &got, &nb, hp, &det, &det_cap);
+                    tcb_put(blk[i]);
+                } else {
+                    struct localhost *h = blk[i];
+                    ssize_t r;
+                    struct sockaddr_in a;
+                    while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0) {
+                        got++, nb += (uint64_t)r;
+                        if (hp) hs += fnv64(buf, (size_t)r < cap ? (size_t)r : cap);
+                    }
+                    udp_put(h);
+                }
+            }
             atomic_fetch_add_explicit(&g_drain_ns[2], (long long)((mono_ms() - c0) * 1e6), memory_order_relaxed);
-            ndet = 0;
         }
     }
     free(det);
@@ -2044,7 +2187,31 @@ int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
     pthread_cond_broadcast(&g_pl_cv);
     pthread_mutex_unlock(&g_pl_mx);
     if (bytes) *bytes = nb;
+    if (sum) *sum = hs;
     return (int64_t)got;
+}
+
+int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes) {
+    return drain_impl(buf, cap, bytes, NULL);
+}
+
+int64_t nstack_drain_all_sum(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum) {
+    return drain_impl(buf, cap, bytes, sum);
+}
+
+int nstack_set_rx_inplace(int on, void (*release)(rxg_mbuf *m, void *arg), void *arg) {
+    pthread_mutex_lock(&g_lock);
+    g_inplace = on != 0;
+    g_mb_release = release;
+    g_mb_arg = arg;
+    const int rc = g_ctx ? rxg_tune_deliver(g_ctx, g_inplace ? RXG_DLV_TCP_IN_PLACE : 0u) : RXG_OK;
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+void nstack_mbufs_put(rxg_mbuf *const *m, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+        if (m[i]) mb_put(m[i]);
 }
 
 int nstack_flow_ids(uint32_t *uid, uint32_t cap_u, uint32_t *tid, uint32_t cap_t) {

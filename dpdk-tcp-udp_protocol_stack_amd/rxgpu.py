@@ -127,9 +127,11 @@ class GenCfg(C.Structure):
 
 
 class Mbuf(C.Structure):
-    """rxg_mbuf: rte_mbuf-shaped descriptor (buf_addr@0, data_off@16, data_len@40)."""
+    """rxg_mbuf: rte_mbuf-shaped descriptor (buf_addr@0, data_off@16, refcnt@18,
+    data_len@40)."""
     _fields_ = [("buf_addr", C.c_void_p), ("_r0", C.c_uint8 * 8), ("data_off", C.c_uint16),
-                ("_r1", C.c_uint8 * 22), ("data_len", C.c_uint16), ("_r2", C.c_uint8 * 86)]
+                ("refcnt", C.c_uint16), ("_r1", C.c_uint8 * 20), ("data_len", C.c_uint16),
+                ("_r2", C.c_uint8 * 86)]
 
 
 assert C.sizeof(Mbuf) == 128
@@ -756,6 +758,9 @@ class NStack:
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
                    ("nstack_flow_ids", _i32, [_vp, _u32, _vp, _u32]),
                    ("nstack_drain_all", C.c_int64, [_vp, C.c_size_t, _vp]),
+                   ("nstack_drain_all_sum", C.c_int64, [_vp, C.c_size_t, _vp, _vp]),
+                   ("nstack_set_rx_inplace", _i32, [_i32, _vp, _vp]),
+                   ("nstack_mbufs_put", None, [_vp, _u32]),
                    ("nstack_last_burst_phases", _i32, [_vp]),
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
@@ -778,6 +783,8 @@ class NStack:
 
     def fini(self):
         self.lib.nstack_fini()
+        self._held = []  # (in place: the stack let go of every frame)
+        self._inplace = False
 
     # socket calls: thin pass-through with the reference's argument meaning
     def socket(self, type_):
@@ -916,6 +923,7 @@ class NStack:
             m.buf_addr = C.cast(b, C.c_void_p)
             m.data_off = 0
             m.data_len = len(f)
+            m.refcnt = 1  # the caller's reference (rte_pktmbuf_alloc)
         arr = (C.POINTER(Mbuf) * len(ms))(*[C.pointer(m) for m in ms])
         return arr, (bufs, ms)
 
@@ -930,6 +938,7 @@ class NStack:
         arr, keep = self.mbufs(frames)
         verdicts = np.ascontiguousarray(verdicts, VERDICT_DTYPE)
         r = self.lib.nstack_deliver(C.cast(arr, _vp), len(frames), _ptr(verdicts), gen, _ptr(rcs))
+        self._let_go(arr, len(frames), keep)
         if r < 0:
             _check(r, "nstack_deliver")
         return r
@@ -939,9 +948,36 @@ class NStack:
         rcs = np.zeros(len(frames), np.int32)
         v = np.zeros(len(frames), VERDICT_DTYPE)
         r = self.lib.nstack_rx_burst(C.cast(arr, _vp), len(frames), _ptr(rcs), _ptr(v))
+        self._let_go(arr, len(frames), keep)
         if r < 0:
             _check(r, "nstack_rx_burst")
         return r, rcs, v
+
+    def _let_go(self, arr, n, keep):
+        """after a burst call: in place, the frames stay alive while the stack
+        holds them (kept here until fini) and the caller's references go"""
+        if getattr(self, "_inplace", False):
+            self._held.append((arr, keep))
+            self.lib.nstack_mbufs_put(C.cast(arr, _vp), n)
+
+    def set_rx_inplace(self, on: bool = True):
+        """nstack_set_rx_inplace (no release callback: poll Mbuf.refcnt)"""
+        self._inplace = bool(on)
+        if not hasattr(self, "_held"):
+            self._held = []
+        _check(self.lib.nstack_set_rx_inplace(1 if on else 0, None, None), "nstack_set_rx_inplace")
+
+    def mbufs_put(self, arr, n: int):
+        """nstack_mbufs_put: drop the caller's reference on n mbufs"""
+        self.lib.nstack_mbufs_put(C.cast(arr, _vp), n)
+
+    def drain_all_sum(self, buf: np.ndarray):
+        """nstack_drain_all_sum: (items received, bytes, sum of FNV-1a 64 of what each read returned)"""
+        nb, hs = _u64(), _u64()
+        r = self.lib.nstack_drain_all_sum(_ptr(buf), buf.nbytes, C.byref(nb), C.byref(hs))
+        if r < 0:
+            _check(int(r), "nstack_drain_all_sum")
+        return int(r), nb.value, hs.value
 
     @staticmethod
     def mbufs_over(pkts: np.ndarray, off: np.ndarray, lens: np.ndarray, off_unit_log2: int):
@@ -953,6 +989,7 @@ class NStack:
         for i in range(n):
             ms[i].buf_addr = base + (int(off[i]) << off_unit_log2)
             ms[i].data_len = int(lens[i])
+            ms[i].refcnt = 1  # the caller's reference (rte_pktmbuf_alloc)
         arr = (C.POINTER(Mbuf) * n)(*[C.pointer(ms[i]) for i in range(n)])
         return arr, ms
 

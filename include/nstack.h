@@ -15,6 +15,10 @@
  * Deliberate differences (DESIGN.md §Socket layer):
  *   - the lists are guarded by a lock (the reference mutates them from the
  *     app lcore while the protocol lcore walks them, common.c:302,336,620,660);
+ *   - control blocks are reference-counted: a call blocked in nrecv /
+ *     nrecvfrom / naccept on a block that another thread closes (or whose
+ *     last ACK frees it) wakes and returns -1 (errno EBADF) instead of
+ *     waiting on freed memory;
  *   - get_hostinfo_fromfd walks the list correctly (common.c:116 advances
  *     from the list head and never terminates past the second socket);
  *   - nrecvfrom/nrecv/naccept honour MSG_DONTWAIT in `flags` (the reference
@@ -77,6 +81,10 @@ int nclose(int fd);
  * the outcome is the same).  rc_out[i] (nullable) = what udp_process/tcp_process would
  * have returned (KNI frames: 1); v_out (nullable) = the verdicts.
  * Returns the number of UDP datagrams delivered, or a negative RXG_E* code.
+ * A burst run as two halves whose second half could not go through the GPU
+ * after the first was delivered returns the first half's count: the second
+ * half's rc_out entries hold the (negative RXG_E*) error and its v_out
+ * entries are zero, so the caller can pass those frames again.
  * Called by one protocol thread, which also runs nstack_tx_burst (as
  * pkt_process runs udp_out / tcp_out); while the burst is on the GPU the
  * stack's lock is released, so application threads' socket calls run beside
@@ -159,11 +167,33 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * the receive buffer each call uses.  Returns the datagrams + fragments
  * received (EOF fragments are read and not counted, as oracle_drain_all does;
  * a negative RXG_E* code on error); *bytes = the bytes the calls returned.
- * Takes the stack's lock per chunk of 64 blocks, stepping aside between
- * chunks while the protocol thread waits for it, so no block it reads can be
- * freed under it and a concurrent nstack_rx_burst is not held up for a
- * whole pass. */
+ * Takes the stack's lock only to take a reference on the next 1024 blocks
+ * (stepping aside while the protocol thread waits for it); the reads run
+ * under each block's own mutex, so a concurrent nstack_rx_burst delivers
+ * beside them, and a block freed meanwhile (last ACK) stays valid until the
+ * call lets go of it. */
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
+/* nstack_drain_all, and *sum = the sum (mod 2^64) over every datagram and
+ * fragment read of the FNV-1a 64 hash of the bytes the read returned: an
+ * order-free check of the content the application received (tests). */
+int64_t nstack_drain_all_sum(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum);
+
+/* In-place TCP receive (DPDK zero-copy; off by default).  on != 0: a
+ * receive fragment whose payload was captured whole is not copied (the
+ * rte_malloc + rte_memcpy of ng_tcp_enqueue_recvbuffer, tcp.c:133-185): it
+ * points into its frame, and the stack takes a reference on the frame's mbuf
+ * (rxg_mbuf.refcnt += 1, atomically, as rte_mbuf_refcnt_update) until the
+ * application has read it.  The GPU then sends back only the segment
+ * records, no payload (RXG_DLV_TCP_IN_PLACE).  The put that drops an mbuf's
+ * count to 0 calls release(m, arg) (nullable; e.g. the mempool's free, as
+ * rte_pktmbuf_free).  The caller holds its own reference on each mbuf it
+ * passes (refcnt >= 1) and drops it after nstack_rx_burst / nstack_deliver
+ * returns (nstack_mbufs_put); an mbuf's frame must stay in place until its
+ * count is 0. */
+int nstack_set_rx_inplace(int on, void (*release)(rxg_mbuf *m, void *arg), void *arg);
+/* drop one reference on each of n mbufs (rte_pktmbuf_free of a burst):
+ * release(m, arg) of nstack_set_rx_inplace for each whose count reaches 0 */
+void nstack_mbufs_put(rxg_mbuf *const *m, uint32_t n);
 
 /* Where the last nstack_rx_burst's time went, in ms: [0] gather of the mbufs
  * into pinned staging (host), [1] copy in, [2] classify (K1), [3] UDP

@@ -152,7 +152,9 @@ typedef struct rxg_mbuf {
     void *buf_addr;        /* @0  */
     uint8_t _r0[8];
     uint16_t data_off;     /* @16 */
-    uint8_t _r1[22];
+    uint16_t refcnt;       /* @18: references (rte_mbuf_refcnt); librxgpu never reads it,
+                              libnstack's in-place delivery holds frames with it */
+    uint8_t _r1[20];
     uint16_t data_len;     /* @40 */
     uint8_t _r2[86];
 } rxg_mbuf;                /* 128 bytes, like rte_mbuf */
@@ -364,7 +366,9 @@ typedef struct rxg_segment {
     uint32_t seq;    /* sent_seq, host order (ntohl of frame bytes 38-41) */
     uint32_t ack;    /* recv_ack, host order (ntohl of frame bytes 42-45) */
     int32_t plen;    /* total_length - 20 - 4*hl (signed: tcp.c:145-146, 391) */
-    uint32_t offset; /* first payload byte in the payload buffer (16-B aligned) */
+    uint32_t offset; /* first payload byte in the payload buffer (16-B aligned); records
+                        only (no payload buffer, RXG_DLV_TCP_IN_PLACE): the payload's
+                        offset in its frame, 34 + 4*hl */
     uint16_t sport;  /* raw (network order) source port, frame bytes 34-35 */
     uint16_t dport;  /* raw destination port, frame bytes 36-37 */
     uint16_t ncopy;  /* payload bytes in the buffer: min(plen, caplen - 34 - 4*hl) for a
@@ -376,7 +380,9 @@ typedef struct rxg_segment {
 /* Device form, asynchronous on `stream`: d_v = the burst's verdicts; d_seg
  * (room for n) gets the rc-0 TCP segments with a tcb id below the id space,
  * sorted by (flow, frame); d_totals = {segments, payload bytes used, 1 if
- * payload_cap was too small (those payloads are not written)}.  The device
+ * payload_cap was too small (those payloads are not written)}.  d_payload
+ * NULL: the records only (offset = the payload's offset in its frame, no
+ * payload gathered).  The device
  * workspace grows on demand (stream-ordered). */
 int rxg_tcp_compact_dev(rxg_ctx *ctx, const uint8_t *d_pkts, const uint32_t *d_off,
                         const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2,
@@ -428,6 +434,19 @@ int rxg_process_mbufs_deliver(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_
 int rxg_deliver_submit(rxg_ctx *ctx, rxg_mbuf *const *m, uint32_t n, rxg_verdict *out,
                        rxg_delivery *d);
 int rxg_deliver_wait(rxg_ctx *ctx, rxg_delivery *d, float ms[8]);
+
+/* Delivery options (0 = the default).  RXG_DLV_TCP_IN_PLACE: the TCP payloads
+ * stay where they are, in the caller's frames — the DPDK zero-copy receive,
+ * where the socket's fragment points into the mbuf and holds it
+ * (rte_mbuf_refcnt_update) until the application has read it, instead of the
+ * rte_malloc + rte_memcpy of ng_tcp_enqueue_recvbuffer (tcp.c:133-185).  The
+ * device sorts the segments and decodes their records as before but gathers
+ * no payload, and only the 32-B records cross PCIe back:
+ * rxg_delivery.tcp_payload is NULL and each record's offset is its payload's
+ * offset in its frame (34 + 4*hl; ncopy captured bytes).  The caller keeps
+ * the frames in place for as long as it points into them. */
+#define RXG_DLV_TCP_IN_PLACE 0x1u
+int rxg_tune_deliver(rxg_ctx *ctx, uint32_t flags);
 
 /* Keep a burst's TCP payload buffer (rxg_delivery.tcp_payload_ref) alive past
  * the context's next burst call — e.g. while receive fragments that point into

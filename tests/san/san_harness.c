@@ -18,7 +18,9 @@
  * and TX framing) fed with oracle verdicts.
  */
 #include <arpa/inet.h>
+#include <errno.h>
 #include <netinet/in.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -204,8 +206,12 @@ static void pcap_cases(void) {
 }
 
 /* classify a burst against the stack's current control blocks (oracle
- * verdicts: the GPU's are bit-identical, tests/test_gpu_parity.py) and deliver */
-static void deliver(burst *b, int *rc) {
+ * verdicts: the GPU's are bit-identical, tests/test_gpu_parity.py) and
+ * deliver, through the caller's mbufs (persistent: in-place delivery points
+ * into them) or, mb NULL, through descriptors on the stack */
+static void deliver_mb(burst *b, int *rc, rxg_mbuf *mbp);
+static void deliver(burst *b, int *rc) { deliver_mb(b, rc, NULL); }
+static void deliver_mb(burst *b, int *rc, rxg_mbuf *mbp) {
     rxg_udp_sock u[64];
     rxg_tcb t[64];
     uint32_t nu = 0, nt = 0;
@@ -221,14 +227,133 @@ static void deliver(burst *b, int *rc) {
     for (uint32_t i = 0; i < b->n; ++i)
         if (v[i].flow_id != RXG_FLOW_NONE)
             v[i].flow_id = v[i].cls == RXG_CLS_TCP ? tid[v[i].flow_id] : uid[v[i].flow_id];
-    rxg_mbuf mb[64], *mp[64];
-    memset(mb, 0, sizeof mb);
+    rxg_mbuf mbl[64], *mp[64];
+    rxg_mbuf *mb = mbp ? mbp : mbl;
+    memset(mb, 0, 64 * sizeof(rxg_mbuf));
     for (uint32_t i = 0; i < b->n; ++i) {
         mb[i].buf_addr = b->buf + ((size_t)b->off[i] << 6);
         mb[i].data_len = b->len[i];
+        mb[i].refcnt = 1; /* the caller's reference (rte_pktmbuf_alloc) */
         mp[i] = &mb[i];
     }
     CHECK(nstack_deliver(mp, b->n, v, gen, rc) >= 0);
+    if (mbp) nstack_mbufs_put(mp, b->n); /* the caller lets go (rte_pktmbuf_free) */
+}
+
+/* ---- block lifetime under two threads, and in-place receive ------------- */
+static void on_release(rxg_mbuf *m, void *arg) {
+    (void)m;
+    ++*(int *)arg;
+}
+
+typedef struct {
+    int fd, kind; /* 0 nrecv, 1 nrecvfrom, 2 naccept */
+    ssize_t r;
+    int err;
+    volatile int entered;
+} blocker;
+
+static void *block_call(void *p) {
+    blocker *b = p;
+    char out[256];
+    struct sockaddr_in s;
+    socklen_t sl = sizeof s;
+    b->entered = 1;
+    if (b->kind == 0)
+        b->r = nrecv(b->fd, out, sizeof out, 0);
+    else if (b->kind == 1)
+        b->r = nrecvfrom(b->fd, out, sizeof out, 0, (struct sockaddr *)&s, &sl);
+    else
+        b->r = naccept(b->fd, (struct sockaddr *)&s, &sl);
+    b->err = errno;
+    return NULL;
+}
+
+static void start_blocked(blocker *b, pthread_t *th) {
+    CHECK(pthread_create(th, NULL, block_call, b) == 0);
+    while (!b->entered) usleep(1000);
+    usleep(100000); /* in the call, waiting */
+}
+
+static void lifetime_cases(void) {
+    CHECK(nstack_init(RXG_HOST_ONLY, 256, 1 << 20) == RXG_OK);
+    const uint32_t L = inet_addr("192.168.100.77"), C = inet_addr("10.0.0.9");
+    CHECK(nstack_set_local(L, MAC_A) == RXG_OK);
+    const int us = nsocket(AF_INET, SOCK_DGRAM, 0);
+    struct sockaddr_in a = {.sin_family = AF_INET, .sin_port = htons(8889), .sin_addr.s_addr = L};
+    CHECK(nbind(us, (struct sockaddr *)&a, sizeof a) == 0);
+    const int ls = nsocket(AF_INET, SOCK_STREAM, 0);
+    a.sin_port = htons(9999);
+    CHECK(nbind(ls, (struct sockaddr *)&a, sizeof a) == 0);
+    CHECK(nlisten(ls, 16) == 0);
+    CHECK(nstack_tcb_add(C, L, htons(40000), htons(9999), 4) == 0); /* ESTABLISHED */
+    struct sockaddr_in peer;
+    socklen_t pl2 = sizeof peer;
+    const int cs = naccept(ls, (struct sockaddr *)&peer, &pl2);
+    CHECK(cs >= 0);
+
+    /* in place: the data segments' fragments point into their frames and hold
+     * their mbufs until read; the other frames' mbufs go at the caller's put */
+    int released = 0;
+    CHECK(nstack_set_rx_inplace(1, on_release, &released) == RXG_OK);
+    static rxg_mbuf mb[64];
+    uint8_t f[2048], pl[1400], out[2048];
+    for (size_t i = 0; i < sizeof pl; ++i) pl[i] = (uint8_t)(i * 13 + 1);
+    burst b = {.buf = calloc(1, 1 << 20)};
+    size_t n;
+    n = frame(f, 6, C, htons(40000), L, htons(9999), 0x18, 1001, pl, 300); /* PSH data */
+    push(&b, f, n, n);
+    n = frame(f, 17, C, htons(5555), L, htons(8889), 0, 0, pl, 40); /* a datagram (copied) */
+    push(&b, f, n, n);
+    n = frame(f, 6, C, htons(40000), L, htons(9999), 0x18, 1301, pl + 300, 700);
+    push(&b, f, n, n);
+    n = frame(f, 6, C, htons(40000), L, htons(9999), 0x18, 2001, pl, 500);
+    push(&b, f, n, 300); /* captured short: copied, zero filled */
+    oracle_tx_cksum(b.buf, b.off, b.len, b.n, 6);
+    int rc[64];
+    deliver_mb(&b, rc, mb);
+    CHECK(rc[0] == 0 && rc[1] == 0 && rc[2] == 0);
+    CHECK(mb[0].refcnt == 1 && mb[2].refcnt == 1); /* held by their fragments */
+    CHECK(mb[1].refcnt == 0 && mb[3].refcnt == 0 && released == 2);
+    CHECK(nrecv(cs, out, sizeof out, MSG_DONTWAIT) == 300 && memcmp(out, pl, 300) == 0);
+    CHECK(nrecv(cs, out, sizeof out, MSG_DONTWAIT) == 700 && memcmp(out, pl + 300, 700) == 0);
+    CHECK(nrecv(cs, out, sizeof out, MSG_DONTWAIT) == 500);
+    CHECK(mb[0].refcnt == 0 && mb[2].refcnt == 0 && released == 4); /* the batch is freed */
+    CHECK(nrecvfrom(us, out, sizeof out, MSG_DONTWAIT, NULL, NULL) == 48);
+
+    /* an application thread blocked in nrecv while another closes the
+     * connection and the peer's last ACK frees the tcb (tcp.c:312-331): the
+     * call wakes and returns -1 (EBADF); the tcb's memory goes with its put */
+    blocker br = {.fd = cs, .kind = 0};
+    pthread_t th;
+    start_blocked(&br, &th);
+    CHECK(nclose(cs) == 0); /* FIN queued, LAST_ACK */
+    b.n = 0, b.pos = 0;
+    n = frame(f, 6, C, htons(40000), L, htons(9999), 0x10, 2501, NULL, 0); /* the last ACK */
+    push(&b, f, n, n);
+    oracle_tx_cksum(b.buf, b.off, b.len, b.n, 6);
+    deliver(&b, rc);
+    CHECK(rc[0] == 0);
+    pthread_join(th, NULL);
+    CHECK(br.r == -1 && br.err == EBADF);
+    CHECK(nstack_tcb_count() == 1); /* the listener */
+
+    /* nrecvfrom blocked on a socket another thread closes */
+    blocker bu = {.fd = us, .kind = 1};
+    start_blocked(&bu, &th);
+    CHECK(nclose(us) == 0);
+    pthread_join(th, NULL);
+    CHECK(bu.r == -1 && bu.err == EBADF);
+
+    /* naccept blocked on a listener another thread closes */
+    blocker ba = {.fd = ls, .kind = 2};
+    start_blocked(&ba, &th);
+    CHECK(nclose(ls) == 0);
+    pthread_join(th, NULL);
+    CHECK(ba.r == -1 && ba.err == EBADF);
+    CHECK(nstack_set_rx_inplace(0, NULL, NULL) == RXG_OK);
+    free(b.buf);
+    nstack_fini();
 }
 
 static void socket_cases(void) {
@@ -374,6 +499,7 @@ int main(void) {
     oracle_edge_cases();
     pcap_cases();
     socket_cases();
+    lifetime_cases();
     oracle_stack_cases();
     printf("SAN OK\n");
     return 0;

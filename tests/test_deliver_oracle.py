@@ -263,19 +263,27 @@ def ns_host():
     s.fini()
 
 
+@pytest.mark.parametrize("inplace", [False, True], ids=["copy", "inplace"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6, 7, 8])
-def test_delivery_matches_oracle(ns_host, seed):
+def test_delivery_matches_oracle(ns_host, seed, inplace):
+    """inplace: receive fragments point into the frames (nstack_set_rx_inplace)
+    instead of copies (tcp.c:133-185); every nrecv result is the same"""
+    if inplace:
+        ns_host.set_rx_inplace(True)
     _run(ns_host, "cpu", seed)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True], ids=["copy", "inplace"])
 @pytest.mark.parametrize("seed", [1, 5])
-def test_delivery_through_gpu_matches_oracle(seed):
+def test_delivery_through_gpu_matches_oracle(seed, inplace):
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU test needs a GPU (no fallback path exists)")
     ns = R.NStack(0)
     try:
+        if inplace:  # the GPU sends back segment records only (RXG_DLV_TCP_IN_PLACE)
+            ns.set_rx_inplace(True)
         _run(ns, "gpu", seed)
     finally:
         ns.fini()

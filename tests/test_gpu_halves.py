@@ -239,16 +239,40 @@ def test_drain_all_reads_long_fragments_through_the_split_path(torch_dev, cap):
         ns.fini()
 
 
-def test_two_threads_receive_every_byte(torch_dev):
+def _fnv_sum(payloads):
+    """sum mod 2^64 of FNV-1a 64 over each payload (nstack_drain_all_sum's
+    check), vectorised over the payloads"""
+    n = len(payloads)
+    lens = np.array([len(p) for p in payloads], np.int64)
+    m = np.zeros((n, int(lens.max(initial=1))), np.uint8)
+    for i, p in enumerate(payloads):
+        m[i, :len(p)] = np.frombuffer(p, np.uint8)
+    h = np.full(n, 0xcbf29ce484222325, np.uint64)
+    prime = np.uint64(0x100000001b3)
+    with np.errstate(over="ignore"):
+        for j in range(m.shape[1]):
+            live = lens > j
+            h[live] = (h[live] ^ m[live, j].astype(np.uint64)) * prime
+        return int(h[lens > 0].sum(dtype=np.uint64))
+
+
+@pytest.mark.parametrize("mode", ["pooled", "inplace"])
+def test_two_threads_receive_every_byte(torch_dev, mode):
     """The reference's arrangement: the protocol loop on one thread
     (nstack_rx_burst), the application on another draining every socket
-    (nstack_drain_all) at the same time.  drain_all takes fragments out under
-    the locks and reads them after; rx_burst waits for a pooled payload buffer
-    while the application still holds them all.  Every payload byte of every
-    burst must reach the application exactly once."""
+    (nstack_drain_all_sum) at the same time.  pooled: the payloads come back
+    from the GPU into pooled pinned buffers that the fragments point into
+    (rx_burst waits for one while the application still holds them all);
+    inplace: the fragments point into the frames, which their mbufs' counts
+    hold (nstack_set_rx_inplace).  Every payload byte of every burst must
+    reach the application exactly once and unchanged: the sum of the FNV-1a
+    hashes of what the reads returned equals that of the payloads sent, so a
+    buffer reused early (a payload overwritten while still queued) fails it."""
     import threading
     ns = R.NStack(0, max_burst=4096, max_bytes=4096 * 1536)
     try:
+        if mode == "inplace":
+            ns.set_rx_inplace(True)
         conns = []
         for k in range(512):
             cip, cport = f"10.8.{k >> 8}.{k & 255}", 4000 + k
@@ -256,28 +280,31 @@ def test_two_threads_receive_every_byte(torch_dev):
             assert ns.lib.nstack_tcb_add(*t, 4) == 0
             conns.append((cip, cport))
         rng = np.random.default_rng(34)
-        bursts, want_items, want_bytes = [], 0, 0
+        bursts, want_items, want_bytes, payloads = [], 0, 0, []
         for b in range(16):
             frames = []
             for i in range(4000):
                 cip, cport = conns[int(rng.integers(len(conns)))]
                 n = int(rng.choice([1446, 1446, 700, 33]))
-                frames.append(F.tcp_frame(cip, cport, L, 9998, bytes(rng.integers(0, 256, n, np.uint8)),
-                                          flags=0x18, seq=i, ack=1))
+                pl = bytes(rng.integers(0, 256, n, np.uint8))
+                frames.append(F.tcp_frame(cip, cport, L, 9998, pl, flags=0x18, seq=i, ack=1))
                 want_items, want_bytes = want_items + 1, want_bytes + n
+                payloads.append(pl)
             buf, off, lens = F.pack_frames(frames, 6)
             arr, keep = R.NStack.mbufs_over(buf, off, lens, 6)
             bursts.append((arr, len(frames), keep, buf))
-        got = [0, 0]
+        want_sum = _fnv_sum(payloads)
+        got = [0, 0, 0]
         stop = threading.Event()
 
         def app():
             buf = np.zeros(65536, np.uint8)
-            while not stop.is_set():
-                g, nb = ns.drain_all(buf)
-                got[0], got[1] = got[0] + g, got[1] + nb
-            g, nb = ns.drain_all(buf)
-            got[0], got[1] = got[0] + g, got[1] + nb
+            while True:
+                last = stop.is_set()
+                g, nb, hs = ns.drain_all_sum(buf)
+                got[0], got[1], got[2] = got[0] + g, got[1] + nb, (got[2] + hs) % (1 << 64)
+                if last:
+                    break
 
         c0, w0 = ns.stat(6), ns.stat(11)
         th = threading.Thread(target=app)
@@ -285,11 +312,18 @@ def test_two_threads_receive_every_byte(torch_dev):
         try:
             for arr, n, _keep, _buf in bursts:
                 assert ns.rx_burst_mbufs(arr, n) >= 0
+                if mode == "inplace":
+                    ns.mbufs_put(arr, n)  # the caller's reference
         finally:
             stop.set()
             th.join()
         assert (got[0], got[1]) == (want_items, want_bytes)
+        assert got[2] == want_sum
         assert ns.stat(7) == 0  # no batch left holding a payload buffer
-        print("copied bytes", ns.stat(6) - c0, "bursts that waited", ns.stat(11) - w0)
+        if mode == "inplace":  # every hold on a frame let go, exactly once
+            for _arr, _n, keep, _buf in bursts:
+                assert all(keep[i].refcnt == 0 for i in range(len(keep)))
+            assert ns.stat(6) == c0  # nothing copied
+        print(mode, "copied bytes", ns.stat(6) - c0, "bursts that waited", ns.stat(11) - w0)
     finally:
         ns.fini()
