@@ -968,6 +968,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                     if time.perf_counter() > t_end:
                         raise RuntimeError("mbuf set still held after 5 s")
                     time.sleep(0)
+                    ns.reclaim()  # (what the application thread has read lets go of its frames)
             return a_j
         rbuf = np.zeros(65536, np.uint8)
         ns.rx_burst_mbufs(next_set(), B)  # warm (staging, tables committed)

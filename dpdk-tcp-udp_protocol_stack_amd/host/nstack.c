@@ -114,6 +114,7 @@ struct offload {
     uint16_t length;
     struct dgram_batch *batch; /* non-NULL: this ring item is a burst's datagrams for
                                   the socket, delivered with one copy (GPU compaction) */
+    struct offload *gnext;     /* (on the garbage list, see reclaim) */
 };
 
 /* The datagrams of one burst for one socket, in burst order, as the GPU's
@@ -131,13 +132,35 @@ struct dgram_batch {
     unsigned char *data;
 };
 
-static void offload_free(struct offload *o) {
+/* Items the application threads are done with go back to the protocol
+ * thread, which allocated them: freed there (reclaim, at its next burst
+ * call), they stay in its malloc arena's fast paths instead of each free
+ * taking the arena's lock against its next allocations (glibc frees a chunk
+ * into the arena it came from), and the frames they hold (in-place receive)
+ * are let go on the core that took them.  Lock-free: pushed one by one,
+ * taken all at once. */
+static __thread int t_proto; /* this thread makes the protocol loop's calls */
+static _Atomic(struct offload *) g_off_garbage;
+
+static void offload_free_now(struct offload *o) {
     if (!o) return;
     if (o->batch)
         free(o->batch); /* (meta and data live in the batch's allocation) */
     else
         free(o->data);
     free(o);
+}
+static void offload_free(struct offload *o) {
+    if (!o) return;
+    if (t_proto) {
+        offload_free_now(o);
+        return;
+    }
+    struct offload *old = atomic_load_explicit(&g_off_garbage, memory_order_relaxed);
+    do
+        o->gnext = old;
+    while (!atomic_compare_exchange_weak_explicit(&g_off_garbage, &old, o, memory_order_release,
+                                                  memory_order_relaxed));
 }
 
 struct tcp_stream {
@@ -176,6 +199,7 @@ struct tcp_fragment {
                                  tcb, in one allocation (GPU segment sort) */
     rxg_mbuf *mb;             /* in-place delivery: data points into this mbuf's frame,
                                  held (refcnt) until the fragment's item is freed */
+    struct tcp_fragment *gnext; /* (on the garbage list, see reclaim) */
 };
 
 /* The fragments one burst queues on one tcb (its receive fragments, or the
@@ -224,7 +248,8 @@ static inline void mb_put(rxg_mbuf *m) {
     if (__atomic_fetch_sub(&m->refcnt, 1, __ATOMIC_ACQ_REL) == 1 && g_mb_release)
         g_mb_release(m, g_mb_arg);
 }
-static void frag_item_free(struct tcp_fragment *f) {
+static _Atomic(struct tcp_fragment *) g_frag_garbage;
+static void frag_item_free_now(struct tcp_fragment *f) {
     if (f->batch) {
         for (uint32_t j = 0; j < f->batch->n; j++)
             if (f->batch->frag[j].mb) mb_put(f->batch->frag[j].mb);
@@ -245,6 +270,33 @@ static void frag_item_free(struct tcp_fragment *f) {
         else
             free(f->data);
         free(f);
+    }
+}
+static void frag_item_free(struct tcp_fragment *f) {
+    if (t_proto) {
+        frag_item_free_now(f);
+        return;
+    }
+    struct tcp_fragment *old = atomic_load_explicit(&g_frag_garbage, memory_order_relaxed);
+    do
+        f->gnext = old;
+    while (!atomic_compare_exchange_weak_explicit(&g_frag_garbage, &old, f, memory_order_release,
+                                                  memory_order_relaxed));
+}
+/* the protocol thread frees what the application threads let go of */
+static void reclaim(void) {
+    t_proto = 1;
+    struct tcp_fragment *f = atomic_exchange_explicit(&g_frag_garbage, NULL, memory_order_acquire);
+    while (f) {
+        struct tcp_fragment *nx = f->gnext;
+        frag_item_free_now(f);
+        f = nx;
+    }
+    struct offload *o = atomic_exchange_explicit(&g_off_garbage, NULL, memory_order_acquire);
+    while (o) {
+        struct offload *nx = o->gnext;
+        offload_free_now(o);
+        o = nx;
     }
 }
 /* a standalone fragment at the tail (ring full: -ENOBUFS, the caller keeps it) */
@@ -667,6 +719,7 @@ int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
 }
 
 void nstack_fini(void) {
+    reclaim();
     pthread_mutex_lock(&g_lock);
     while (g_pstHost) {
         struct localhost *h = g_pstHost;
@@ -698,6 +751,7 @@ void nstack_fini(void) {
     }
     g_local_ip = 0;
     memset(g_local_mac, 0, sizeof(g_local_mac));
+    reclaim(); /* (what the blocks' last puts let go of) */
     g_inplace = 0; /* (options last one stack) */
     g_mb_release = NULL;
     g_mb_arg = NULL;
@@ -1454,6 +1508,7 @@ static uint32_t host_segments(rxg_mbuf *const *m, uint32_t n, const rxg_verdict 
 int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
                    int *rc_out) {
     if (!m || !v) return n ? RXG_EINVAL : 0;
+    reclaim();
     pthread_mutex_lock(&g_lock);
     int rc = g_ctx ? RXG_OK : RXG_EINVAL;
     int delivered = 0;
@@ -1719,6 +1774,12 @@ static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8
     for (uint32_t a = 0, b; a < nseg; a = b) {
         b = a + 1;
         while (b < nseg && sg[b].flow == sg[a].flow) b++;
+        /* look-ahead: the next connection's tcb and, in place, the mbufs of
+         * the next segments (each gets a reference) */
+        if (b < nseg && sg[b].flow < s_tcb_cap && s_tcb_cb[sg[b].flow])
+            __builtin_prefetch(s_tcb_cb[sg[b].flow], 1, 0);
+        if (g_inplace)
+            for (uint32_t j = b; j < b + 8 && j < nseg; j++) __builtin_prefetch(m[sg[j].frame], 1, 0);
         struct tcp_stream *s = sg[a].flow < s_tcb_cap ? s_tcb_cb[sg[a].flow] : NULL;
         if (s) deliver_tcp_conn(s, sg + a, b - a, payload, pl_ref, m, handled, rc_out);
     }
@@ -1795,6 +1856,7 @@ static void pl_wait_free(void) {
     while (!pl_free() && atomic_load_explicit(&g_drainers, memory_order_relaxed) &&
            mono_ms() - t0 < 20.0) {
         pthread_mutex_unlock(&g_lock);
+        reclaim(); /* (the batches the application let go of free their buffers here) */
         pthread_mutex_lock(&g_pl_mx);
         if (!pl_free()) {
             struct timespec ts;
@@ -1824,6 +1886,7 @@ int nstack_set_halves(uint32_t min_half) {
 
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
+    reclaim();
     proto_lock();
     pl_wait_free(); /* (two threads: the application frees the payload buffers) */
     const double t0 = mono_ms();
@@ -2036,52 +2099,87 @@ static uint64_t fnv64(const void *p, size_t n) {
     return h;
 }
 
-/* the fragments of ring items drain_tcb took out of a tcb, read after its
- * mutex is released: counted (EOF fragments are read and not counted),
- * copied into buf, and freed (a batch's hold on a payload buffer or on its
- * frames' mbufs ends here) */
-static void drain_detached(void **it, uint32_t k, void *buf, uint64_t *got, uint64_t *nb,
+/* what drain_all took out of the tcbs it visited, read after their mutexes
+ * are released */
+struct drain_scratch {
+    void **det; /* ring items taken out */
+    uint32_t nd, det_cap;
+    const unsigned char **fp; /* their fragments, flattened */
+    uint32_t *fl, fcap;
+};
+
+/* the detached items read: each fragment counted (EOF fragments are read and
+ * not counted), copied into buf, hashed (hs non-NULL), then the items freed
+ * (a batch's hold on a payload buffer or on its frames' mbufs ends there).
+ * The fragments lie scattered (in place: in their frames), so the copy loop
+ * prefetches the lines of the fragment DRAIN_AHEAD places ahead. */
+static void drain_detached(struct drain_scratch *sc, void *buf, uint64_t *got, uint64_t *nb,
                            uint64_t *hs) {
-    for (uint32_t i = 0; i < k; i++) {
-        struct tcp_fragment *f = it[i];
-        if (i + 1 < k) __builtin_prefetch(it[i + 1], 0, 0);
-        if (f->batch) {
-            const struct frag_batch *b = f->batch;
-            for (uint32_t j = b->next; j < b->n; j++) {
-                const struct tcp_fragment *g = &b->frag[j];
-                if (j + 1 < b->n && b->frag[j + 1].data)
-                    for (uint32_t o = 0; o < b->frag[j + 1].length; o += 64)
-                        __builtin_prefetch(b->frag[j + 1].data + o, 0, 0);
+    enum { DRAIN_AHEAD = 4 };
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < sc->nd; i++) {
+        const struct tcp_fragment *f = sc->det[i];
+        const uint32_t a = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
+        if (m + (n - a) > sc->fcap) {
+            uint32_t c1 = sc->fcap, c2 = sc->fcap;
+            if (grow((void **)&sc->fp, &c1, m + (n - a), sizeof(*sc->fp)) ||
+                grow((void **)&sc->fl, &c2, m + (n - a), sizeof(*sc->fl))) {
+                m = 0; /* (out of memory: read without the flat list) */
+                break;
+            }
+            sc->fcap = c1 < c2 ? c1 : c2;
+        }
+        for (uint32_t j = a; j < n; j++) {
+            const struct tcp_fragment *g = f->batch ? &f->batch->frag[j] : f;
+            sc->fp[m] = g->data;
+            sc->fl[m++] = g->length;
+        }
+    }
+    for (uint32_t i = 0; i < m; i++) {
+        if (i + DRAIN_AHEAD < m && sc->fl[i + DRAIN_AHEAD]) {
+            const uintptr_t p0 = (uintptr_t)sc->fp[i + DRAIN_AHEAD] & ~(uintptr_t)63;
+            const uintptr_t p1 = (uintptr_t)sc->fp[i + DRAIN_AHEAD] + sc->fl[i + DRAIN_AHEAD];
+            for (uintptr_t q = p0; q < p1; q += 64) __builtin_prefetch((const void *)q, 0, 0);
+        }
+        if (sc->fl[i]) {
+            memcpy(buf, sc->fp[i], sc->fl[i]);
+            (*got)++, *nb += sc->fl[i];
+            if (hs) *hs += fnv64(buf, sc->fl[i]);
+        }
+    }
+    for (uint32_t i = 0; i < sc->nd; i++) {
+        struct tcp_fragment *f = sc->det[i];
+        if (!m) { /* (the fallback: fragment by fragment) */
+            const uint32_t a = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
+            for (uint32_t j = a; j < n; j++) {
+                const struct tcp_fragment *g = f->batch ? &f->batch->frag[j] : f;
                 if (g->length) {
                     memcpy(buf, g->data, g->length);
                     (*got)++, *nb += g->length;
                     if (hs) *hs += fnv64(buf, g->length);
                 }
             }
-        } else if (f->length) {
-            memcpy(buf, f->data, f->length);
-            (*got)++, *nb += f->length;
-            if (hs) *hs += fnv64(buf, f->length);
         }
         frag_item_free(f);
     }
+    sc->nd = 0;
 }
 
 /* one tcb's receive ring emptied (its reference held): its items are taken
- * out under one hold of its mutex and read after it is released; an item
- * with a fragment longer than `cap` is read in place through nrecv's split
- * path */
+ * out under one hold of its mutex, to be read after it is released
+ * (drain_detached); an item with a fragment longer than `cap` is read in
+ * place through nrecv's split path */
 static void drain_tcb(struct tcp_stream *s, void *buf, size_t cap, uint64_t *got, uint64_t *nb,
-                      uint64_t *hs, void ***det, uint32_t *det_cap) {
-    uint32_t nd = 0;
+                      uint64_t *hs, struct drain_scratch *sc) {
     struct tcp_fragment *f;
     pthread_mutex_lock(&s->mutex);
     while (!s->dead && ring_peek(s->rcvbuf, (void **)&f) == 0) {
         const uint32_t first = f->batch ? f->batch->next : 0, n = f->batch ? f->batch->n : 1;
         uint32_t j = first;
         while (j < n && (f->batch ? f->batch->frag[j].length : f->length) <= cap) j++;
-        if (j < n || (nd == *det_cap && grow((void **)det, det_cap, *det_cap ? 2 * *det_cap : 256,
-                                             sizeof(void *)))) {
+        if (j < n || (sc->nd == sc->det_cap &&
+                      grow((void **)&sc->det, &sc->det_cap, sc->det_cap ? 2 * sc->det_cap : 256,
+                           sizeof(void *)))) {
             struct tcp_fragment *h = tq_front(s->rcvbuf);
             if (h->length > cap) {
                 pthread_mutex_unlock(&s->mutex);
@@ -2103,30 +2201,31 @@ static void drain_tcb(struct tcp_stream *s, void *buf, size_t cap, uint64_t *got
         }
         ring_dequeue(s->rcvbuf, (void **)&f);
         s->rq -= n - first;
-        (*det)[nd++] = f;
+        sc->det[sc->nd++] = f;
     }
     tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
     pthread_mutex_unlock(&s->mutex);
-    drain_detached(*det, nd, buf, got, nb, hs);
 }
 
 static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum) {
     /* The application side of the benchmark: every socket read until empty,
      * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
      * visited by stable id.  The stack's lock is held only to take a
-     * reference on the next DRAIN_CHUNK live blocks (a block stays valid
+     * reference on the next DRAIN_CHUNK live blocks (one hold for up to 8192
+     * blocks) (a block stays valid
      * while referenced, even if the protocol thread frees it meanwhile: its
      * memory goes with the last reference); everything else — the rings, the
      * copies — runs under each block's own mutex, beside the protocol
      * thread's deliveries (the reference's app lcore reads its socket rings
      * beside the protocol lcore, netfamily.c:424-430, udp.c:48,
      * common.c:531-536). */
-    enum { DRAIN_CHUNK = 1024 };
-    void *blk[DRAIN_CHUNK];
+    enum { DRAIN_CHUNK = 8192 };
+    void **blk = malloc(DRAIN_CHUNK * sizeof(void *));
+    if (!blk) return RXG_ENOMEM;
     uint64_t got = 0, nb = 0, hs = 0;
     uint64_t *hp = sum ? &hs : NULL;
-    void **det = NULL;
-    uint32_t det_cap = 0;
+    struct drain_scratch sc;
+    memset(&sc, 0, sizeof(sc));
     atomic_fetch_add_explicit(&g_drainers, 1, memory_order_relaxed);
     for (int kind = 0; kind < 2; kind++) {
         uint32_t id = 0;
@@ -2165,8 +2264,9 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
                                             : (void *)((struct localhost *)blk[i + 2])->rcvbuf,
                                        0, 0);
                 if (kind) {
-                    drain_tcb(blk[i], buf, cap, &got, &nb, hp, &det, &det_cap);
-                    tcb_put(blk[i]);
+                    drain_tcb(blk[i], buf, cap, &got, &nb, hp, &sc);
+                    tcb_put(blk[i]); /* (the items taken out are this call's) */
+                    if (sc.nd >= 256 || i + 1 == k) drain_detached(&sc, buf, &got, &nb, hp);
                 } else {
                     struct localhost *h = blk[i];
                     ssize_t r;
@@ -2181,7 +2281,10 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
             atomic_fetch_add_explicit(&g_drain_ns[2], (long long)((mono_ms() - c0) * 1e6), memory_order_relaxed);
         }
     }
-    free(det);
+    free(sc.det);
+    free(sc.fp);
+    free(sc.fl);
+    free(blk);
     atomic_fetch_sub_explicit(&g_drainers, 1, memory_order_relaxed);
     pthread_mutex_lock(&g_pl_mx); /* a waiting protocol thread re-checks */
     pthread_cond_broadcast(&g_pl_cv);
@@ -2208,6 +2311,8 @@ int nstack_set_rx_inplace(int on, void (*release)(rxg_mbuf *m, void *arg), void 
     pthread_mutex_unlock(&g_lock);
     return rc;
 }
+
+void nstack_reclaim(void) { reclaim(); }
 
 void nstack_mbufs_put(rxg_mbuf *const *m, uint32_t n) {
     for (uint32_t i = 0; i < n; i++)
@@ -2362,6 +2467,7 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
                     uint32_t max_frames, int cksum, uint64_t *span) {
     if (span) *span = 0;
     if (!pkts || !off || !len) return max_frames ? RXG_EINVAL : 0;
+    reclaim();
     proto_lock();
     uint32_t n = 0;
     uint64_t pos = 0;

@@ -761,6 +761,7 @@ class NStack:
                    ("nstack_drain_all_sum", C.c_int64, [_vp, C.c_size_t, _vp, _vp]),
                    ("nstack_set_rx_inplace", _i32, [_i32, _vp, _vp]),
                    ("nstack_mbufs_put", None, [_vp, _u32]),
+                   ("nstack_reclaim", None, []),
                    ("nstack_last_burst_phases", _i32, [_vp]),
                    ("nstack_tcb_state", _i32, [_u32, _u32, _u16, _u16, _vp, _vp, _vp, _vp]),
                    ("nstack_tcb_sndq", _i32, [_u32, _u32, _u16, _u16, _u32, _vp, _vp]),
@@ -966,6 +967,10 @@ class NStack:
         if not hasattr(self, "_held"):
             self._held = []
         _check(self.lib.nstack_set_rx_inplace(1 if on else 0, None, None), "nstack_set_rx_inplace")
+
+    def reclaim(self):
+        """nstack_reclaim: free what application threads let go of (protocol thread)"""
+        self.lib.nstack_reclaim()
 
     def mbufs_put(self, arr, n: int):
         """nstack_mbufs_put: drop the caller's reference on n mbufs"""

@@ -167,7 +167,7 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * the receive buffer each call uses.  Returns the datagrams + fragments
  * received (EOF fragments are read and not counted, as oracle_drain_all does;
  * a negative RXG_E* code on error); *bytes = the bytes the calls returned.
- * Takes the stack's lock only to take a reference on the next 1024 blocks
+ * Takes the stack's lock only to take a reference on the next 8192 blocks
  * (stepping aside while the protocol thread waits for it); the reads run
  * under each block's own mutex, so a concurrent nstack_rx_burst delivers
  * beside them, and a block freed meanwhile (last ACK) stays valid until the
@@ -191,6 +191,12 @@ int64_t nstack_drain_all_sum(void *buf, size_t cap, uint64_t *bytes, uint64_t *s
  * returns (nstack_mbufs_put); an mbuf's frame must stay in place until its
  * count is 0. */
 int nstack_set_rx_inplace(int on, void (*release)(rxg_mbuf *m, void *arg), void *arg);
+/* Items the application has read (fragments, datagram batches) are handed
+ * back to the protocol thread and freed by its next nstack_rx_burst /
+ * nstack_tx_burst / nstack_deliver call (or nstack_reclaim, a protocol-thread
+ * call): in place, a frame's mbuf count reaches 0 there.  A thread that made
+ * one of those calls frees what it reads at once. */
+void nstack_reclaim(void);
 /* drop one reference on each of n mbufs (rte_pktmbuf_free of a burst):
  * release(m, arg) of nstack_set_rx_inplace for each whose count reaches 0 */
 void nstack_mbufs_put(rxg_mbuf *const *m, uint32_t n);

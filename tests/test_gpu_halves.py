@@ -317,6 +317,7 @@ def test_two_threads_receive_every_byte(torch_dev, mode):
         finally:
             stop.set()
             th.join()
+        ns.reclaim()  # (the application thread's reads are freed by the protocol side)
         assert (got[0], got[1]) == (want_items, want_bytes)
         assert got[2] == want_sum
         assert ns.stat(7) == 0  # no batch left holding a payload buffer

@@ -33,6 +33,20 @@ if [ "${SWING:-0}" = 1 ]; then
   step swing_after 240 python tools/cfg2_swing.py || exit $?
   grep '^{' $OUT/swing_after.log > $OUT/swing_after_$TAG.json || true
 fi
+if [ "${SWINGDIAG:-0}" = 1 ]; then
+  # right after the tests (the order the driver and round 4 used): short
+  # cfg2 + cfg5 benches back to back, then after a pause, with amd-smi
+  # (clocks, power, temperatures) sampled all along
+  ( while true; do echo "T $(date +%s.%N)"; timeout 10 amd-smi metric -g 0 -c -p -t 2>/dev/null; sleep 0.2; done ) > $OUT/smi_$TAG.log 2>&1 &
+  SMI=$!
+  Q="--workload cfg2,cfg5 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
+  for k in 1 2; do echo "T $(date +%s.%N) quick$k" >> $OUT/smi_marks_$TAG.log; bench quick$k 240 $Q || { kill $SMI; exit 1; }; done
+  sleep 20
+  echo "T $(date +%s.%N) quick3" >> $OUT/smi_marks_$TAG.log
+  bench quick3 240 $Q || { kill $SMI; exit 1; }
+  echo "T $(date +%s.%N) end" >> $OUT/smi_marks_$TAG.log
+  kill $SMI
+fi
 export TMPDIR=/tmp
 if [ "${PMC:-0}" = 1 ]; then
   step pmc 900 python tools/pmc_traffic.py $TAG cfg2,cfg3,cfg4,cfg5 || exit $?
