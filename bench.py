@@ -1492,6 +1492,9 @@ def main():
     ap.add_argument("--flow-load", type=int, default=0,
                     help="flow tables at load <= 2**-N (rxg_tune_flow_load; 0 = default)")
     ap.add_argument("--sweep-counts", action="store_true", help="sweep with per-flow counts on")
+    ap.add_argument("--tune-tables", type=int, default=0,
+                    help="rxg_tune_tables flags (A/B: 4 = RXG_TT_COUNT_2BUF, the round-4 two "
+                         "count-index buffers)")
     ap.add_argument("--shard-gen", default="direct", choices=["direct", "split"],
                     help="N > 1: each rank generates its RSS shard directly (direct) or every "
                          "rank generates the global burst, splits it and gathers its shard "
@@ -1563,6 +1566,8 @@ def main():
     ctx = R.Context(local)
     if a.flow_load:
         ctx.tune_flow_load(a.flow_load)
+    if a.tune_tables:
+        ctx.tune_tables(a.tune_tables)
     global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8
     V8 = not a.no_v8
     RAMP_MS = a.ramp_ms

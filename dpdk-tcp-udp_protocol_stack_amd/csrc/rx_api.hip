@@ -200,7 +200,7 @@ struct rxg_ctx {
         hipEvent_t ev = nullptr;
         hipStream_t st = nullptr;
         bool used = false;
-    } wu[3];
+    } wu[4]; // index buffers 0..2, slabs (WS_*)
     // region offsets depend on the burst shape (frame count, binned path, size);
     // a change of shape waits on every region
     struct ws_shape {
@@ -210,6 +210,7 @@ struct rxg_ctx {
         bool operator!=(const ws_shape &o) const { return n != o.n || lists != o.lists || bytes != o.bytes; }
     } ws_layout;
     uint32_t ws_flip = 0; // index buffer of the next split-stream burst
+    uint32_t ws_nbuf = 3; // index buffers of the split-stream bursts (RXG_TT_COUNT_2BUF: 2)
     hipEvent_t ev_k1 = nullptr; // split-stream burst: classify done (count stream waits on it)
     void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
     size_t d_aux_cap = 0;
@@ -1120,9 +1121,11 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B))) return RXG_EINVAL;
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_COUNT_2BUF)))
+        return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
+    c->ws_nbuf = (flags & RXG_TT_COUNT_2BUF) ? 2u : 3u;
     return RXG_OK;
 }
 
@@ -1201,7 +1204,7 @@ uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport
 }
 
 // workspace regions (rxg_ctx::wu)
-enum { WS_BUF0 = 0, WS_BUF1 = 1, WS_SLAB = 2 };
+enum { WS_BUF0 = 0, WS_BUF1 = 1, WS_BUF2 = 2, WS_SLAB = 3 };
 
 static hipError_t ws_wait(rxg_ctx *c, int r, hipStream_t s) {
     const rxg_ctx::ws_use &u = c->wu[r];
@@ -1228,7 +1231,7 @@ static int ws_prepare(rxg_ctx *c, size_t ws, const rxg_ctx::ws_shape &layout, hi
         int rc = ensure_dev_async((void **)&c->d_ws, &c->d_ws_cap, ws, s);
         if (rc) return rc;
     } else if (layout != c->ws_layout) {
-        for (int r = 0; r < 3; ++r) HIPCHK(ws_wait(c, r, s));
+        for (int r = 0; r < 4; ++r) HIPCHK(ws_wait(c, r, s));
     }
     c->ws_layout = layout;
     return RXG_OK;
@@ -1240,7 +1243,13 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
                        const uint16_t *d_len, uint32_t n, uint32_t off_unit_log2, uint32_t g,
                        uint32_t p, uint32_t fpg, uint32_t pipe, uint4 *d_out,
                        unsigned long long *d_counts, hipStream_t s, hipStream_t cs) {
-    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr, 2);
+    // three index buffers: burst k's classify writes buffer k % 3, which the
+    // count of burst k - 3 read (long done), so it never waits for the count
+    // of burst k - 2, whose slab blocks (a whole CU each) can only start once
+    // burst k - 1's classify drains.  With two, every step waited for that
+    // count (+2.5% per step at cfg4, rocprofv3 trace, profiles/r05b)
+    const uint32_t nb = c->ws_nbuf;
+    const size_t ws = rx_classify_ws_bytes(n, g, pipe, c->ft, d_counts != nullptr, nb);
     const bool split = cs && cs != s && pipe != 20 && rx_count_uses_slabs(c->ft, d_counts != nullptr);
     // counts the classify kernel adds itself (few flows), or the binned path's:
     // the count stream is ordered after this burst's kernels, as promised
@@ -1256,7 +1265,7 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
     const auto k1 = c->ft.v8 ? rx_classify_launch8 : rx_classify_launch;
     if (!ws) {
         HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
-                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
+                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, nb));
         return join_cs();
     }
     rxg_ctx::ws_shape layout;
@@ -1269,21 +1278,21 @@ static int classify_ws_body(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *d
         HIPCHK(ws_wait(c, WS_BUF0, s));
         HIPCHK(ws_wait(c, WS_SLAB, s));
         HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
-                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, 2));
+                                  d_out, d_counts, s, c->d_ws, RX_PH_ALL, 0, nb));
         HIPCHK(ws_mark(c, WS_BUF0, s));
         HIPCHK(ws_mark(c, WS_SLAB, s));
         return join_cs();
     }
-    const uint32_t b = c->ws_flip;
-    c->ws_flip ^= 1u;
+    const uint32_t b = c->ws_flip % nb;
+    c->ws_flip = (b + 1u) % nb;
     HIPCHK(ws_wait(c, b, s)); // the count that last read this index buffer
     HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
-                              d_out, d_counts, s, c->d_ws, RX_PH_CLASSIFY, b, 2));
+                              d_out, d_counts, s, c->d_ws, RX_PH_CLASSIFY, b, nb));
     HIPCHK(hipEventRecord(c->ev_k1, s));
     HIPCHK(hipStreamWaitEvent(cs, c->ev_k1, 0));
     HIPCHK(ws_wait(c, WS_SLAB, cs));
     HIPCHK(k1(d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe, c->ft,
-                              d_out, d_counts, cs, c->d_ws, RX_PH_COUNT, b, 2));
+                              d_out, d_counts, cs, c->d_ws, RX_PH_COUNT, b, nb));
     HIPCHK(ws_mark(c, b, cs)); // covers the classify too (cs waited on it)
     HIPCHK(ws_mark(c, WS_SLAB, cs));
     return RXG_OK;

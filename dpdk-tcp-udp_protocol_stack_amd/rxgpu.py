@@ -192,6 +192,7 @@ _tune_flow_load = _sig("rxg_tune_flow_load", _i32, _vp, _u32)
 _tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
 TT_NO_UDP_PORT = 0x1
 TT_COUNT_4B = 0x2
+TT_COUNT_2BUF = 0x4
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)

@@ -517,9 +517,13 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
  * RXG_TT_NO_UDP_PORT (applied by the next rxg_flows_sync): no direct UDP port
  * table; every UDP lookup probes the hashed table.  RXG_TT_COUNT_4B (applied
  * at once): the 8193..2M-flow count path keeps 4-B count indices even at
- * <= 65536 flows.  Verdicts and counts depend on neither. */
+ * <= 65536 flows.  RXG_TT_COUNT_2BUF (applied at once): see below.  Verdicts
+ * and counts depend on none of them. */
 #define RXG_TT_NO_UDP_PORT 0x1u
 #define RXG_TT_COUNT_4B 0x2u
+#define RXG_TT_COUNT_2BUF 0x4u /* rxg_classify_dev_cs: two count-index buffers instead of
+                                  three (each burst then waits for the count of the
+                                  burst before the previous one) */
 
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 

@@ -67,6 +67,13 @@ if [ "${BENCH:-1}" = 1 ]; then
     cat $OUT/roofline_check_$TAG.txt
   fi
 fi
+if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs two, alternating
+  Q="--workload cfg4 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
+  for k in 1 2; do
+    bench ab3buf$k 240 $Q || exit $?
+    bench ab2buf$k 240 $Q --tune-tables 4 || exit $?
+  done
+fi
 if [ "${N2:-0}" = 1 ]; then
   bench n2 400 --gpus 2 --steps 5 --warmup 2 || exit $?
 fi
