@@ -67,6 +67,10 @@ if [ "${BENCH:-1}" = 1 ]; then
     cat $OUT/roofline_check_$TAG.txt
   fi
 fi
+if [ "${MEMBW3:-0}" = 1 ]; then  # cfg3 access-shape ceilings (tools/membw_cfg3.hip)
+  step membw_cfg3 150 ./tools/membw_cfg3 || exit $?
+  cp $OUT/membw_cfg3.log $OUT/membw_cfg3_$TAG.txt
+fi
 if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs two, alternating
   Q="--workload cfg4 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
   for k in 1 2; do

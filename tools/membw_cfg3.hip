@@ -1,0 +1,165 @@
+// membw_cfg3.hip — access-shape ceilings for the 1500-B workload (cfg3: 4M
+// frames in 1536-B slots, 1504 captured bytes = 94 chunks of 16 B read per
+// slot, one 16-B store per slot), with no per-frame work beyond a byte sum.
+// Diagnostics only: is a shape whose
+// wave-instructions read each wave's frames as contiguous 1-KiB spans faster
+// than the G=8 group shape of the classify kernel?
+//   stream  : plain grid-stride read of the whole buffer (the read ceiling)
+//   slotg8  : G=8 lanes per slot, 12 passes in flight (the K1 shape, pipe 40)
+//   waveF   : a wave owns F consecutive slots (F*1.5 KiB contiguous), each
+//             lane 1.5*F 16-B loads, every load of the wave one 1-KiB
+//             contiguous span; per-slot sums by a segmented wave reduce
+//             (DPP / swizzle through __shfl_xor); PIPE = the next wave-tile's
+//             loads issued before this one is reduced (register double buffer)
+//   hipcc --offload-arch=gfx950 -O3 tools/membw_cfg3.hip -o tools/membw_cfg3
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CHK(x)                                                                                     \
+    do {                                                                                           \
+        hipError_t e = (x);                                                                        \
+        if (e != hipSuccess) {                                                                     \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);                        \
+            exit(1);                                                                               \
+        }                                                                                          \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 ldnt(const u32x4 *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ unsigned csum(u32x4 v) { return v.x + v.y + v.z + v.w; }
+
+__global__ __launch_bounds__(256) void k_stream(const u32x4 *__restrict__ in, size_t n16,
+                                                unsigned *__restrict__ sink) {
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+        acc += csum(ldnt(in + i));
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// G = 8 lanes per 1536-B slot, all 12 passes in flight (94 chunks read)
+__global__ __launch_bounds__(256) void k_slotg8(const u32x4 *__restrict__ in, size_t nslots,
+                                                u32x4 *__restrict__ out) {
+    const unsigned gl = threadIdx.x & 7u;
+    const size_t groups = (size_t)gridDim.x * 32;
+    for (size_t f = (size_t)blockIdx.x * 32 + (threadIdx.x >> 3); f < nslots; f += groups) {
+        const u32x4 *p = in + f * 96;
+        u32x4 v[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const unsigned c = q * 8 + gl;
+            v[q] = c < 94 ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+        }
+        unsigned acc = 0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc += csum(v[q]);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (gl == 0) __builtin_nontemporal_store(u32x4{acc, (unsigned)f, 0, 0}, out + f);
+    }
+}
+
+// a wave owns F consecutive slots per trip (F even: 1.5 * F loads per lane);
+// load j of lane l reads chunk 64 j + l of the wave-tile, which belongs to
+// slot (64 j + l) / 96; chunks 94, 95 of each slot are padding (not counted)
+template <int F, bool PIPE>
+__global__ __launch_bounds__(256) void k_wave(const u32x4 *__restrict__ in, size_t nslots,
+                                              u32x4 *__restrict__ out) {
+    constexpr int NL = F * 96 / 64;
+    const unsigned lane = threadIdx.x & 63u;
+    const size_t nw = (size_t)gridDim.x * 4;
+    const size_t ntiles = nslots / F; // (the buffer holds whole wave-tiles)
+    size_t t = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    u32x4 v[NL], nv[NL];
+    auto load = [&](u32x4 *dst, size_t tile) {
+        const u32x4 *p = in + (tile < ntiles ? tile : 0) * (F * 96);
+#pragma unroll
+        for (int j = 0; j < NL; ++j) dst[j] = ldnt(p + 64 * j + lane);
+    };
+    if (t < ntiles) load(v, t);
+    for (; t < ntiles; t += nw) {
+        if (PIPE) load(nv, t + nw);
+        unsigned s[F];
+#pragma unroll
+        for (int k = 0; k < F; ++k) s[k] = 0;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const unsigned c = 64 * j + lane; // chunk in the tile
+#pragma unroll
+            for (int k = 0; k < F; ++k) {
+                // compile-time: which slots load j can touch
+                if (64 * j + 63 >= 96 * k && 64 * j < 96 * k + 96) {
+                    const unsigned r = c - 96u * k;
+                    s[k] += (r < 94u) ? csum(v[j]) : 0u;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) s[k] += __shfl_xor(s[k], o);
+        }
+        if (lane < (unsigned)F) {
+            unsigned a = s[0];
+#pragma unroll
+            for (int k = 1; k < F; ++k) a = lane == (unsigned)k ? s[k] : a;
+            __builtin_nontemporal_store(u32x4{a, (unsigned)(t * F + lane), 0, 0}, out + t * F + lane);
+        }
+        if (PIPE) {
+#pragma unroll
+            for (int j = 0; j < NL; ++j) v[j] = nv[j];
+        } else if (t + nw < ntiles) {
+            load(v, t + nw);
+        }
+    }
+}
+
+template <typename K>
+float timeit(K f, int reps) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    f();
+    f();
+    CHK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    const size_t nslots = 4u << 20, bytes = nslots * 1536;
+    const double alg = (double)nslots * (1500 + 22);
+    u32x4 *in, *out;
+    unsigned *sink;
+    CHK(hipMalloc(&in, bytes));
+    CHK(hipMalloc(&out, nslots * 16));
+    CHK(hipMalloc(&sink, 64));
+    CHK(hipMemset(in, 1, bytes));
+    int cu = 0;
+    CHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
+    const int reps = 20;
+    for (int round = 0; round < 3; ++round) {
+        for (int bpc : {4, 8}) {
+            const int g = cu * bpc;
+            float ms = timeit([&] { k_stream<<<g, 256>>>(in, bytes / 16, sink); }, reps);
+            printf("r%d bpc=%d stream          %.4f ms %7.0f GB/s (read)\n", round, bpc, ms,
+                   bytes / ms / 1e6);
+            ms = timeit([&] { k_slotg8<<<g, 256>>>(in, nslots, out); }, reps);
+            printf("r%d bpc=%d slotg8          %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
+#define W(F, P)                                                                                    \
+    ms = timeit([&] { k_wave<F, P><<<g, 256>>>(in, nslots, out); }, reps);                         \
+    printf("r%d bpc=%d wave F=%d pipe=%d   %.4f ms %7.0f GB/s (alg)\n", round, bpc, F, (int)P, ms,   \
+           alg / ms / 1e6);
+            W(2, false) W(2, true) W(4, false) W(4, true) W(8, false)
+#undef W
+        }
+    }
+    return 0;
+}
