@@ -2256,13 +2256,25 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
             pthread_mutex_unlock(&g_lock);
             const double c0 = mono_ms();
             for (uint32_t i = 0; i < k; i++) {
-                /* look-ahead: the blocks 2-4 ahead and their receive rings
-                 * (referenced, so valid; no ring item is dereferenced) */
+                /* look-ahead (every address formed from memory this call keeps
+                 * alive: the referenced blocks, their rings and slot arrays,
+                 * which live as long as the block; no ring item is read): the
+                 * block 4 ahead, the ring of the one 2 ahead, and the head item
+                 * of the next one's ring — its lines prefetched as they lie,
+                 * a fragment batch's header and first fragments (frag_batch:
+                 * the item, then its fragments), whatever the head slot holds
+                 * by the time it is read */
                 if (i + 4 < k) __builtin_prefetch(blk[i + 4], 0, 0);
                 if (i + 2 < k)
                     __builtin_prefetch(kind ? (void *)((struct tcp_stream *)blk[i + 2])->rcvbuf
                                             : (void *)((struct localhost *)blk[i + 2])->rcvbuf,
                                        0, 0);
+                if (kind && i + 1 < k) {
+                    const struct nring *r = ((struct tcp_stream *)blk[i + 1])->rcvbuf;
+                    const char *it = (const char *)r->slot[r->head % r->cap];
+                    if (it)
+                        for (int q = 0; q < 8; q++) __builtin_prefetch(it + 64 * q, 0, 0);
+                }
                 if (kind) {
                     drain_tcb(blk[i], buf, cap, &got, &nb, hp, &sc);
                     tcb_put(blk[i]); /* (the items taken out are this call's) */
