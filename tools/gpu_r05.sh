@@ -79,6 +79,10 @@ if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs 
   done
 fi
 if [ "${N2:-0}" = 1 ]; then
+  # the N = 2 logic with two ranks on this one GPU: the default per-rank
+  # shards, then the split of one global burst (the golden frame digest over
+  # both ranks)
   bench n2 400 --gpus 2 --steps 5 --warmup 2 || exit $?
+  bench n2split 400 --gpus 2 --steps 5 --warmup 2 --shard-gen split --workload cfg2,cfg3 || exit $?
 fi
 echo ALLDONE
