@@ -2338,6 +2338,289 @@ hipError_t launch_sh(const uint8_t *pkts, const uint32_t *off, const uint16_t *l
 }
 
 // ---------------------------------------------------------------------------
+// WC kernel (RX_DIAG pipes 80-83; the access-shape experiment of VERDICT r4
+// next #7, tools/membw_cfg3.hip): a wave owns F consecutive frames per trip
+// and reads their byte span as contiguous 1-KiB wave-instructions (lane l
+// loads chunk 64 j + l of the span), where the G=8 group kernel's
+// instructions touch 8 frames x 128 B.  Each lane adds its chunks past a
+// frame's head (chunks 4.., the last masked at the capture) into that frame's
+// partial; a wave reduce per frame gives the tail sums; the frames' head
+// chunks 0..3 go through LDS to the frame's owner lane (lane f), which
+// parses them, adds the head sum and, as the SH kernel's end of block,
+// probes, checks and writes the verdict.  The next trip's span is loaded
+// while the probes are in flight (PIPE).  A trip whose frames are not dense
+// (out of order, overlapping, a span over 64 * NL chunks), and a frame whose
+// checksummed bytes end before its capture, take the generic paths (the whole
+// wave per frame; the tail re-summed from HBM by its owner).
+template <int F, int NL, bool PIPE>
+__global__ __launch_bounds__(256) void rx_classify_wc_kernel(
+    const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
+    const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
+    uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins) {
+    static_assert(F >= 1 && F <= 8 && NL >= 1 && NL <= 12, "wave tile");
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    __shared__ __attribute__((aligned(16))) uint4 s_hd[4][F][4]; // per wave: head chunks
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+    if (lds_bins) __syncthreads();
+    const uint64_t ntile = ((uint64_t)n + F - 1) / F;
+    const uint64_t nw = (uint64_t)gridDim.x * 4u;
+    // a trip's frames, wave-uniform after readlane: frame t*F + f at byte fo[f]
+    // (relative to fo[0]), capture cp[f]; dense: the span fits the loads
+    struct trip {
+        uint64_t t, base;
+        uint32_t fo[F];
+        int32_t cp[F];
+        uint32_t span; // chunks
+        bool dense;
+    };
+    auto desc = [&](uint64_t t, uint32_t &o, int32_t &c) {
+        const uint64_t p = t * F + (lane < (uint32_t)F ? lane : 0u);
+        const bool v = t < ntile && lane < (uint32_t)F && p < n;
+        o = off[v ? p : 0];
+        c = v ? (int32_t)len[v ? p : 0] : 0;
+    };
+    auto geometry = [&](trip &T, uint64_t t, uint32_t o, int32_t c) {
+        T.t = t;
+        uint64_t pos[F];
+        bool ok = t < ntile;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            pos[f] = (uint64_t)__builtin_amdgcn_readlane((int)o, f) << unit_log2;
+            T.cp[f] = __builtin_amdgcn_readlane(c, f);
+        }
+        T.base = pos[0];
+        uint64_t end = pos[0];
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const uint64_t e = pos[f] + (uint64_t)((T.cp[f] + 15) & ~15);
+            if (T.cp[f] > 0) {
+                ok = ok && pos[f] >= end; // in order, no overlap
+                end = e;
+            }
+            T.fo[f] = (uint32_t)((pos[f] - T.base) >> 4);
+        }
+        const uint64_t sp = (end - T.base) >> 4;
+        T.dense = ok && sp <= 64u * NL;
+        T.span = T.dense ? (uint32_t)sp : 0u;
+    };
+    auto load = [&](uint4 (&v)[NL], const trip &T) {
+        const uint8_t *b = pkts + T.base;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const uint32_t k = 64u * j + lane;
+            v[j] = ldg16<true>(b + ((uint64_t)(k < T.span ? k : 0u) << 4)); // masked at use
+        }
+    };
+
+    uint64_t t = (uint64_t)blockIdx.x * 4u + wv;
+    trip T, N;
+    uint4 v[NL], nv[NL];
+    {
+        uint32_t o;
+        int32_t c;
+        desc(t, o, c);
+        geometry(T, t, o, c);
+        load(v, T);
+    }
+    for (; t < ntile; t += nw) {
+        uint32_t no;
+        int32_t nc;
+        desc(t + nw, no, nc); // the next trip's descriptors, in flight through this one
+        // ---- the frames' partial sums (chunks 4..) and head chunks to LDS
+        uint32_t ps[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) ps[f] = 0;
+        if (T.dense) {
+#pragma unroll
+            for (int j = 0; j < NL; ++j) {
+                const uint32_t k = 64u * j + lane;
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    const uint32_t r = k - T.fo[f]; // chunk of frame f (wraps below it)
+                    const int32_t cpf = T.cp[f];
+                    if (k < T.span && r < ((uint32_t)cpf + 15u) >> 4) {
+                        if (r < 4u)
+                            s_hd[wv][f][r] = v[j];
+                        else
+                            ps[f] = lane_chunk_sum(ps[f], v[j], 16 * (int32_t)r, cpf);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < F; ++f) ps[f] = gsum<64>(ps[f]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- owner lane f: parse, sums, probe loads
+        const uint32_t fl = lane < (uint32_t)F ? lane : 0u;
+        int32_t cp = 0;
+        uint32_t tail = 0;
+#pragma unroll
+        for (int f = 0; f < F; ++f)
+            if (fl == (uint32_t)f) cp = T.cp[f], tail = ps[f];
+        const uint64_t p = t * F + fl;
+        const bool valid = lane < (uint32_t)F && t < ntile && p < n;
+        const uint8_t *fb = pkts + ((uint64_t)off[valid ? p : 0] << unit_log2);
+        uint4 c[4];
+        if (T.dense) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[k] = chunk_below(s_hd[wv][fl][k], 16 * k, cp);
+        }
+        if (!T.dense) { // (wave-uniform) heads from HBM
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                c[k] = chunk_below(ldg16<false>(valid && 16 * k < cp ? fb + 16 * k : pkts), 16 * k, cp);
+        }
+        const sh_head h = sh_parse(c, cp);
+        uint32_t acc = sh_head_sum(c, h);
+        const int32_t e = h.e;
+        const bool resum = h.do_sum && e > 64 && (!T.dense || e != cp);
+        if (h.do_sum && e > 64 && !resum) acc += tail;
+        if (__ballot(valid && resum) != 0ull) { // rare (wave-uniform branch): the tail from HBM
+            if (valid && resum)
+                for (int32_t s = 64; s < e; s += 16) acc = lane_chunk_sum(acc, ldg16<false>(fb + s), s, e);
+        }
+        // probe loads: the port entry and the hashed table's 4-slot window
+        const bool probe = valid && h.l4;
+        const uint32_t maxp = h.is_udp ? ft.udp_probe : ft.tcp_probe;
+        const bool probe0 = probe && maxp > 0;
+        const bool udp_port = h.is_udp && ft.udp_port != nullptr;
+        const bool hash0 = probe0 && !udp_port;
+        const uint32_t *ptab = udp_port ? ft.udp_port : ft.listen;
+        const uint32_t dport = h.is_udp ? h.kb : (h.kc >> 16);
+        const uint32_t pe = probe ? ptab[dport] : RXG_FLOW_NONE;
+        constexpr int PW = 4;
+        uint32_t pj = rx_hash3s(ft.hseed, h.ka, h.kb, h.kc) & (h.is_udp ? ft.udp_mask : ft.tcp_mask);
+        const uint4 *tb = h.is_udp ? ft.udp : ft.tcp;
+        uint4 sw[PW];
+#pragma unroll
+        for (int w = 0; w < PW; ++w) sw[w] = ld_slot(hash0 ? tb + pj + w : reinterpret_cast<const uint4 *>(pkts));
+        // the next trip's span, in flight while the probes return
+        if constexpr (PIPE) {
+            geometry(N, t + nw, no, nc);
+            load(nv, N);
+        }
+        // ---- verdict
+        uint32_t ck = 0;
+        if (h.do_sum) {
+            ck = (~fold16(acc)) & 0xFFFFu;
+            if (ck == 0u && h.proto == 17u) ck = 0xFFFFu;
+        }
+        uint32_t flags = 0, poff = 0, plen = 0;
+        if (h.is_udp) {
+            poff = 42;
+            plen = h.dgl > 8u ? h.dgl - 8u : 0u;
+            if (h.dgl <= 8u) flags |= RXG_F_UDP_SHORT;
+        } else if (h.is_tcp) {
+            const int32_t pl = (int32_t)h.tl - 20 - 4 * (int32_t)h.hl;
+            poff = 34u + 4u * h.hl;
+            if (pl < 0) flags |= RXG_F_TCP_NEGLEN;
+            plen = pl < 0 ? 0u : (uint32_t)pl;
+        }
+        const bool trunc = (int32_t)h.nd > cp;
+        const bool trunc_ok = trunc || (h.is_udp && (int32_t)(42u + plen) > cp);
+        uint32_t flow = RXG_FLOW_NONE;
+        int32_t rc = RXG_RC_KNI;
+        bool hashed = probe0;
+        if (probe0 && udp_port) hashed = !rx_udp_port_decide(pe, h.ka, ft.udp_dip, &flow);
+        if (hashed) {
+            const uint32_t mk = h.is_udp ? ft.udp_mask : ft.tcp_mask;
+            uint32_t pr = 0;
+            bool done = false;
+            if (hash0) {
+#pragma unroll
+                for (int w = 0; w < PW; ++w) {
+                    if (!done) {
+                        const uint4 sl = sw[w];
+                        if (sl.w == RX_SLOT_EMPTY) {
+                            done = true;
+                        } else if (sl.x == h.ka && sl.y == h.kb && sl.z == h.kc) {
+                            flow = sl.w;
+                            done = true;
+                        } else if (++pr >= maxp) {
+                            done = true;
+                        } else {
+                            pj = (pj + 1) & mk;
+                        }
+                    }
+                }
+            }
+            while (!done) { // past the window, or a UDP key on a shared port
+                const uint4 sl = ld_slot(tb + pj);
+                if (sl.w == RX_SLOT_EMPTY) break;
+                if (sl.x == h.ka && sl.y == h.kb && sl.z == h.kc) {
+                    flow = sl.w;
+                    break;
+                }
+                if (++pr >= maxp) break;
+                pj = (pj + 1) & mk;
+            }
+        }
+        if (h.is_tcp && valid && flow == RXG_FLOW_NONE) flow = pe; // listener
+        if (h.is_udp)
+            rc = flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                       : ((flags & RXG_F_UDP_SHORT) ? RXG_RC_UDP_NOMEM : RXG_RC_OK);
+        if (rc == RXG_RC_OK ? trunc_ok : trunc) flags |= RXG_F_TRUNC;
+        const bool ok = h.l4 && h.stored == ck;
+        if (h.is_tcp) {
+            if (!ok) flow = RXG_FLOW_NONE;
+            rc = !ok ? RXG_RC_TCP_BAD_CKSUM : (flow == RXG_FLOW_NONE ? RXG_RC_TCP_NO_TCB : RXG_RC_OK);
+        }
+        if (valid) {
+            const uint32_t cidx =
+                rc == RXG_RC_OK && flow != RXG_FLOW_NONE ? (h.is_tcp ? ft.nu : 0u) + flow : 0xFFFFFFFFu;
+            uint4 vd;
+            vd.x = flow;
+            vd.y = (poff & 0xFFFFu) | (plen << 16);
+            vd.z = ck | (h.cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+            vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
+            st_verdict(ft, out, p, vd);
+            lane_count(cidx, counts, hist, lds_bins);
+            if (ft.count_idx) put_count_idx(ft, p, cidx);
+        }
+        if constexpr (PIPE) {
+            T = N;
+#pragma unroll
+            for (int j = 0; j < NL; ++j) v[j] = nv[j];
+        } else {
+            geometry(T, t + nw, no, nc);
+            load(v, T);
+        }
+        // (the next trip's LDS head writes follow this trip's reads in the wave's order)
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lds_bins) {
+        __syncthreads();
+        for (uint32_t i = tid; i < lds_bins; i += 256) {
+            const uint32_t cnt = hist[i];
+            if (cnt) atomicAdd(&counts[i], (unsigned long long)cnt);
+        }
+    }
+}
+
+template <int F, int NL, bool PIPE>
+hipError_t launch_wc(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
+                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
+                     uint32_t lds_bins, hipStream_t s, const uint32_t *, const uint32_t *) {
+    const size_t lds = (size_t)lds_bins * 4u;
+    int cu = 0, bpc = 0;
+    hipError_t e = rx_occupancy(reinterpret_cast<const void *>(rx_classify_wc_kernel<F, NL, PIPE>), 256,
+                                lds, &cu, &bpc);
+    if (e != hipSuccess) return e;
+    uint64_t occ = (uint64_t)bpc;
+    if (ft.bpc_cap && occ > ft.bpc_cap) occ = ft.bpc_cap;
+    const uint64_t waves = ((uint64_t)n + F - 1) / F;
+    uint64_t blocks = (uint64_t)cu * occ;
+    if (blocks * 4 > waves) blocks = (waves + 3) / 4;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL((rx_classify_wc_kernel<F, NL, PIPE>), dim3((uint32_t)blocks), dim3(256), lds, s,
+                       pkts, off, len, n, unit_log2, ft, out, counts, lds_bins);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Per-flow counts for 8192 < flows <= 2M (too many for a per-block LDS
 // histogram at full occupancy, and scattered 8-B global atomics each cost one
 // memory-side request): the classify kernel writes one count index per frame
@@ -2683,6 +2966,11 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 1064, launch_sh<16, 4>}, {0, 1, 1, 2064, launch_sh<32, 4>},
     // 167: 67 without the flow probe
     {0, 1, 1, 167, launch_sh<1, 4, SH_MAPC, false, 2>},
+    // ---- the wave-contiguous shape (WC kernel): F frames per wave trip, NL
+    // loads per lane; 80 / 81: F = 2, NL = 3 (1.5-KiB slots) with / without
+    // the next trip's span in flight; 82 / 83: F = 4, NL = 6
+    {0, 1, 1, 80, launch_wc<2, 3, true>}, {0, 1, 1, 81, launch_wc<2, 3, false>},
+    {0, 1, 1, 82, launch_wc<4, 6, true>}, {0, 1, 1, 83, launch_wc<4, 6, false>},
 #endif
 };
 
@@ -2730,6 +3018,8 @@ const char *rx_variant_kernel(uint32_t g, uint32_t pipe) {
     case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
     case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78:
         return "rx_classify_sh_kernel";
+    case 80: case 81: case 82: case 83:
+        return "rx_classify_wc_kernel";
     default:
         return "rx_classify_stream_kernel";
     }

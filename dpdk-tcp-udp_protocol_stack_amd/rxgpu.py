@@ -59,7 +59,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 0),
 # compiled only into the RX_DIAG build (librxgpu_diag.so, RXGPU_LIB=...):
 # tuning shapes with correct verdicts ...
 DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (8, 2, 2, 1), (16, 2, 1, 0), (0, 0, 0, 54), (0, 0, 0, 66),
-                        (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65)]
+                        (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65),
+                        (0, 0, 0, 80), (0, 0, 0, 81), (0, 0, 0, 82), (0, 0, 0, 83)]  # WC kernel
 # ... and ablations, wrong verdicts (or counts) by construction
 DIAG_ABLATIONS = [(1, 4, 1, 101), (1, 4, 1, 104), (1, 4, 1, 108), (1, 4, 1, 113), (1, 4, 1, 201),
                   (1, 4, 1, 204), (1, 4, 1, 213), (0, 0, 0, 130), (0, 0, 0, 46), (0, 0, 0, 146),

@@ -177,7 +177,8 @@ def test_verdict8_odd_and_unaligned(ctx, torch_dev, n, shift):
     assert got.tobytes() == want8.tobytes(), (n, shift, _mismatch_report(got, want8))
 
 
-@pytest.mark.parametrize("variant", R.KERNEL_VARIANTS, ids=lambda v: "v" + "-".join(map(str, v)))
+@pytest.mark.parametrize("variant", R.compiled_variants(R.KERNEL_VARIANTS + R.DIAG_TUNING_VARIANTS),
+                         ids=lambda v: "v" + "-".join(map(str, v)))
 def test_every_kernel_variant(ctx, torch_dev, variant):
     """each compiled (lanes, passes, frames-per-group) variant, on mixed sizes"""
     fl = np.load(os.path.join(GOLD, "edge_flows.npz"))
@@ -744,3 +745,31 @@ def test_sh_short_spans(ctx, torch_dev, variant, size):
         ctx.tune(0)
     assert got.tobytes() == want.tobytes(), (variant, size, _mismatch_report(got, want))
     assert np.array_equal(cnt, wcnt), (variant, size)
+
+
+WC_VARIANTS = [(0, 0, 0, 80), (0, 0, 0, 81), (0, 0, 0, 82), (0, 0, 0, 83)]
+
+
+@pytest.mark.parametrize("variant", R.compiled_variants(WC_VARIANTS))
+@pytest.mark.parametrize("wl", ["cfg3", "cfg4", "cfg2"])
+@pytest.mark.parametrize("n", [1, 3, 4097])
+def test_wave_contiguous_kernel(ctx, torch_dev, variant, wl, n):
+    """the WC kernel (RX_DIAG build, the cfg3 access-shape experiment): dense
+    1.5-KiB slots (its fast path), packed IMIX and 64-B slots (spans that fit
+    or not), ragged trips at the end of the burst, with counts, bit-exact
+    against the oracle"""
+    cfg = rxdist.gen_cfg(wl, **({"n_tcp": 300} if wl == "cfg3" else
+                                {"n_udp": 200, "n_tcp": 200} if wl == "cfg4" else {"n_udp": 64}))
+    udp, tcb = R.gen_flows(cfg)
+    pk, off, ln = R.gen_host(cfg, 0, n, 6)
+    ctx.flows_sync(udp, tcb)
+    want = O.Tables(udp, tcb).classify(pk, off, ln, 6)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 0, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, wl, _mismatch_report(got, want))
+    ok = want["rc"] == 0
+    fid = want["flow_id"].astype(np.int64) + np.where(want["cls"] == R.CLS_UDP, 0, len(udp))
+    assert np.array_equal(cnt, np.bincount(fid[ok], minlength=len(udp) + len(tcb)).astype(np.uint64))

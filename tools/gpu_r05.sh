@@ -71,6 +71,11 @@ if [ "${MEMBW3:-0}" = 1 ]; then  # cfg3 access-shape ceilings (tools/membw_cfg3.
   step membw_cfg3 150 ./tools/membw_cfg3 || exit $?
   cp $OUT/membw_cfg3.log $OUT/membw_cfg3_$TAG.txt
 fi
+if [ "${WC:-0}" = 1 ]; then  # the RX_DIAG build: WC kernel parity, then the interleaved cfg3 sweep
+  RXGPU_LIB=$PWD/dpdk-tcp-udp_protocol_stack_amd/librxgpu_diag.so step pytest_diag 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 170 --timeout-method thread -k "wave_contiguous or every_kernel_variant" || exit $?
+  RXGPU_LIB=$PWD/dpdk-tcp-udp_protocol_stack_amd/librxgpu_diag.so step sweep_wc 400 python bench.py --sweep cfg3 --steps 20 --warmup 3 --sweep-counts --sweep-variants "8,2,2,40;0,0,0,80;0,0,0,81;0,0,0,82;0,0,0,83;8,2,2,0" || exit $?
+  grep sweep $OUT/sweep_wc.log > $OUT/sweep_wc_$TAG.txt || true
+fi
 if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs two, alternating
   Q="--workload cfg4 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
   for k in 1 2; do
