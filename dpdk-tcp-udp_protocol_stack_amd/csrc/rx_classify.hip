@@ -2432,18 +2432,31 @@ __global__ __launch_bounds__(256) void rx_classify_wc_kernel(
 #pragma unroll
         for (int f = 0; f < F; ++f) ps[f] = 0;
         if (T.dense) {
+            // per chunk: one sum, F range tests; the head chunks (4 of every
+            // frame) go to LDS and the one partial last chunk of a frame is
+            // masked in a wave-uniform branch, so the common chunk costs
+            // about a dozen VALU (an earlier wave-owns-frames kernel masked
+            // every chunk and became issue-bound)
 #pragma unroll
             for (int j = 0; j < NL; ++j) {
                 const uint32_t k = 64u * j + lane;
+                const uint32_t cs = k < T.span ? chunk_sum(v[j]) : 0u;
+                bool part = false;
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
                     const uint32_t r = k - T.fo[f]; // chunk of frame f (wraps below it)
-                    const int32_t cpf = T.cp[f];
-                    if (k < T.span && r < ((uint32_t)cpf + 15u) >> 4) {
-                        if (r < 4u)
-                            s_hd[wv][f][r] = v[j];
-                        else
-                            ps[f] = lane_chunk_sum(ps[f], v[j], 16 * (int32_t)r, cpf);
+                    const uint32_t nfull = (uint32_t)T.cp[f] >> 4;
+                    ps[f] += (r - 4u < nfull - 4u && nfull > 4u) ? cs : 0u; // r in [4, nfull)
+                    if (r < 4u && r < (((uint32_t)T.cp[f] + 15u) >> 4)) s_hd[wv][f][r] = v[j];
+                    part = part || (r == nfull && r >= 4u && (T.cp[f] & 15));
+                }
+                if (__ballot(part) != 0ull) { // (wave-uniform) a frame's partial last chunk
+#pragma unroll
+                    for (int f = 0; f < F; ++f) {
+                        const uint32_t r = k - T.fo[f];
+                        const uint32_t nfull = (uint32_t)T.cp[f] >> 4;
+                        if (r == nfull && r >= 4u && (T.cp[f] & 15))
+                            ps[f] = lane_chunk_sum(ps[f], v[j], 16 * (int32_t)r, T.cp[f]);
                     }
                 }
             }
