@@ -455,6 +455,12 @@ static struct localhost *g_pstHost;
 static struct tcp_stream *g_tcb_set;
 static unsigned char g_ucFdTable[D_MAX_FD_COUNT / 8 + 1];
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* guards lists + snapshot */
+/* The id and descriptor maps (s_udp_cb / s_tcb_cb, g_fd_cb) are written only
+ * with g_lock held AND under g_tab, so an application call can look a block
+ * up and take its reference under g_tab alone — a lock held for a few stores
+ * — instead of waiting behind the protocol thread's whole delivery, which
+ * holds g_lock (lock order: g_lock, then g_tab). */
+static pthread_mutex_t g_tab = PTHREAD_MUTEX_INITIALIZER;
 static int g_dirty = 1;       /* the creation-order export (nstack_flows) is stale */
 static uint64_t g_snap_gen; /* bumped whenever a lookup result may change */
 static int g_burst_stale;   /* the burst's verdicts were made for an older snapshot */
@@ -484,9 +490,6 @@ static void proto_lock(void) {
     atomic_fetch_add_explicit(&g_proto_waiting, 1, memory_order_relaxed);
     pthread_mutex_lock(&g_lock);
     atomic_fetch_sub_explicit(&g_proto_waiting, 1, memory_order_relaxed);
-}
-static void app_yield(void) {
-    while (atomic_load_explicit(&g_proto_waiting, memory_order_relaxed)) sched_yield();
 }
 /* bursts of at least 2 * g_half_min frames run as two halves in flight
  * (nstack_set_halves; 0 = never) */
@@ -545,7 +548,9 @@ static void fd_refresh(int fd) {
         if (h->fd == fd) cb = h;
     for (struct tcp_stream *s = g_tcb_set; s && !cb; s = s->next)
         if (s->fd == fd) cb = s;
+    pthread_mutex_lock(&g_tab);
     g_fd_cb[fd] = cb;
+    pthread_mutex_unlock(&g_tab);
 }
 
 /* a block just took fd (nsocket, naccept): it is the newest of its list, so
@@ -557,8 +562,11 @@ static void fd_add(int fd, void *cb) {
     g_fd_nblk[fd]++;
     const void *cur = g_fd_cb[fd];
     if (!cur || ((const struct localhost *)cb)->protocol == IPPROTO_UDP ||
-        ((const struct localhost *)cur)->protocol != IPPROTO_UDP)
+        ((const struct localhost *)cur)->protocol != IPPROTO_UDP) {
+        pthread_mutex_lock(&g_tab);
         g_fd_cb[fd] = cb;
+        pthread_mutex_unlock(&g_tab);
+    }
 }
 /* block cb (already unlinked) carried fd and is freed: O(1) unless it was the
  * answer and another block still carries the fd (then the walk) */
@@ -566,10 +574,26 @@ static void fd_del(int fd, const void *cb) {
     if (fd < 0 || fd >= D_MAX_FD_COUNT) return;
     if (g_fd_nblk[fd]) g_fd_nblk[fd]--;
     if (g_fd_cb[fd] != cb) return;
-    if (!g_fd_nblk[fd])
+    if (!g_fd_nblk[fd]) {
+        pthread_mutex_lock(&g_tab);
         g_fd_cb[fd] = NULL;
-    else
+        pthread_mutex_unlock(&g_tab);
+    } else {
         fd_refresh(fd);
+    }
+}
+
+/* an application call's lookup: the block with this descriptor, referenced
+ * (cb_get), or NULL; under g_tab only (see g_tab) */
+static void *fd_get_ref(int fd) {
+    if (fd < 0 || fd >= D_MAX_FD_COUNT) return NULL;
+    pthread_mutex_lock(&g_tab);
+    void *cb = g_fd_cb[fd];
+    if (cb)
+        cb_get(((struct localhost *)cb)->protocol == IPPROTO_UDP ? &((struct localhost *)cb)->ref
+                                                                  : &((struct tcp_stream *)cb)->ref);
+    pthread_mutex_unlock(&g_tab);
+    return cb;
 }
 
 static void *get_hostinfo_fromfd(int fd) {
@@ -652,10 +676,15 @@ static int reg_udp(struct localhost *h) { /* LL_ADD (common.c:302) */
     uint32_t id;
     int rc = rxg_flows_add(g_ctx, &u, 1, NULL, 0, &id, NULL);
     if (rc < 0) return rc;
+    pthread_mutex_lock(&g_tab);
     uint32_t cap = s_udp_cap;
-    if (grow((void **)&s_udp_cb, &s_udp_cap, id + 1, sizeof(void *))) return RXG_ENOMEM;
+    if (grow((void **)&s_udp_cb, &s_udp_cap, id + 1, sizeof(void *))) {
+        pthread_mutex_unlock(&g_tab);
+        return RXG_ENOMEM;
+    }
     if (s_udp_cap > cap) memset(s_udp_cb + cap, 0, (s_udp_cap - cap) * sizeof(void *));
     s_udp_cb[id] = h;
+    pthread_mutex_unlock(&g_tab);
     h->flow_id = id;
     g_snap_gen++;
     g_dirty = 1;
@@ -666,10 +695,15 @@ static int reg_tcb(struct tcp_stream *s) { /* LL_ADD (tcp.c:52, common.c:336) */
     uint32_t id;
     int rc = rxg_flows_add(g_ctx, NULL, 0, &t, 1, NULL, &id);
     if (rc < 0) return rc;
+    pthread_mutex_lock(&g_tab);
     uint32_t cap = s_tcb_cap;
-    if (grow((void **)&s_tcb_cb, &s_tcb_cap, id + 1, sizeof(void *))) return RXG_ENOMEM;
+    if (grow((void **)&s_tcb_cb, &s_tcb_cap, id + 1, sizeof(void *))) {
+        pthread_mutex_unlock(&g_tab);
+        return RXG_ENOMEM;
+    }
     if (s_tcb_cap > cap) memset(s_tcb_cb + cap, 0, (s_tcb_cap - cap) * sizeof(void *));
     s_tcb_cb[id] = s;
+    pthread_mutex_unlock(&g_tab);
     s->flow_id = id;
     g_snap_gen++;
     g_dirty = 1;
@@ -677,13 +711,17 @@ static int reg_tcb(struct tcp_stream *s) { /* LL_ADD (tcp.c:52, common.c:336) */
 }
 static void unreg_udp(struct localhost *h) { /* LL_REMOVE (common.c:620) */
     (void)rxg_flows_remove(g_ctx, &h->flow_id, 1, NULL, 0);
+    pthread_mutex_lock(&g_tab);
     if (h->flow_id < s_udp_cap) s_udp_cb[h->flow_id] = NULL;
+    pthread_mutex_unlock(&g_tab);
     g_snap_gen++;
     g_dirty = 1;
 }
 static void unreg_tcb(struct tcp_stream *s) { /* LL_REMOVE (tcp.c:321, common.c:660) */
     (void)rxg_flows_remove(g_ctx, NULL, 0, &s->flow_id, 1);
+    pthread_mutex_lock(&g_tab);
     if (s->flow_id < s_tcb_cap) s_tcb_cb[s->flow_id] = NULL;
+    pthread_mutex_unlock(&g_tab);
     g_snap_gen++;
     g_dirty = 1;
 }
@@ -732,12 +770,15 @@ void nstack_fini(void) {
         tcb_kill(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
+    pthread_mutex_lock(&g_tab);
     memset(g_fd_cb, 0, sizeof(g_fd_cb));
+    free(s_udp_cb), free(s_tcb_cb);
+    s_udp_cb = NULL, s_tcb_cb = NULL;
+    s_udp_cap = s_tcb_cap = 0;
+    pthread_mutex_unlock(&g_tab);
     memset(g_fd_nblk, 0, sizeof(g_fd_nblk));
-    free(s_udp), free(s_udp_cb), free(s_tcb), free(s_tcb_cb), free(s_v), free(s_udp_id),
-        free(s_tcb_id), free(s_handled);
-    s_udp = NULL, s_udp_cb = NULL, s_tcb = NULL, s_tcb_cb = NULL, s_v = NULL, s_udp_id = NULL,
-    s_tcb_id = NULL, s_handled = NULL;
+    free(s_udp), free(s_tcb), free(s_v), free(s_udp_id), free(s_tcb_id), free(s_handled);
+    s_udp = NULL, s_tcb = NULL, s_v = NULL, s_udp_id = NULL, s_tcb_id = NULL, s_handled = NULL;
     s_udp_cap = s_tcb_cap = s_v_cap = s_nu = s_nt = s_udp_xcap = s_tcb_xcap = s_handled_cap = 0;
     memset(g_stat, 0, sizeof(g_stat));
     /* every counter nstack_stat reports describes the current stack */
@@ -954,10 +995,7 @@ ssize_t nsend(int sockfd, const void *buf, size_t len, int flags) { /* :418-460 
 static ssize_t nrecv_tcb(struct tcp_stream *s, void *buf, size_t len, int flags);
 
 ssize_t nrecv(int sockfd, void *buf, size_t len, int flags) { /* :462-515 */
-    pthread_mutex_lock(&g_lock);
-    struct tcp_stream *s = get_hostinfo_fromfd(sockfd);
-    if (s) cb_get(&s->ref); /* (linked: the block lives until our put) */
-    pthread_mutex_unlock(&g_lock);
+    struct tcp_stream *s = fd_get_ref(sockfd); /* (linked: the block lives until our put) */
     if (!s) return -1;
     ssize_t r = 0;
     if (s->protocol == IPPROTO_TCP) r = nrecv_tcb(s, buf, len, flags);
@@ -1008,10 +1046,7 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
 ssize_t nrecvfrom(int sockfd, void *buf, size_t len, int flags, struct sockaddr *src_addr,
                   socklen_t *addrlen) { /* :517-565 */
     (void)addrlen;
-    pthread_mutex_lock(&g_lock);
-    struct localhost *h = get_hostinfo_fromfd(sockfd);
-    if (h) cb_get(&h->ref);
-    pthread_mutex_unlock(&g_lock);
+    struct localhost *h = fd_get_ref(sockfd);
     if (!h) return -1;
     const ssize_t r = udp_recv(h, buf, len, flags, src_addr);
     cb_put(h);
@@ -1107,10 +1142,7 @@ ssize_t nsendto(int sockfd, const void *buf, size_t len, int flags,
     (void)flags, (void)addrlen;
     const struct sockaddr_in *a = (const struct sockaddr_in *)dest_addr;
     if (!a) return -1;
-    pthread_mutex_lock(&g_lock);
-    struct localhost *h = get_hostinfo_fromfd(sockfd);
-    if (h) cb_get(&h->ref);
-    pthread_mutex_unlock(&g_lock);
+    struct localhost *h = fd_get_ref(sockfd);
     if (!h) return -1;
     const ssize_t r = udp_send(h, buf, len, a);
     cb_put(h);
@@ -2210,9 +2242,9 @@ static void drain_tcb(struct tcp_stream *s, void *buf, size_t cap, uint64_t *got
 static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum) {
     /* The application side of the benchmark: every socket read until empty,
      * EOF fragments read and not counted (as oracle_drain_all).  Blocks are
-     * visited by stable id.  The stack's lock is held only to take a
-     * reference on the next DRAIN_CHUNK live blocks (one hold for up to 8192
-     * blocks) (a block stays valid
+     * visited by stable id.  Only the id maps' lock (g_tab, never the
+     * stack's lock) is held, to take a reference on the next DRAIN_CHUNK
+     * live blocks (one hold for up to 8192 blocks) (a block stays valid
      * while referenced, even if the protocol thread frees it meanwhile: its
      * memory goes with the last reference); everything else — the rings, the
      * copies — runs under each block's own mutex, beside the protocol
@@ -2231,9 +2263,8 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
         uint32_t id = 0;
         for (int more = 1; more;) {
             const double w0 = mono_ms();
-            app_yield();
-            const double w1 = mono_ms();
-            pthread_mutex_lock(&g_lock);
+            const double w1 = w0;
+            pthread_mutex_lock(&g_tab); /* (not g_lock: see g_tab) */
             const double w2 = mono_ms();
             atomic_fetch_add_explicit(&g_drain_ns[1], (long long)((w1 - w0) * 1e6), memory_order_relaxed);
             atomic_fetch_add_explicit(&g_drain_ns[0], (long long)((w2 - w1) * 1e6), memory_order_relaxed);
@@ -2253,7 +2284,7 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
                 }
             }
             more = id < ncap;
-            pthread_mutex_unlock(&g_lock);
+            pthread_mutex_unlock(&g_tab);
             const double c0 = mono_ms();
             for (uint32_t i = 0; i < k; i++) {
                 /* look-ahead (every address formed from memory this call keeps

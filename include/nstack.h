@@ -167,11 +167,11 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
  * the receive buffer each call uses.  Returns the datagrams + fragments
  * received (EOF fragments are read and not counted, as oracle_drain_all does;
  * a negative RXG_E* code on error); *bytes = the bytes the calls returned.
- * Takes the stack's lock only to take a reference on the next 8192 blocks
- * (stepping aside while the protocol thread waits for it); the reads run
- * under each block's own mutex, so a concurrent nstack_rx_burst delivers
- * beside them, and a block freed meanwhile (last ACK) stays valid until the
- * call lets go of it. */
+ * Never takes the stack's lock: a short lock of the id maps is held to take
+ * a reference on the next 8192 blocks; the reads run under each block's own
+ * mutex, so a concurrent nstack_rx_burst delivers beside them, and a block
+ * freed meanwhile (last ACK) stays valid until the call lets go of it.
+ * nrecv / nrecvfrom / nsendto look their descriptor up the same way. */
 int64_t nstack_drain_all(void *buf, size_t cap, uint64_t *bytes);
 /* nstack_drain_all, and *sum = the sum (mod 2^64) over every datagram and
  * fragment read of the FNV-1a 64 hash of the bytes the read returned: an
