@@ -15,6 +15,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <stdatomic.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -49,20 +50,20 @@ struct nring {
     uint32_t cap, head, count;
 };
 
-static struct nring *ring_create(uint32_t cap) {
-    struct nring *r = calloc(1, sizeof(*r));
-    if (!r) return NULL;
+/* rings live inside their control block (one line fewer for a reader to
+ * fetch); only the slot array is allocated */
+static struct nring *ring_init(struct nring *r, uint32_t cap) {
     r->slot = calloc(cap, sizeof(void *));
-    if (!r->slot) {
-        free(r);
-        return NULL;
-    }
+    if (!r->slot) return NULL;
     r->cap = cap;
+    r->head = r->count = 0;
     return r;
 }
 static void ring_free(struct nring *r) {
-    if (r) free(r->slot);
-    free(r);
+    if (r) {
+        free(r->slot);
+        r->slot = NULL;
+    }
 }
 static int ring_enqueue(struct nring *r, void *p) {
     if (r->count == r->cap) return -ENOBUFS;
@@ -94,15 +95,18 @@ struct localhost {
     uint32_t localip;
     unsigned char localmac[6];
     uint16_t localport;
-    unsigned char protocol;
+    unsigned char protocol; /* (@16 in both block kinds: get_hostinfo_fromfd's cast) */
     struct nring *sndbuf, *rcvbuf;
-    struct localhost *prev, *next;
-    pthread_cond_t cond;
-    pthread_mutex_t mutex;
     uint32_t flow_id; /* stable id in the GPU flow tables (verdict flow_id) */
     uint32_t queued;  /* datagrams in rcvbuf (a batch item holds several) */
+    /* what a reader touches, together: the lock, the receive ring, the state */
+    pthread_mutex_t mutex;
+    struct nring rcv_r;
     atomic_int ref;   /* the lists' reference + one per reader (cb_get / udp_put) */
     int dead;         /* unlinked (nclose): readers return, the last put frees */
+    struct nring snd_r;
+    struct localhost *prev, *next;
+    pthread_cond_t cond;
 };
 
 struct dgram_batch;
@@ -174,15 +178,18 @@ struct tcp_stream {
     uint32_t snd_nxt, rcv_nxt;
     int status;
     struct nring *sndbuf, *rcvbuf;
-    struct tcp_stream *prev, *next;
-    pthread_cond_t cond;
-    pthread_mutex_t mutex;
-    pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
-    uint32_t flow_id;           /* stable id in the GPU flow tables (verdict flow_id) */
     uint32_t rq, sq;            /* fragments in rcvbuf / sndbuf (a batch item holds several) */
+    /* what a reader touches, together: the lock, the receive ring, the state */
+    pthread_mutex_t mutex;
+    struct nring rcv_r;
     atomic_int ref;             /* the lists' reference + one per reader (cb_get / tcb_put) */
     int dead;                   /* unlinked (last ACK, nclose): readers return, the last
                                    put frees */
+    uint32_t flow_id;           /* stable id in the GPU flow tables (verdict flow_id) */
+    struct nring snd_r;
+    struct tcp_stream *prev, *next;
+    pthread_cond_t cond;
+    pthread_cond_t accept_cond; /* naccept waits here, paired with g_lock */
 };
 
 struct frag_batch;
@@ -381,6 +388,9 @@ static void tq_clear(struct nring *r, uint32_t *cnt) {
         if ((list) == (item)) (list) = (item)->next;                                               \
         (item)->prev = (item)->next = NULL;                                                        \
     } while (0)
+
+_Static_assert(offsetof(struct localhost, protocol) == offsetof(struct tcp_stream, protocol),
+               "get_hostinfo_fromfd reads either block's protocol byte at one offset");
 
 /* ---- control-block lifetime ----------------------------------------------
  * A block carries a reference count: one for being linked (lists, id and fd
@@ -820,8 +830,8 @@ int nsocket(int domain, int type, int protocol) {
         if (!h) goto fail;
         h->fd = fd;
         h->protocol = IPPROTO_UDP;
-        h->rcvbuf = ring_create(D_RING_SIZE);
-        h->sndbuf = ring_create(D_RING_SIZE);
+        h->rcvbuf = ring_init(&h->rcv_r, D_RING_SIZE);
+        h->sndbuf = ring_init(&h->snd_r, D_RING_SIZE);
         if (!h->rcvbuf || !h->sndbuf) {
             ring_free(h->rcvbuf);
             ring_free(h->sndbuf);
@@ -844,8 +854,8 @@ int nsocket(int domain, int type, int protocol) {
         if (!s) goto fail;
         s->fd = fd;
         s->protocol = IPPROTO_TCP;
-        s->rcvbuf = ring_create(D_RING_SIZE);
-        s->sndbuf = ring_create(D_RING_SIZE);
+        s->rcvbuf = ring_init(&s->rcv_r, D_RING_SIZE);
+        s->sndbuf = ring_init(&s->snd_r, D_RING_SIZE);
         if (!s->rcvbuf || !s->sndbuf) {
             ring_free(s->rcvbuf);
             ring_free(s->sndbuf);
@@ -1261,8 +1271,8 @@ static struct tcp_stream *tcb_new(uint32_t sip, uint32_t dip, uint16_t sport, ui
     s->protocol = IPPROTO_TCP;
     s->fd = -1;
     s->status = status;
-    s->rcvbuf = ring_create(D_RING_SIZE);
-    s->sndbuf = ring_create(D_RING_SIZE);
+    s->rcvbuf = ring_init(&s->rcv_r, D_RING_SIZE);
+    s->sndbuf = ring_init(&s->snd_r, D_RING_SIZE);
     if (!s->rcvbuf || !s->sndbuf) {
         ring_free(s->rcvbuf);
         ring_free(s->sndbuf);
@@ -2295,7 +2305,8 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
                  * a fragment batch's header and first fragments (frag_batch:
                  * the item, then its fragments), whatever the head slot holds
                  * by the time it is read */
-                if (i + 4 < k) __builtin_prefetch(blk[i + 4], 0, 0);
+                if (i + 4 < k)
+                    for (int q = 0; q < 3; q++) __builtin_prefetch((const char *)blk[i + 4] + 64 * q, 0, 0);
                 if (i + 2 < k)
                     __builtin_prefetch(kind ? (void *)((struct tcp_stream *)blk[i + 2])->rcvbuf
                                             : (void *)((struct localhost *)blk[i + 2])->rcvbuf,
