@@ -24,6 +24,7 @@ against the oracle (the exit code is 3 if any differs).
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import glob
 import json
 import os
@@ -391,6 +392,13 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
                            unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                            traffic=pmc_traffic(name) if world == 1 else None,
                            kernel=kdisp)
+    g = w["gen"]
+    if world == 1 and g.get("frame_len") and not g.get("packed") and not g.get("size_mode") \
+            and g["slot_bytes"] <= 1536:
+        # the same burst read in the classify kernel's slot shape, and plainly,
+        # in this process (a same-process access-shape table)
+        res["slot_shape_ceiling"] = slot_ceiling(dev.index or 0, pk, n, g["slot_bytes"],
+                                                 g["frame_len"], kdisp.get("median_ms"))
     # parity of this run: a seeded sample of the verdicts regenerated on the CPU
     stage(rank, f"{name}: parity")
     t_par = time.perf_counter()
@@ -906,7 +914,6 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
     application reading every socket (nrecvfrom / nrecv, common.c:462-565).
     CPU baseline: oracle/ref_stack.c, the reference's per-frame
     udp_process / tcp_process and socket calls, over the same frames."""
-    import ctypes as C
     w = rxdist.WORKLOADS[name]
     cfg = rxdist.gen_cfg(name)
     ul = w["unit_log2"]
@@ -1057,27 +1064,12 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # lock while a burst is on the GPU)
         import threading
 
-        def overlapped(cpus=None, unpin=False):
-            stop = threading.Event()
-            ov = [0, 0]
-            app_t = [0.0, 0]  # time inside drain_all, passes
+        # the application lcore in C (tools/libappthread.so: nstack_drain_all
+        # in a loop, 20-us pause when a pass finds nothing); a Python thread
+        # in that role measured the interpreter's lock hand-offs, not the stack
+        applib = _appthread_lib()
 
-            def app_thread():
-                if cpus:
-                    os.sched_setaffinity(0, {cpus[1]})
-                b2 = np.zeros(65536, np.uint8)
-                while not stop.is_set():
-                    a0 = time.perf_counter()
-                    g2, n2 = ns.drain_all(b2)
-                    app_t[0] += time.perf_counter() - a0
-                    app_t[1] += 1
-                    ov[0] += g2
-                    ov[1] += n2
-                    if g2 == 0:  # nothing queued: let the protocol thread take the lock
-                        time.sleep(0.0001)
-                g2, n2 = ns.drain_all(b2)
-                ov[0] += g2
-                ov[1] += n2
+        def overlapped(cpus=None, unpin=False):
             main_aff = os.sched_getaffinity(0)
             if cpus:
                 os.sched_setaffinity(0, {cpus[0]})
@@ -1086,11 +1078,12 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             d0, s0, c0 = int(ns.stat(1)), int(ns.stat(5)), int(ns.stat(6))
             w0 = [int(ns.stat(8 + j)) for j in range(3)]
             pw0 = int(ns.stat(11))
-            th = threading.Thread(target=app_thread)
-            t0 = time.perf_counter()
-            th.start()
             ov_rx, ov_ph, ov_cp, ov_tr = [], [], [], []
             w_pool0 = pool_waits[0]
+            r = AppResult()
+            t0 = time.perf_counter()
+            if applib.app_start(cpus[1] if cpus else -1, 0) != 0:
+                raise RuntimeError("app_start failed")
             try:
                 for _ in range(K):
                     arr = next_set()
@@ -1099,27 +1092,30 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                     ov_rx.append(time.perf_counter() - a0)
                     ov_ph.append(ns.last_burst_phases())
                     ov_cp.append(int(ns.stat(6)))
-                    ov_tr.append((ov[0], int(ns.stat(7))))
+                    ov_tr.append(int(ns.stat(7)))
             finally:
-                stop.set()
-                th.join()
+                applib.app_stop(C.byref(r))
                 os.sched_setaffinity(0, main_aff)
             t_ov = time.perf_counter() - t0
+            if r.err:
+                raise R.RxgError(int(r.err), "nstack_drain_all (application thread)")
             return dict(mpps=round(B * K / t_ov / 1e6, 3), ms_per_burst=round(t_ov / K * 1e3, 3),
-                        received=ov[0], payload_bytes=ov[1],
-                        received_equal=ov[0] == items, dropped=int(ns.stat(1)) - d0,
+                        received=int(r.items), payload_bytes=int(r.bytes),
+                        received_equal=int(r.items) == items, dropped=int(ns.stat(1)) - d0,
                         stale_bursts=int(ns.stat(5)) - s0,
                         copied_payload_bytes=int(ns.stat(6)) - c0,
                         bursts_waited_for_buffer=int(ns.stat(11)) - pw0,
                         bursts_waited_for_mbufs=pool_waits[0] - w_pool0,
                         copied_mb_by_burst=[round((b - a) / 1e6, 1) for a, b in zip([c0] + ov_cp, ov_cp)],
-                        drained_and_held_by_burst=ov_tr,
+                        held_batches_by_burst=ov_tr,
                         app_ms_per_burst={k: round((int(ns.stat(8 + j)) - w0[j]) / 1e6 / K, 3) for j, k in
                                           enumerate(("lock_wait", "yield", "read_out"))},
                         rx_burst_ms=round(float(np.median(ov_rx)) * 1e3, 3),
+                        rx_burst_mean_ms=round(float(np.mean(ov_rx)) * 1e3, 3),
                         rx_burst_phases_ms={k: round(float(np.median([p[k] for p in ov_ph])), 4)
                                             for k in ov_ph[0]},
-                        app_drain_ms=round(app_t[0] * 1e3 / K, 3), app_passes=app_t[1],
+                        app_drain_ms=round(r.drain_ms / K, 3), app_passes=int(r.passes),
+                        app_empty_passes=int(r.empty), app_thread="C (tools/libappthread.so)",
                         cpus=list(cpus) if cpus else None,
                         note="application thread draining while the protocol thread runs "
                              "the bursts" + ("; the two threads on the lcores above" if cpus else
@@ -1169,11 +1165,53 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
     return res
 
 
+class AppResult(C.Structure):
+    """tools/appthread.c app_result"""
+    _fields_ = [("items", C.c_int64), ("bytes", C.c_uint64), ("sum", C.c_uint64),
+                ("passes", C.c_uint64), ("empty", C.c_uint64), ("drain_ms", C.c_double),
+                ("err", C.c_int64)]
+
+
+def _appthread_lib():
+    """tools/libappthread.so (built by __graft_entry__.build / make -C tools),
+    loaded after libnstack.so so that it binds the same stack"""
+    p = os.path.join(ROOT, "tools", "libappthread.so")
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} missing: run make -C tools")
+    lib = C.CDLL(p)
+    lib.app_start.argtypes = [C.c_int, C.c_int]
+    lib.app_stop.argtypes = [C.POINTER(AppResult)]
+    return lib
+
+
+def slot_ceiling(local, pk, n, slot_bytes, read_bytes, kernel_ms=None, reps=9):
+    """tools/libceiling.so ceiling_slot_ms over the workload's own burst: the
+    classify kernel's slot shape (8 lanes per slot, the frame's 16-B chunks,
+    16 B stored per slot) with no parsing, and a plain read of the same
+    n * slot_bytes; the dominant kernel's median dispatch beside them"""
+    p = os.path.join(ROOT, "tools", "libceiling.so")
+    if not os.path.exists(p):
+        return None
+    torch.cuda.synchronize()
+    a, b = C.c_double(0.0), C.c_double(0.0)
+    rc = C.CDLL(p).ceiling_slot_ms(C.c_int(local), C.c_void_p(pk.data_ptr()), C.c_ulonglong(n),
+                                   C.c_uint(slot_bytes), C.c_uint(read_bytes), C.c_int(reps),
+                                   C.byref(a), C.byref(b))
+    if rc != 0:
+        log(f"bench: ceiling_slot_ms failed (HIP error {rc})")
+        return None
+    out = dict(slot_ms=round(a.value, 4), stream_ms=round(b.value, 4),
+               stream_gbs=round(n * slot_bytes / (b.value * 1e-3) / 1e9, 1))
+    if kernel_ms:
+        out.update(kernel_median_ms=kernel_ms, kernel_over_slot=round(kernel_ms / a.value, 3),
+                   kernel_over_stream=round(kernel_ms / b.value, 3))
+    return out
+
+
 def hbm_read_ceiling(local, nbytes=4 << 30, reps=9):
     """this box's measured HBM read ceiling (GB/s) beside the 8 TB/s spec:
     tools/libceiling.so's plain coalesced read (tools/ceiling.hip), the
     fastest shape of tools/membw_large.hip; None if the tool is not built"""
-    import ctypes as C
     p = os.path.join(ROOT, "tools", "libceiling.so")
     if not os.path.exists(p):
         log("bench: tools/libceiling.so not built; hbm_read_ceiling_gbs = null")
@@ -1388,7 +1426,9 @@ def _wl_summary(r, peak=HBM_PEAK_GBS):
              parity_ok=(_g(r, "parity", "mismatches") == 0) if _g(r, "parity") else None,
              digest_ok=_g(r, "digest", "digest_ok"), counts_match=_g(r, "counts_match"),
              cpu_mpps=_g(r, "cpu_baseline", "value"),
-             v8_frac=_g(r, "verdict8", "frac"), tx_frac=_g(r, "tx_cksum", "frac"))
+             v8_frac=_g(r, "verdict8", "frac"), tx_frac=_g(r, "tx_cksum", "frac"),
+             kernel_over_slot_shape=_g(r, "slot_shape_ceiling", "kernel_over_slot"),
+             kernel_over_stream=_g(r, "slot_shape_ceiling", "kernel_over_stream"))
     return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.items()
             if v is not None}
 

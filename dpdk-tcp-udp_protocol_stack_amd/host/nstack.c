@@ -2155,9 +2155,15 @@ struct drain_scratch {
  * (a batch's hold on a payload buffer or on its frames' mbufs ends there).
  * The fragments lie scattered (in place: in their frames), so the copy loop
  * prefetches the lines of the fragment DRAIN_AHEAD places ahead. */
+#ifndef NSTACK_DRAIN_AHEAD /* (tools/Makefile builds variants for tools/sock_host_bench) */
+#define NSTACK_DRAIN_AHEAD 4
+#endif
+#ifndef NSTACK_DRAIN_LOC
+#define NSTACK_DRAIN_LOC 0
+#endif
 static void drain_detached(struct drain_scratch *sc, void *buf, uint64_t *got, uint64_t *nb,
                            uint64_t *hs) {
-    enum { DRAIN_AHEAD = 4 };
+    enum { DRAIN_AHEAD = NSTACK_DRAIN_AHEAD };
     uint32_t m = 0;
     for (uint32_t i = 0; i < sc->nd; i++) {
         const struct tcp_fragment *f = sc->det[i];
@@ -2181,7 +2187,7 @@ static void drain_detached(struct drain_scratch *sc, void *buf, uint64_t *got, u
         if (i + DRAIN_AHEAD < m && sc->fl[i + DRAIN_AHEAD]) {
             const uintptr_t p0 = (uintptr_t)sc->fp[i + DRAIN_AHEAD] & ~(uintptr_t)63;
             const uintptr_t p1 = (uintptr_t)sc->fp[i + DRAIN_AHEAD] + sc->fl[i + DRAIN_AHEAD];
-            for (uintptr_t q = p0; q < p1; q += 64) __builtin_prefetch((const void *)q, 0, 0);
+            for (uintptr_t q = p0; q < p1; q += 64) __builtin_prefetch((const void *)q, 0, NSTACK_DRAIN_LOC);
         }
         if (sc->fl[i]) {
             memcpy(buf, sc->fp[i], sc->fl[i]);

@@ -1,0 +1,60 @@
+"""bench.py's application lcore in C (tools/libappthread.so): it binds the
+stack bench.py loaded (the same libnstack.so instance) and reads every
+datagram the protocol thread delivers while it runs — what the two-thread
+socket rows of the bench line count.  Host-only stack, oracle verdicts."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import frames as F
+import oracle_bind as O
+import rxgpu as R
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+L = "192.168.100.77"
+
+
+def test_c_application_thread_reads_everything():
+    sys.path.insert(0, ROOT)
+    import bench  # noqa: E402  (the loader and the result layout bench.py uses)
+    ns = R.NStack(R.HOST_ONLY)
+    try:
+        lib = bench._appthread_lib()
+        ports = list(range(20000, 20064))
+        for p in ports:
+            assert ns.bind(ns.socket(R.SOCK_DGRAM), L, p) == 0
+        rng = np.random.default_rng(5)
+        want_items = want_bytes = 0
+        r = bench.AppResult()
+        assert lib.app_start(-1, 0) == 0
+        try:
+            for _ in range(20):
+                frames = []
+                for k in range(256):
+                    n = int(rng.integers(1, 600))
+                    frames.append(F.udp_frame("10.0.0.%d" % (k % 200 + 1), 5555, L,
+                                              ports[int(rng.integers(0, len(ports)))],
+                                              bytes(rng.integers(0, 256, n, dtype=np.uint8))))
+                    want_items += 1
+                    want_bytes += n + 8  # nrecvfrom's length is the UDP length (udp.c:31-46)
+                u, t, gen = ns.flows(with_gen=True)
+                buf, off, lens = F.pack_frames(frames)
+                v = ns.to_ids(O.Tables(u, t).classify(buf, off, lens, 6))
+                rcs = np.zeros(len(frames), np.int32)
+                ns.deliver(frames, v, rcs, gen)
+                assert (rcs == 0).all()
+        finally:
+            assert lib.app_stop(C.byref(r)) == 0
+        assert r.err == 0
+        assert (r.items, r.bytes) == (want_items, want_bytes)
+        assert r.passes >= 1
+        assert lib.app_stop(C.byref(r)) == -1  # not running
+    finally:
+        ns.fini()
+
+
+if __name__ == "__main__":
+    pytest.main([__file__, "-q"])

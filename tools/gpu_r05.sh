@@ -22,6 +22,30 @@ if [ "${SWING:-0}" = 1 ]; then
   grep '^{' $OUT/swing_first.log > $OUT/swing_first_$TAG.json || true
   bench bench_cfg2_first 240 --workload cfg2 --no-cfg1 --no-sockrate --no-tx --no-v8 || exit $?
 fi
+if [ "${PROC:-0}" = 1 ]; then
+  # cfg2 per process: default / second / high-priority stream, a second
+  # context, a burst behind a spacer (tools/cfg2_proc.py), in 5 processes
+  for k in 1 2 3 4 5; do
+    NCTX=6 step proc$k 120 python tools/cfg2_proc.py || exit $?
+    grep '^{' $OUT/proc$k.log >> $OUT/proc_$TAG.jsonl || true
+  done
+  # 6 contexts in one process under the kernel trace: kernel durations vs gaps per case
+  NCTX=6 step proctrace 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_proc_$TAG -o run \
+      -- python3 tools/cfg2_proc.py || exit $?
+  f=$(find $OUT/prof_proc_$TAG -name '*kernel_trace.csv' | head -1)
+  [ -n "$f" ] && python tools/proc_trace.py $OUT/proctrace.log "$f" > $OUT/proc_trace_$TAG.txt 2>&1
+  cat $OUT/proc_trace_$TAG.txt
+fi
+if [ "${SOCKHOST:-0}" = 1 ]; then
+  # the host socket path alone (no GPU): drain_all's prefetch variants,
+  # interleaved, in place and copy (tools/sock_host_bench.c, tools/Makefile nsv)
+  C0=$(python3 -c 'import os; print(sorted(os.sched_getaffinity(0))[0])')
+  for r in 1 2; do for v in a4l0 a8l0 a16l0 a4l3 a8l3 a8l1 a2l0 a0l0; do
+    echo "== $v round $r" >> $OUT/sockhost_$TAG.txt
+    LD_LIBRARY_PATH=tools/nsv/$v:dpdk-tcp-udp_protocol_stack_amd:oracle timeout -k 5 60 ./tools/sock_host_bench 1 $C0 >> $OUT/sockhost_$TAG.txt 2>&1 || exit $?
+  done; done
+  LD_LIBRARY_PATH=tools/nsv/a4l0:dpdk-tcp-udp_protocol_stack_amd:oracle timeout -k 5 60 ./tools/sock_host_bench 0 $C0 >> $OUT/sockhost_$TAG.txt 2>&1 || exit $?
+fi
 if [ "${TESTS:-1}" = 1 ]; then
   # plain test failures (rc 1) still let the bench run; anything else (a
   # timeout, an abort, a fault) ends the session

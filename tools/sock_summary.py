@@ -25,5 +25,5 @@ for line in open(sys.argv[1]):
                   f"waited {x.get('bursts_waited_for_buffer')}")
             if x.get("copied_mb_by_burst"):
                 print("    copied MB by burst", x["copied_mb_by_burst"])
-                print("    (items drained, batches holding a buffer) by burst", x.get("drained_and_held_by_burst"))
+                print("    batches holding a buffer, by burst", x.get("held_batches_by_burst"))
                 print("    app ms per burst", x.get("app_ms_per_burst"))
