@@ -430,6 +430,7 @@ static void ft_fill(rxg_ctx *c) {
     c->ft.udpc = fs.udpc.empty() ? nullptr : c->d_udpc;
     c->ft.udpc_mask = fs.udpc.empty() ? 0 : (uint32_t)fs.udpc.size() - 1;
     c->ft.udpc_probe = fs.udpc_probe;
+    c->ft.udpc_other = fs.udpc_other;
     c->ft.udp_port = fs.port.empty() ? nullptr : c->d_udp_port;
     c->ft.udp_dip = fs.udp_dip;
     c->ft.udpw = fs.udpw.empty() ? nullptr : c->d_udpw;

@@ -720,9 +720,14 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
         flow = probe ? (dport & 0x3FFu) : RXG_FLOW_NONE;
     } else if (LDT && probe && is_udp) { // compact UDP table in LDS
         const uint32_t k = rx_bswap16(dport) - ft.udpw_lo;
-        if (dip == ft.udp_dip && k < ft.udpw_n) { // the port window decides (one LDS read)
-            const uint32_t e = lw[k];
+        // with a port window: on udp_dip the window holds every bound port
+        // (outside it, no socket), elsewhere only the udpc_other keys can match
+        const bool win = ft.udpw_n != 0u;
+        if (win && dip == ft.udp_dip) { // the port window decides (one LDS read)
+            const uint32_t e = k < ft.udpw_n ? lw[k] : 0xFFFFu;
             flow = e == 0xFFFFu ? RXG_FLOW_NONE : e;
+        } else if (win && ft.udpc_other == 0u) {
+            flow = RXG_FLOW_NONE;
         } else {
             uint32_t i = rx_hash3s(ft.hseed, dip, dport, 17u) & ft.udpc_mask;
             for (uint32_t pr = 0; pr < ft.udpc_probe; ++pr, i = (i + 1) & ft.udpc_mask) {

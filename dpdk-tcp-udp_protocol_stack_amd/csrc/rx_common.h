@@ -37,6 +37,11 @@ struct rx_ft_dev {
     // by the lane kernel: slot = {dip, dport | flow << 16}, empty = y ~0u
     const uint2 *udpc;
     uint32_t udpc_mask, udpc_probe;
+    // compact keys not bound to udp_dip: with a port window and none of them,
+    // every UDP frame is decided without a probe (a miss outside the window is
+    // a miss), so the probe-sequence length the per-context hash seed gives
+    // the generator's unknown-flow key (:7) never enters the kernel's time
+    uint32_t udpc_other;
     // UDP direct port table (null: not built): u32[65536] indexed by the raw
     // dst port, for sockets bound to udp_dip (the address most sockets share:
     // the host's own); see rx_udp_port_decide

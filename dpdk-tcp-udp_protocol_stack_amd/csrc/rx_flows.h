@@ -216,6 +216,7 @@ struct rx_flowset {
     // compact UDP table + port window (rx_common.h), derived
     std::vector<uint2> udpc;
     uint32_t udpc_probe = 0;
+    uint32_t udpc_other = 0; // compact keys whose address is not udp_dip
     std::vector<uint16_t> udpw;
     uint32_t udpw_lo = 0;
     bool small_dirty = true;
@@ -304,6 +305,7 @@ struct rx_flowset {
         small_dirty = true;
         udpc.clear();
         udpc_probe = 0;
+        udpc_other = 0;
         udpw.clear();
         udpw_lo = 0;
         // flow ids are stored in 16 bits (compact slot) and as u16 != 0xFFFF (window)
@@ -319,6 +321,7 @@ struct rx_flowset {
             while (udpc[i].y != 0xFFFFFFFFu) i = (i + 1) & mask, ++d;
             udpc[i] = make_uint2(sl.x, (sl.y & 0xFFFFu) | (sl.w << 16));
             udpc_probe = std::max(udpc_probe, d + 1);
+            if (sl.x != udp_dip) ++udpc_other;
         }
         if (port.empty()) return;
         uint32_t mn = 65536, mx = 0;

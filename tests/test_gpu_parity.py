@@ -238,7 +238,8 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
                                      (0, 0, 0, 20)]))
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("far", [False, True])
-def test_udp_port_window(ctx, torch_dev, variant, tables, far):
+@pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
+def test_udp_port_window(ctx, torch_dev, variant, tables, far, others):
     """small UDP socket sets (the compact LDS table) with the LDS port window:
     keys on the main address inside the window (bound, unbound, rebound:
     newest wins), outside it, on another address sharing window ports, and on
@@ -246,12 +247,16 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far):
     a few longer ones; verdicts and counts bit-exact against the oracle, with
     the window (tables 0; far = a main-address socket 10000 ports away, so
     the ports span more than the window's 4096 and none is built) and
-    without the port tables (NO_UDP_PORT)"""
+    without the port tables (NO_UDP_PORT).  one_address: no socket off the
+    main address, so with the window every key outside it is decided as a
+    miss without a probe (rx_ft_dev::udpc_other == 0)"""
     L, L2, L3 = "192.168.100.77", "10.9.9.9", "172.16.0.1"
     socks = [(L, 30000 + 3 * k) for k in range(300)]        # window 30000..33000
     socks += [(L2, 30000 + 21 * k) for k in range(20)]      # another address, shared ports
     socks += [(L, 30000 + 30 * k) for k in range(10)]       # rebinds: newest wins
     socks += [(L, 40000 if far else 33000), (L2, 5555)]
+    if not others:
+        socks = [x for x in socks if x[0] == L]
     udp = np.zeros(len(socks), R.UDP_SOCK_DTYPE)
     for i, (ip, port) in enumerate(socks):
         udp[i] = (R.ip_raw(ip), R.port_raw(port), 17, 0)

@@ -107,6 +107,13 @@ if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs 
     bench ab2buf$k 240 $Q --tune-tables 4 || exit $?
   done
 fi
+if [ "${ABCS:-0}" = 1 ]; then  # cfg4 (and cfg5): count passes on the count stream (default) vs after K1 on its stream
+  Q="--workload cfg4,cfg5 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
+  for k in 1 2; do
+    bench abcs$k 240 $Q || exit $?
+    bench abnocs$k 240 $Q --no-count-stream || exit $?
+  done
+fi
 if [ "${N2:-0}" = 1 ]; then
   # the N = 2 logic with two ranks on this one GPU: the default per-rank
   # shards, then the split of one global burst (the golden frame digest over

@@ -39,6 +39,52 @@ __global__ __launch_bounds__(256) void k_stream(const u32x4 *__restrict__ in, si
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// the plain read with U independent 16-B loads in flight per lane (U blocks
+// of the grid-stride sequence at once): does more in flight (a wider window
+// of open DRAM rows) slow the plain read the way the slot shapes are slow?
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_u(const u32x4 *__restrict__ in, size_t n16,
+                                                  unsigned *__restrict__ sink) {
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ldnt(in + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += csum(v[u]);
+    }
+    for (; i < n16; i += stride) acc += csum(ldnt(in + i));
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// G = 8 lanes per slot in two phases of 6 loads (half the bytes in flight)
+__global__ __launch_bounds__(256) void k_slotg8_half(const u32x4 *__restrict__ in, size_t nslots,
+                                                     u32x4 *__restrict__ out) {
+    const unsigned gl = threadIdx.x & 7u;
+    const size_t groups = (size_t)gridDim.x * 32;
+    for (size_t f = (size_t)blockIdx.x * 32 + (threadIdx.x >> 3); f < nslots; f += groups) {
+        const u32x4 *p = in + f * 96;
+        unsigned acc = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u32x4 v[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const unsigned c = (h * 6 + q) * 8 + gl;
+                v[q] = c < 94 ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc += csum(v[q]);
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (gl == 0) __builtin_nontemporal_store(u32x4{acc, (unsigned)f, 0, 0}, out + f);
+    }
+}
+
 // G = 8 lanes per 1536-B slot, all 12 passes in flight (94 chunks read)
 __global__ __launch_bounds__(256) void k_slotg8(const u32x4 *__restrict__ in, size_t nslots,
                                                 u32x4 *__restrict__ out) {
@@ -145,6 +191,23 @@ int main() {
     int cu = 0;
     CHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
     const int reps = 20;
+    // in-flight sweep: the plain read with 1/2/4/8 loads per lane and the G=8
+    // slot shape at 1-8 blocks per CU, full and half passes
+    for (int round = 0; round < 2; ++round) {
+        for (int bpc : {1, 2, 3, 4, 6, 8}) {
+            const int g = cu * bpc;
+            float ms;
+#define SU(U)                                                                                      \
+    ms = timeit([&] { k_stream_u<U><<<g, 256>>>(in, bytes / 16, sink); }, reps);                   \
+    printf("s%d bpc=%d stream U=%d      %.4f ms %7.0f GB/s (read)\n", round, bpc, U, ms, bytes / ms / 1e6);
+            SU(1) SU(2) SU(4) SU(8)
+#undef SU
+            ms = timeit([&] { k_slotg8<<<g, 256>>>(in, nslots, out); }, reps);
+            printf("s%d bpc=%d slotg8          %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
+            ms = timeit([&] { k_slotg8_half<<<g, 256>>>(in, nslots, out); }, reps);
+            printf("s%d bpc=%d slotg8 half     %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
+        }
+    }
     for (int round = 0; round < 3; ++round) {
         for (int bpc : {4, 8}) {
             const int g = cu * bpc;
