@@ -192,9 +192,10 @@ int64_t nstack_drain_all_sum(void *buf, size_t cap, uint64_t *bytes, uint64_t *s
  * count is 0. */
 int nstack_set_rx_inplace(int on, void (*release)(rxg_mbuf *m, void *arg), void *arg);
 /* Items the application has read (fragments, datagram batches) are handed
- * back to the protocol thread and freed by its next nstack_rx_burst /
- * nstack_tx_burst / nstack_deliver call (or nstack_reclaim, a protocol-thread
- * call): in place, a frame's mbuf count reaches 0 there.  A thread that made
+ * back to the protocol thread and freed by its next nstack_rx_burst (while
+ * that burst is on the GPU) / nstack_tx_burst / nstack_deliver call (or
+ * nstack_reclaim, a protocol-thread call): in place, a frame's mbuf count
+ * reaches 0 there.  A thread that made
  * one of those calls frees what it reads at once. */
 void nstack_reclaim(void);
 /* drop one reference on each of n mbufs (rte_pktmbuf_free of a burst):
