@@ -1164,8 +1164,15 @@ int rxg_ft_dump(rxg_ctx *c, uint32_t which, int device_copy, void *dst, uint64_t
     if (which == 0) h = fs.udp.tab.slots.data(), d = c->d_udp, n = fs.udp.tab.slots.size() * 16ull;
     else if (which == 1) h = fs.tcp.tab.slots.data(), d = c->d_tcp, n = fs.tcp.tab.slots.size() * 16ull;
     else if (which == 2) h = fs.listen.data(), d = c->d_listen, n = 65536 * 4ull;
+    else if (which == 3) h = fs.udpc.data(), d = c->d_udpc, n = fs.udpc.size() * 8ull;
+    else if (which == 4) h = fs.udpw.data(), d = c->d_udpw, n = fs.udpw.size() * 2ull;
     else return RXG_EINVAL;
-    if (info) {
+    if (info && which >= 3) {
+        info[0] = fs.udpc.empty() ? 0u : (uint32_t)fs.udpc.size() - 1, info[1] = fs.udpc_probe;
+        info[2] = fs.seed, info[3] = fs.udpc_other, info[4] = fs.udpw_lo;
+        info[5] = (uint32_t)fs.udpw.size(), info[6] = fs.udp_dip;
+        info[7] = which == 3 ? (uint32_t)fs.udpc.size() : (uint32_t)fs.udpw.size();
+    } else if (info) {
         info[0] = c->ft.tcp_mask, info[1] = c->ft.tcp_probe, info[2] = c->ft.hseed;
         info[3] = fs.tcp.tab.mask, info[4] = fs.tcp.tab.probe, info[5] = fs.seed;
         info[6] = c->dirty ? 1u : 0u, info[7] = (uint32_t)(n / 16);

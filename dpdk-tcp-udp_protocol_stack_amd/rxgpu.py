@@ -727,10 +727,12 @@ def sockaddr(ip: str, port: int) -> SockaddrIn:
 
 
 def ft_dump(h, which: int, device: bool):
-    """rxg_ft_dump of context handle h: (uint32 array of the table, info[8])"""
+    """rxg_ft_dump of context handle h: (uint32 array of the table, info[8]);
+    which 3 / 4: the compact UDP table / the port window (include/rxgpu.h)"""
     info = np.zeros(8, np.uint32)
     _check(_ft_dump(h, which, int(device), None, 0, _ptr(info)), "rxg_ft_dump")  # sizes
-    words = int(info[7]) * 4 if which < 2 else 65536
+    words = {0: int(info[7]) * 4, 1: int(info[7]) * 4, 2: 65536, 3: int(info[7]) * 2,
+             4: (int(info[7]) + 1) // 2}[which]
     buf = np.zeros(words, np.uint32)
     _check(_ft_dump(h, which, int(device), _ptr(buf), buf.nbytes, _ptr(info)), "rxg_ft_dump")
     return buf, info

@@ -546,10 +546,15 @@ int rxg_flow_counts(rxg_ctx *ctx, uint64_t *counts, uint32_t ncounts);
 int rxg_counts_reset(rxg_ctx *ctx);
 uint32_t rxg_num_flows(const rxg_ctx *ctx);
 
-/* Diagnostics: flow table `which` (0 UDP slots, 1 TCP slots, 2 listeners) as
- * the device holds it (device_copy != 0; after this context's bursts drain)
- * or as the host image is, up to `bytes`; info (nullable) = {device tcp_mask,
- * tcp_probe, hseed, host tcp mask, probe, seed, changes pending, slots}. */
+/* Diagnostics: flow table `which` (0 UDP slots, 1 TCP slots, 2 listeners,
+ * 3 the lane kernel's compact UDP table (8-B slots {dip, dport | flow << 16}),
+ * 4 its UDP port window (u16 flow ids, 0xFFFF none)) as the device holds it
+ * (device_copy != 0; after this context's bursts drain) or as the host image
+ * is, up to `bytes`; info (nullable) = {device tcp_mask, tcp_probe, hseed,
+ * host tcp mask, probe, seed, changes pending, slots} for 0-2, and for 3-4
+ * {slots - 1 of the compact table, its longest probe, hseed, compact keys off
+ * the window's address, window's first port (host order), window length,
+ * window's address (raw), entries of `which`}. */
 int rxg_ft_dump(rxg_ctx *ctx, uint32_t which, int device_copy, void *dst, uint64_t bytes,
                 uint32_t info[8]);
 
