@@ -1065,8 +1065,9 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         import threading
 
         # the application lcore in C (tools/libappthread.so: nstack_drain_all
-        # in a loop, 20-us pause when a pass finds nothing); a Python thread
-        # in that role measured the interpreter's lock hand-offs, not the stack
+        # in a loop, waiting on the deliveries counter when a pass finds
+        # nothing); a Python thread in that role measured the interpreter's
+        # lock hand-offs, not the stack
         applib = _appthread_lib()
 
         def overlapped(cpus=None, unpin=False):
@@ -1115,7 +1116,8 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         rx_burst_phases_ms={k: round(float(np.median([p[k] for p in ov_ph])), 4)
                                             for k in ov_ph[0]},
                         app_drain_ms=round(r.drain_ms / K, 3), app_passes=int(r.passes),
-                        app_empty_passes=int(r.empty), app_thread="C (tools/libappthread.so)",
+                        app_empty_passes=int(r.empty), app_sleeps=int(r.sleeps),
+                        app_thread="C (tools/libappthread.so)",
                         cpus=list(cpus) if cpus else None,
                         note="application thread draining while the protocol thread runs "
                              "the bursts" + ("; the two threads on the lcores above" if cpus else
@@ -1169,7 +1171,7 @@ class AppResult(C.Structure):
     """tools/appthread.c app_result"""
     _fields_ = [("items", C.c_int64), ("bytes", C.c_uint64), ("sum", C.c_uint64),
                 ("passes", C.c_uint64), ("empty", C.c_uint64), ("drain_ms", C.c_double),
-                ("err", C.c_int64)]
+                ("err", C.c_int64), ("sleeps", C.c_uint64)]
 
 
 def _appthread_lib():

@@ -242,6 +242,10 @@ static uint64_t g_pl_waits; /* submits that waited for a buffer (stat 11) */
 /* drain_all's time, ns (stats 8-10): waiting for the stack's lock, stepping
  * aside for the protocol thread, reading the taken-out fragments */
 static atomic_llong g_drain_ns[3];
+/* bursts delivered (nstack_rx_burst, nstack_deliver; stat 12): bumped with
+ * release order after a burst's deliveries, so a polling application that
+ * reads a new value (acquire) finds that burst's items in drain_all's look */
+static atomic_ullong g_deliveries;
 /* In-place TCP delivery (nstack_set_rx_inplace): a receive fragment whose
  * payload was captured whole points into its frame and holds the frame's mbuf
  * (refcnt@18, as rte_mbuf_refcnt_update) until the application has read it;
@@ -306,10 +310,17 @@ static void reclaim(void) {
         o = nx;
     }
 }
+/* The queue counters (a tcb's rq / sq, a UDP socket's queued) are written
+ * under the block's mutex and read without it by drain_all's look for work
+ * (drain_impl): relaxed atomic stores and that relaxed load, so the look is
+ * no data race (holders of the mutex read them plainly). */
+static inline uint32_t cnt_peek(const uint32_t *c) { return __atomic_load_n(c, __ATOMIC_RELAXED); }
+static inline void cnt_set(uint32_t *c, uint32_t v) { __atomic_store_n(c, v, __ATOMIC_RELAXED); }
+
 /* a standalone fragment at the tail (ring full: -ENOBUFS, the caller keeps it) */
 static int tq_push(struct nring *r, uint32_t *cnt, struct tcp_fragment *f) {
     if (*cnt >= D_RING_SIZE || ring_enqueue(r, f)) return -ENOBUFS;
-    (*cnt)++;
+    cnt_set(cnt, *cnt + 1);
     return 0;
 }
 /* the logical head, or NULL */
@@ -333,7 +344,7 @@ static struct tcp_fragment *tq_at(struct nring *r, uint32_t k) {
 static void tq_pop(struct nring *r, uint32_t *cnt) {
     struct tcp_fragment *f;
     if (ring_peek(r, (void **)&f)) return;
-    (*cnt)--;
+    cnt_set(cnt, *cnt - 1);
     if (f->batch && ++f->batch->next < f->batch->n) return;
     ring_dequeue(r, (void **)&f);
     frag_item_free(f);
@@ -345,7 +356,7 @@ static struct tcp_fragment *tq_detach(struct nring *r, uint32_t *cnt) {
     if (ring_peek(r, (void **)&f)) return NULL;
     if (!f->batch) {
         ring_dequeue(r, (void **)&f);
-        (*cnt)--;
+        cnt_set(cnt, *cnt - 1);
         return f;
     }
     const struct tcp_fragment *m = &f->batch->frag[f->batch->next];
@@ -370,7 +381,7 @@ static struct tcp_fragment *tq_detach(struct nring *r, uint32_t *cnt) {
 static void tq_clear(struct nring *r, uint32_t *cnt) {
     void *p;
     while (ring_dequeue(r, &p) == 0) frag_item_free(p);
-    *cnt = 0;
+    cnt_set(cnt, 0);
 }
 
 #define LL_ADD(item, list)                                                                         \
@@ -794,6 +805,7 @@ void nstack_fini(void) {
     /* every counter nstack_stat reports describes the current stack */
     g_stale_parts = g_copied_bytes = g_pl_waits = 0;
     for (int j = 0; j < 3; j++) atomic_store_explicit(&g_drain_ns[j], 0, memory_order_relaxed);
+    atomic_store_explicit(&g_deliveries, 0, memory_order_relaxed);
     g_isn_seed = 0;
     while (g_arp) {
         struct arp_entry *e = g_arp;
@@ -1103,10 +1115,10 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
                 r->protocol = IPPROTO_UDP;
                 r->data = rest;
                 r->length = (uint16_t)(length - len);
-                if (ring_enqueue(h->rcvbuf, r)) offload_free(r), h->queued--;
+                if (ring_enqueue(h->rcvbuf, r)) offload_free(r), cnt_set(&h->queued, h->queued - 1);
             } else {
                 free(r);
-                h->queued--;
+                cnt_set(&h->queued, h->queued - 1);
             }
             memset(buf, 0, len);
             memcpy(buf, b->data + d->off, d->ncopy < len ? d->ncopy : len);
@@ -1116,7 +1128,7 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
         }
         memcpy(buf, b->data + d->off, d->ncopy); /* :558-564: payload, then zeros */
         memset((unsigned char *)buf + d->ncopy, 0, length - d->ncopy);
-        h->queued--;
+        cnt_set(&h->queued, h->queued - 1);
         offload_free(spent);
         pthread_mutex_unlock(&h->mutex);
         return (ssize_t)length;
@@ -1136,7 +1148,7 @@ static ssize_t udp_recv(struct localhost *h, void *buf, size_t len, int flags,
         pthread_mutex_unlock(&h->mutex);
         return (ssize_t)len;
     }
-    h->queued--;
+    cnt_set(&h->queued, h->queued - 1);
     pthread_mutex_unlock(&h->mutex);
     ssize_t n = o->length; /* :558-564 */
     memcpy(buf, o->data, o->length);
@@ -1483,7 +1495,7 @@ static int deliver_one(const rxg_mbuf *m, const rxg_verdict *v, int *rc) {
     memcpy(o->data, f + v->payload_off, ncopy); /* udp.c:46 */
     pthread_mutex_lock(&h->mutex);
     int e = h->queued >= D_RING_SIZE ? -ENOBUFS : ring_enqueue(h->rcvbuf, o); /* udp.c:48 */
-    if (!e) h->queued++, pthread_cond_signal(&h->cond); /* udp.c:50-52 */
+    if (!e) cnt_set(&h->queued, h->queued + 1), pthread_cond_signal(&h->cond); /* udp.c:50-52 */
     pthread_mutex_unlock(&h->mutex);
     if (e) {
         free(o->data);
@@ -1569,6 +1581,7 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
             free(sg);
         }
         delivered = deliver_burst(m, n, v, rc_out, done);
+        atomic_fetch_add_explicit(&g_deliveries, 1, memory_order_release);
     }
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK ? delivered : rc;
@@ -1630,7 +1643,7 @@ static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const ui
             offload_free(o);
             g_stat[1] += take;
         } else {
-            h->queued += take;
+            cnt_set(&h->queued, h->queued + take);
             g_stat[0] += take;
             delivered += (int)take;
             pthread_cond_signal(&h->cond); /* udp.c:50-52 */
@@ -1793,7 +1806,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
             frag_item_free(&rb->item);
             g_stat[4] -= rtake, g_stat[1] += rtake;
         } else {
-            s->rq += rtake;
+            cnt_set(&s->rq, s->rq + rtake);
             pthread_cond_signal(&s->cond); /* tcp.c:178-180 */
         }
     }
@@ -1801,7 +1814,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
         if (ring_enqueue(s->sndbuf, &ab->item))
             free(ab);
         else
-            s->sq += atake;
+            cnt_set(&s->sq, s->sq + atake);
     }
     pthread_mutex_unlock(&s->mutex);
     if (st == TCP_STATUS_CLOSE_WAIT) restate_tcb(s, 0);
@@ -2043,6 +2056,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         g_phase_ms[10] = (float)(d[0].nseg + (parts > 1 ? d[1].nseg : 0));
         g_phase_ms[11] = (float)(d[0].ndgram + (parts > 1 ? d[1].ndgram : 0));
     }
+    if (done[0]) atomic_fetch_add_explicit(&g_deliveries, 1, memory_order_release);
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK || partial ? delivered : rc;
 }
@@ -2254,7 +2268,7 @@ static void drain_tcb(struct tcp_stream *s, void *buf, size_t cap, uint64_t *got
             continue;
         }
         ring_dequeue(s->rcvbuf, (void **)&f);
-        s->rq -= n - first;
+        cnt_set(&s->rq, s->rq - (n - first));
         sc->det[sc->nd++] = f;
     }
     tq_clear(s->sndbuf, &s->sq); /* its queued control fragments (ACKs) sent */
@@ -2293,14 +2307,17 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
             const uint32_t ncap = kind ? s_tcb_cap : s_udp_cap;
             uint32_t k = 0;
             for (; id < ncap && k < DRAIN_CHUNK; id++) {
+                /* a block with nothing queued is passed over without a
+                 * reference (its counters read, not its reference count
+                 * written: the protocol thread keeps the line) */
                 if (kind) {
                     struct tcp_stream *t = s_tcb_cb[id];
-                    if (!t) continue;
+                    if (!t || (!cnt_peek(&t->rq) && !cnt_peek(&t->sq))) continue;
                     cb_get(&t->ref);
                     blk[k++] = t;
                 } else {
                     struct localhost *h = s_udp_cb[id];
-                    if (!h) continue;
+                    if (!h || !cnt_peek(&h->queued)) continue;
                     cb_get(&h->ref);
                     blk[k++] = h;
                 }
@@ -2628,7 +2645,8 @@ int nstack_tx_burst(uint8_t *pkts, uint64_t cap_bytes, uint32_t *off, uint16_t *
 }
 
 uint64_t nstack_stat(int which) {
-    if (which < 0 || which > 11) return 0;
+    if (which < 0 || which > 12) return 0;
+    if (which == 12) return (uint64_t)atomic_load_explicit(&g_deliveries, memory_order_acquire);
     if (which == 7) return (uint64_t)atomic_load_explicit(&g_pl_batches, memory_order_relaxed);
     if (which >= 8) return (uint64_t)atomic_load_explicit(&g_drain_ns[which - 8], memory_order_relaxed);
     pthread_mutex_lock(&g_lock);

@@ -233,9 +233,12 @@ int nstack_set_halves(uint32_t min_half);
  * stack's lock, stepping aside for the protocol thread, reading out the
  * fragments it took from the tcbs (outside the lock); 11 = bursts that waited
  * for a pooled payload buffer while an application thread was draining (at
- * most 20 ms each; the stack's lock released meanwhile).  Counter 1
- * also counts TX items dropped (a send ring full, or a datagram too long for
- * a frame). */
+ * most 20 ms each; the stack's lock released meanwhile); 12 = bursts
+ * delivered (nstack_rx_burst, nstack_deliver), read without any lock: a
+ * polling application that reads a value it has not seen finds that burst's
+ * items in its next nstack_drain_all (bumped with release order after the
+ * deliveries, read with acquire).  Counter 1 also counts TX items dropped (a
+ * send ring full, or a datagram too long for a frame). */
 uint64_t nstack_stat(int which);
 
 #ifdef __cplusplus

@@ -49,8 +49,11 @@ static void *app(void *arg) {
     (void)arg;
     while (!atomic_load(&stop)) {
         uint64_t nb;
+        const uint64_t seen = nstack_stat(12); /* (as tools/appthread.c) */
         const int64_t g = nstack_drain_all(appbuf, sizeof appbuf, &nb);
         if (g > 0) atomic_fetch_add(&app_items, g);
+        else
+            while (nstack_stat(12) == seen && !atomic_load(&stop)) __builtin_ia32_pause();
     }
     uint64_t nb;
     const int64_t g = nstack_drain_all(appbuf, sizeof appbuf, &nb);
