@@ -29,6 +29,7 @@ def test_c_application_thread_reads_everything():
         rng = np.random.default_rng(5)
         want_items = want_bytes = 0
         r = bench.AppResult()
+        d0 = ns.stat(12)
         assert lib.app_start(-1, 0) == 0
         try:
             for _ in range(20):
@@ -50,6 +51,7 @@ def test_c_application_thread_reads_everything():
             assert lib.app_stop(C.byref(r)) == 0
         assert r.err == 0
         assert (r.items, r.bytes) == (want_items, want_bytes)
+        assert ns.stat(12) - d0 == 20  # one per delivered burst (lock-free counter)
         assert r.passes >= 1
         assert lib.app_stop(C.byref(r)) == -1  # not running
     finally:
