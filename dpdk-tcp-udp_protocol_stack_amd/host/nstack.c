@@ -136,6 +136,68 @@ struct dgram_batch {
     unsigned char *data;
 };
 
+/* ---- batch memory: each thread's cache of freed blocks, by size class ----
+ * A burst allocates one or two batches per connection (its receive fragments,
+ * its ACKs) or socket (its datagrams), and the protocol thread frees as many
+ * (reclaim); glibc serves blocks of these sizes (0.2-1.5 KB) from its small
+ * bins at 35-300 ns per call once its 7-entry per-size cache is exhausted
+ * (a burst frees thousands at once), a free list here at a few ns.  Blocks up
+ * to BP_CLASSES x BP_GRAN bytes, kept per class up to BP_KEEP; larger ones,
+ * and frees past the cap, go to malloc / free.  A thread's cache is released
+ * when it exits (bp_key) and by nstack_fini for the calling thread. */
+enum { BP_GRAN = 256, BP_CLASSES = 64, BP_KEEP = 16384 };
+struct bp_hdr {
+    uint32_t cls; /* 0: not cached (freed to malloc) */
+    uint32_t pad;
+    struct bp_hdr *next;
+}; /* 16 B: the block keeps malloc's 16-B alignment */
+static __thread struct bp_hdr *t_bp_head[BP_CLASSES];
+static __thread uint32_t t_bp_n[BP_CLASSES];
+static pthread_key_t bp_key;
+static pthread_once_t bp_once = PTHREAD_ONCE_INIT;
+static void bp_drain(void) {
+    for (int c = 0; c < BP_CLASSES; c++) {
+        while (t_bp_head[c]) {
+            struct bp_hdr *h = t_bp_head[c];
+            t_bp_head[c] = h->next;
+            free(h);
+        }
+        t_bp_n[c] = 0;
+    }
+}
+static void bp_thread_exit(void *v) { (void)v, bp_drain(); }
+static void bp_key_init(void) { (void)pthread_key_create(&bp_key, bp_thread_exit); }
+static void *bp_alloc(size_t sz) {
+    const size_t c = (sz + sizeof(struct bp_hdr) + BP_GRAN - 1) / BP_GRAN;
+    struct bp_hdr *h;
+    if (c < BP_CLASSES && t_bp_head[c]) {
+        h = t_bp_head[c];
+        t_bp_head[c] = h->next;
+        t_bp_n[c]--;
+        return h + 1;
+    }
+    h = malloc(c < BP_CLASSES ? c * BP_GRAN : sz + sizeof(*h));
+    if (!h) return NULL;
+    h->cls = c < BP_CLASSES ? (uint32_t)c : 0u;
+    return h + 1;
+}
+static void bp_free(void *p) {
+    if (!p) return;
+    struct bp_hdr *h = (struct bp_hdr *)p - 1;
+    const uint32_t c = h->cls;
+    if (c && t_bp_n[c] < BP_KEEP) {
+        if (!t_bp_n[c]) { /* (a thread's first cached block: its exit releases the cache) */
+            pthread_once(&bp_once, bp_key_init);
+            (void)pthread_setspecific(bp_key, (void *)1);
+        }
+        h->next = t_bp_head[c];
+        t_bp_head[c] = h;
+        t_bp_n[c]++;
+        return;
+    }
+    free(h);
+}
+
 /* Items the application threads are done with go back to the protocol
  * thread, which allocated them: freed there (reclaim, at its next burst
  * call), they stay in its malloc arena's fast paths instead of each free
@@ -148,10 +210,11 @@ static _Atomic(struct offload *) g_off_garbage;
 
 static void offload_free_now(struct offload *o) {
     if (!o) return;
-    if (o->batch)
-        free(o->batch); /* (meta and data live in the batch's allocation) */
-    else
-        free(o->data);
+    if (o->batch) { /* (one block: the item, the batch, its meta and data) */
+        bp_free(o);
+        return;
+    }
+    free(o->data);
     free(o);
 }
 static void offload_free(struct offload *o) {
@@ -274,7 +337,7 @@ static void frag_item_free_now(struct tcp_fragment *f) {
                 pthread_mutex_unlock(&g_pl_mx);
             }
         }
-        free(f->batch); /* (fragments and payloads live in the batch's allocation) */
+        bp_free(f->batch); /* (fragments and payloads live in the batch's block) */
     } else {
         if (f->mb)
             mb_put(f->mb);
@@ -400,6 +463,7 @@ static void tq_clear(struct nring *r, uint32_t *cnt) {
         (item)->prev = (item)->next = NULL;                                                        \
     } while (0)
 
+_Static_assert(sizeof(struct offload) % 8 == 0, "a datagram batch follows its item in one block");
 _Static_assert(offsetof(struct localhost, protocol) == offsetof(struct tcp_stream, protocol),
                "get_hostinfo_fromfd reads either block's protocol byte at one offset");
 
@@ -806,6 +870,7 @@ void nstack_fini(void) {
     g_stale_parts = g_copied_bytes = g_pl_waits = 0;
     for (int j = 0; j < 3; j++) atomic_store_explicit(&g_drain_ns[j], 0, memory_order_relaxed);
     atomic_store_explicit(&g_deliveries, 0, memory_order_relaxed);
+    bp_drain(); /* (this thread's cached batch blocks; other threads' go when they exit) */
     g_isn_seed = 0;
     while (g_arp) {
         struct arp_entry *e = g_arp;
@@ -1613,15 +1678,15 @@ static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const ui
                                    ? dl->len : (m[dl->frame]->data_len > 42u
                                                     ? m[dl->frame]->data_len - 42u : 0u);
         const size_t bytes = (size_t)(dl->offset - d0->offset) + lastc;
-        struct offload *o = calloc(1, sizeof(*o));
-        struct dgram_batch *b = o ? malloc(sizeof(*b) + take * sizeof(struct dgram_meta) + bytes + 1)
-                                  : NULL;
-        if (!b) {
-            free(o);
+        struct offload *o = bp_alloc(sizeof(*o) + sizeof(struct dgram_batch) +
+                                     take * sizeof(struct dgram_meta) + bytes + 1);
+        if (!o) {
             g_stat[1] += take;
             pthread_mutex_unlock(&h->mutex);
             continue;
         }
+        memset(o, 0, sizeof(*o));
+        struct dgram_batch *b = (struct dgram_batch *)(o + 1);
         b->n = take;
         b->next = 0;
         b->meta = (struct dgram_meta *)(b + 1);
@@ -1701,7 +1766,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
     const uint32_t rtake = nfr < rroom ? nfr : rroom, atake = nack < aroom ? nack : aroom;
     struct frag_batch *rb = NULL, *ab = NULL;
     if (rtake) { /* payload room: only the fragments that fit (a full ring drops the rest) */
-        rb = malloc(sizeof(*rb) + rtake * sizeof(struct tcp_fragment) + pbytes + 1);
+        rb = bp_alloc(sizeof(*rb) + rtake * sizeof(struct tcp_fragment) + pbytes + 1);
         if (rb) {
             memset(&rb->item, 0, sizeof(rb->item));
             rb->item.batch = rb;
@@ -1712,7 +1777,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
         }
     }
     if (atake) {
-        ab = malloc(sizeof(*ab) + atake * sizeof(struct tcp_fragment));
+        ab = bp_alloc(sizeof(*ab) + atake * sizeof(struct tcp_fragment));
         if (ab) {
             memset(&ab->item, 0, sizeof(ab->item));
             ab->item.batch = ab;
@@ -1812,7 +1877,7 @@ static int deliver_tcp_conn(struct tcp_stream *s, const rxg_segment *sg, uint32_
     }
     if (ab) {
         if (ring_enqueue(s->sndbuf, &ab->item))
-            free(ab);
+            bp_free(ab);
         else
             cnt_set(&s->sq, s->sq + atake);
     }
