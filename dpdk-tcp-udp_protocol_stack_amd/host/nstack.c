@@ -2298,6 +2298,62 @@ static void drain_detached(struct drain_scratch *sc, void *buf, uint64_t *got, u
     sc->nd = 0;
 }
 
+/* one UDP socket's receive ring emptied (its reference held): its items are
+ * taken out under one hold of its mutex and read after it is released, each
+ * datagram as udp_recv returns it (common.c:558-564: the captured payload,
+ * then zeros to dgram_len); with a buffer shorter than a datagram can be
+ * (cap < 65535), an item holding one that does not fit, and everything after
+ * it, is read through udp_recv's split path instead */
+static void drain_udp(struct localhost *h, void *buf, size_t cap, uint64_t *got, uint64_t *nb,
+                      uint64_t *hs, struct drain_scratch *sc) {
+    struct offload *o;
+    uint32_t taken = 0;
+    pthread_mutex_lock(&h->mutex);
+    while (!h->dead && ring_peek(h->rcvbuf, (void **)&o) == 0) {
+        const uint32_t a = o->batch ? o->batch->next : 0, n = o->batch ? o->batch->n : 1;
+        if (cap < 65535u) {
+            uint32_t j = a;
+            while (j < n && (o->batch ? (size_t)o->batch->meta[j].len + 8u : (size_t)o->length) <= cap) j++;
+            if (j < n) break;
+        }
+        if (sc->nd == sc->det_cap &&
+            grow((void **)&sc->det, &sc->det_cap, sc->det_cap ? 2 * sc->det_cap : 256, sizeof(void *)))
+            break;
+        ring_dequeue(h->rcvbuf, (void **)&o);
+        sc->det[sc->nd++] = o;
+        taken += n - a;
+    }
+    cnt_set(&h->queued, h->queued - taken);
+    pthread_mutex_unlock(&h->mutex);
+    unsigned char *out = buf;
+    for (uint32_t i = 0; i < sc->nd; i++) {
+        o = sc->det[i];
+        if (o->batch) {
+            const struct dgram_batch *b = o->batch;
+            for (uint32_t j = b->next; j < b->n; j++) {
+                const struct dgram_meta *d = &b->meta[j];
+                const uint32_t length = (uint32_t)d->len + 8u; /* (udp.c:37) */
+                memcpy(out, b->data + d->off, d->ncopy);
+                memset(out + d->ncopy, 0, length - d->ncopy);
+                (*got)++, *nb += length;
+                if (hs) *hs += fnv64(out, length);
+            }
+        } else {
+            memcpy(out, o->data, o->length);
+            (*got)++, *nb += o->length;
+            if (hs) *hs += fnv64(out, o->length);
+        }
+        offload_free(o);
+    }
+    sc->nd = 0;
+    ssize_t r; /* (what did not fit, and what arrived meanwhile) */
+    struct sockaddr_in sa;
+    while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&sa)) >= 0) {
+        (*got)++, *nb += (uint64_t)r;
+        if (hs) *hs += fnv64(buf, (size_t)r < cap ? (size_t)r : cap);
+    }
+}
+
 /* one tcb's receive ring emptied (its reference held): its items are taken
  * out under one hold of its mutex, to be read after it is released
  * (drain_detached); an item with a fragment longer than `cap` is read in
@@ -2416,14 +2472,8 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
                     tcb_put(blk[i]); /* (the items taken out are this call's) */
                     if (sc.nd >= 256 || i + 1 == k) drain_detached(&sc, buf, &got, &nb, hp);
                 } else {
-                    struct localhost *h = blk[i];
-                    ssize_t r;
-                    struct sockaddr_in a;
-                    while ((r = udp_recv(h, buf, cap, MSG_DONTWAIT, (struct sockaddr *)&a)) >= 0) {
-                        got++, nb += (uint64_t)r;
-                        if (hp) hs += fnv64(buf, (size_t)r < cap ? (size_t)r : cap);
-                    }
-                    udp_put(h);
+                    drain_udp(blk[i], buf, cap, &got, &nb, hp, &sc);
+                    udp_put(blk[i]);
                 }
             }
             atomic_fetch_add_explicit(&g_drain_ns[2], (long long)((mono_ms() - c0) * 1e6), memory_order_relaxed);
