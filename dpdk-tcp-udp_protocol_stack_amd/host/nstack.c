@@ -1623,6 +1623,69 @@ static void deliver_tcp_sorted(const rxg_segment *sg, uint32_t nseg, const uint8
                                int *rc_out);
 static uint32_t host_segments(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v,
                               rxg_segment *sg);
+static int deliver_udp_batches(rxg_mbuf *const *m, const rxg_dgram *dg, const uint32_t *first,
+                               const uint8_t *payload, uint32_t nf);
+
+/* The datagram records of a burst whose verdicts came from elsewhere
+ * (nstack_deliver), as the GPU's compaction hands them to nstack_rx_burst
+ * (rxg_udp_compact_dev): the rc-0 UDP verdicts naming a live socket id,
+ * grouped by id in burst order (first[f] .. first[f + 1]), each captured
+ * payload (min(dgram_len - 8, caplen - 42) bytes) at a 16-B aligned offset of
+ * one buffer, a socket's payloads contiguous.  So the host-only path delivers
+ * UDP through the same batches.  Returns the datagrams (0: none, or out of
+ * memory: the frame-by-frame path then delivers them); *payload is the
+ * buffer to free. */
+static uint32_t host_dgrams(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint32_t nf,
+                            rxg_dgram **dg_out, uint32_t **first_out, uint8_t **payload) {
+    *dg_out = NULL, *first_out = NULL, *payload = NULL;
+    uint32_t *first = calloc((size_t)nf + 2, sizeof(uint32_t));
+    if (!first) return 0;
+    uint32_t nd = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (v[i].cls == RXG_CLS_UDP && v[i].rc == RXG_RC_OK && v[i].flow_id < nf &&
+            s_udp_cb[v[i].flow_id])
+            first[v[i].flow_id + 1]++, nd++;
+    rxg_dgram *dg = nd ? malloc((size_t)nd * sizeof(*dg)) : NULL;
+    uint32_t *pos = nd ? malloc((size_t)nf * sizeof(uint32_t)) : NULL;
+    if (!dg || !pos) {
+        free(first), free(dg), free(pos);
+        return 0;
+    }
+    for (uint32_t f = 0; f < nf; f++) first[f + 1] += first[f], pos[f] = first[f];
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!(v[i].cls == RXG_CLS_UDP && v[i].rc == RXG_RC_OK && v[i].flow_id < nf &&
+              s_udp_cb[v[i].flow_id]))
+            continue;
+        const uint8_t *f = (const uint8_t *)m[i]->buf_addr + m[i]->data_off;
+        const uint32_t cap = m[i]->data_len;
+        rxg_dgram *d = &dg[pos[v[i].flow_id]++];
+        d->frame = i;
+        d->sip = cap >= 30 ? rd32(f + 26) : 0;
+        d->sport = cap >= 36 ? rd16(f + 34) : 0;
+        d->len = (uint16_t)v[i].payload_len;
+        const uint32_t avail = cap > 42u ? cap - 42u : 0u;
+        bytes += ((d->len < avail ? d->len : avail) + 15u) & ~15u;
+    }
+    free(pos);
+    uint8_t *pl = malloc(bytes + 16);
+    if (!pl) {
+        free(first), free(dg);
+        return 0;
+    }
+    uint32_t off = 0;
+    for (uint32_t j = 0; j < nd; j++) { /* socket by socket: each one's payloads contiguous */
+        rxg_dgram *d = &dg[j];
+        const rxg_mbuf *mb = m[d->frame];
+        const uint32_t avail = mb->data_len > 42u ? mb->data_len - 42u : 0u;
+        const uint32_t c = d->len < avail ? d->len : avail;
+        d->offset = off;
+        memcpy(pl + off, (const uint8_t *)mb->buf_addr + mb->data_off + 42u, c);
+        off += (c + 15u) & ~15u;
+    }
+    *dg_out = dg, *first_out = first, *payload = pl;
+    return nd;
+}
 
 int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_t gen,
                    int *rc_out) {
@@ -1635,6 +1698,14 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
         g_burst_stale = gen != g_snap_gen; /* classified against other lists */
         g_burst_mutated = 0;
         const uint8_t *done = NULL;
+        rxg_dgram *dg = NULL;
+        uint32_t *first = NULL;
+        uint8_t *pl = NULL;
+        if (!g_burst_stale && n && host_dgrams(m, n, v, s_udp_cap, &dg, &first, &pl)) {
+            delivered += deliver_udp_batches(m, dg, first, pl, s_udp_cap);
+            g_udp_done = 1; /* the per-frame loop leaves UDP alone */
+        }
+        free(dg), free(first), free(pl);
         if (!g_burst_stale && n) { /* the verdicts' flow ids name the live blocks */
             rxg_segment *sg = malloc((size_t)n * sizeof(*sg));
             if (!grow((void **)&s_handled, &s_handled_cap, n, 1) && sg) {
@@ -1645,7 +1716,8 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
             }
             free(sg);
         }
-        delivered = deliver_burst(m, n, v, rc_out, done);
+        delivered += deliver_burst(m, n, v, rc_out, done);
+        g_udp_done = 0;
         atomic_fetch_add_explicit(&g_deliveries, 1, memory_order_release);
     }
     pthread_mutex_unlock(&g_lock);
