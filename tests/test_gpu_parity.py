@@ -289,7 +289,8 @@ def test_udp_port_window(ctx, torch_dev, variant, tables, far, others):
         ctx.tune_tables(0)
     assert got.tobytes() == want.tobytes(), (variant, tables, _mismatch_report(got, want))
     assert np.array_equal(cnt, wcnt), (variant, tables)
-    assert (want["rc"] == 0).sum() > 1000 and (want["rc"] == -3).sum() > 500
+    # (hits: ~1,660 with the second address's sockets, ~925 without)
+    assert (want["rc"] == 0).sum() > 800 and (want["rc"] == -3).sum() > 500
 
 
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
