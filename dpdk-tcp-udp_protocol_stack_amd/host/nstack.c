@@ -2078,7 +2078,11 @@ int nstack_set_halves(uint32_t min_half) {
 
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
-    t_proto = 1; /* (the garbage lists are freed below, while the burst is on the GPU) */
+    t_proto = 1;
+    /* the garbage lists are freed below, while the burst is on the GPU; with
+     * pooled payload buffers (not in place) first, since the submit picks a
+     * buffer and the batches the application let go of may be what holds one */
+    if (!g_inplace) reclaim();
     proto_lock();
     pl_wait_free(); /* (two threads: the application frees the payload buffers) */
     const double t0 = mono_ms();
