@@ -142,10 +142,12 @@ struct dgram_batch {
  * (reclaim); glibc serves blocks of these sizes (0.2-1.5 KB) from its small
  * bins at 35-300 ns per call once its 7-entry per-size cache is exhausted
  * (a burst frees thousands at once), a free list here at a few ns.  Blocks up
- * to BP_CLASSES x BP_GRAN bytes, kept per class up to BP_KEEP; larger ones,
- * and frees past the cap, go to malloc / free.  A thread's cache is released
- * when it exits (bp_key) and by nstack_fini for the calling thread. */
+ * to BP_CLASSES x BP_GRAN bytes, kept up to BP_KEEP per class and BP_BYTES in
+ * all per thread; larger ones, and frees past the caps, go to malloc / free.
+ * A thread's cache is released when it exits (bp_key) and by nstack_fini for
+ * the calling thread. */
 enum { BP_GRAN = 256, BP_CLASSES = 64, BP_KEEP = 16384 };
+#define BP_BYTES (64ull << 20)
 struct bp_hdr {
     uint32_t cls; /* 0: not cached (freed to malloc) */
     uint32_t pad;
@@ -153,6 +155,7 @@ struct bp_hdr {
 }; /* 16 B: the block keeps malloc's 16-B alignment */
 static __thread struct bp_hdr *t_bp_head[BP_CLASSES];
 static __thread uint32_t t_bp_n[BP_CLASSES];
+static __thread uint64_t t_bp_bytes; /* bytes held by this thread's cache */
 static pthread_key_t bp_key;
 static pthread_once_t bp_once = PTHREAD_ONCE_INIT;
 static void bp_drain(void) {
@@ -164,6 +167,7 @@ static void bp_drain(void) {
         }
         t_bp_n[c] = 0;
     }
+    t_bp_bytes = 0;
 }
 static void bp_thread_exit(void *v) { (void)v, bp_drain(); }
 static void bp_key_init(void) { (void)pthread_key_create(&bp_key, bp_thread_exit); }
@@ -174,6 +178,7 @@ static void *bp_alloc(size_t sz) {
         h = t_bp_head[c];
         t_bp_head[c] = h->next;
         t_bp_n[c]--;
+        t_bp_bytes -= c * BP_GRAN;
         return h + 1;
     }
     h = malloc(c < BP_CLASSES ? c * BP_GRAN : sz + sizeof(*h));
@@ -185,7 +190,7 @@ static void bp_free(void *p) {
     if (!p) return;
     struct bp_hdr *h = (struct bp_hdr *)p - 1;
     const uint32_t c = h->cls;
-    if (c && t_bp_n[c] < BP_KEEP) {
+    if (c && t_bp_n[c] < BP_KEEP && t_bp_bytes + c * BP_GRAN <= BP_BYTES) {
         if (!t_bp_n[c]) { /* (a thread's first cached block: its exit releases the cache) */
             pthread_once(&bp_once, bp_key_init);
             (void)pthread_setspecific(bp_key, (void *)1);
@@ -193,6 +198,7 @@ static void bp_free(void *p) {
         h->next = t_bp_head[c];
         t_bp_head[c] = h;
         t_bp_n[c]++;
+        t_bp_bytes += c * BP_GRAN;
         return;
     }
     free(h);
