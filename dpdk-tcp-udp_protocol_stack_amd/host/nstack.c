@@ -44,7 +44,11 @@ enum {
     TCP_STATUS_LAST_ACK
 }; /* tcp.h:10-26 */
 
-/* ---- rings (stand-in for rte_ring; guarded by the owner's mutex) -------- */
+/* ---- rings (stand-in for rte_ring; guarded by the owner's mutex) --------
+ * The slot entries and head are stored with relaxed atomic stores: drain_all
+ * reads the head slot of the next block's ring without its mutex, as a
+ * prefetch hint (a value possibly stale, never dereferenced), and those
+ * reads are then no data race. */
 struct nring {
     void **slot;
     uint32_t cap, head, count;
@@ -67,7 +71,7 @@ static void ring_free(struct nring *r) {
 }
 static int ring_enqueue(struct nring *r, void *p) {
     if (r->count == r->cap) return -ENOBUFS;
-    r->slot[(r->head + r->count) % r->cap] = p;
+    __atomic_store_n(&r->slot[(r->head + r->count) % r->cap], p, __ATOMIC_RELAXED);
     r->count++;
     return 0;
 }
@@ -84,7 +88,7 @@ static int ring_peek_at(struct nring *r, uint32_t k, void **p) {
 static int ring_dequeue(struct nring *r, void **p) {
     if (!r->count) return -ENOENT;
     *p = r->slot[r->head];
-    r->head = (r->head + 1) % r->cap;
+    __atomic_store_n(&r->head, (r->head + 1) % r->cap, __ATOMIC_RELAXED);
     r->count--;
     return 0;
 }
@@ -2544,8 +2548,9 @@ static int64_t drain_impl(void *buf, size_t cap, uint64_t *bytes, uint64_t *sum)
                                             : (void *)((struct localhost *)blk[i + 2])->rcvbuf,
                                        0, 0);
                 if (kind && i + 1 < k) {
-                    const struct nring *r = ((struct tcp_stream *)blk[i + 1])->rcvbuf;
-                    const char *it = (const char *)r->slot[r->head % r->cap];
+                    struct nring *r = ((struct tcp_stream *)blk[i + 1])->rcvbuf;
+                    const uint32_t hd = __atomic_load_n(&r->head, __ATOMIC_RELAXED);
+                    const char *it = (const char *)__atomic_load_n(&r->slot[hd % r->cap], __ATOMIC_RELAXED);
                     if (it)
                         for (int q = 0; q < 8; q++) __builtin_prefetch(it + 64 * q, 0, 0);
                 }

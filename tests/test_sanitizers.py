@@ -42,3 +42,28 @@ def test_host_code_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0 and "SAN OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
     assert "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_socket_layer_threads_under_tsan(tmp_path):
+    """tests/san/tsan_harness.c: the protocol thread's bursts (UDP and TCP
+    batch paths, in-place receive), an application thread draining every
+    socket, another reading sockets one by one and a thread closing and
+    re-binding sockets, all at once, under ThreadSanitizer: no report"""
+    if not os.path.exists(os.path.join(PKG, "librxgpu.so")):
+        pytest.fail("librxgpu.so not built (run __graft_entry__.build())")
+    san = ["-fsanitize=thread", "-g", "-O1"]
+    objs = []
+    for src in ("oracle/ref_cpu.c", "dpdk-tcp-udp_protocol_stack_amd/host/nstack.c",
+                "tests/san/tsan_harness.c"):
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.run(["gcc", "-std=gnu11", *san, "-Iinclude", "-c", os.path.join(ROOT, src), "-o", o],
+                       check=True, cwd=ROOT)
+        objs.append(o)
+    exe = str(tmp_path / "tsan_harness")
+    subprocess.run(["gcc", *san, *objs, "-o", exe, f"-L{PKG}", "-lrxgpu", f"-Wl,-rpath,{PKG}",
+                    "-lpthread"], check=True, cwd=ROOT)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=0:exitcode=66"))
+    assert r.returncode == 0 and "TSAN OK" in r.stdout, r.stdout[-2000:] + r.stderr[-6000:]
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
