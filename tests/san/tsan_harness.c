@@ -5,6 +5,8 @@
  * bursts use), an application thread draining every socket
  * (nstack_drain_all_sum, waiting on the deliveries counter), a second
  * application thread reading sockets one by one (nrecvfrom / nrecv), and a
+ * thread sending from the UDP sockets (nsendto) while the protocol thread's
+ * TX pass frames what they queued and the ACKs (nstack_tx_burst), and a
  * thread closing and re-creating sockets meanwhile (nclose / nsocket / nbind;
  * in the second half of the bursts, so the first half takes the batch paths
  * and the second mostly the frame-by-frame path of a changed list).
@@ -115,6 +117,26 @@ static void *drainer(void *arg) {
     return NULL;
 }
 
+/* a thread sending datagrams from the UDP sockets (nsendto), which the
+ * protocol thread's TX pass (nstack_tx_burst) frames meanwhile */
+static atomic_llong g_sent;
+static void *sender(void *arg) {
+    (void)arg;
+    unsigned k = 0;
+    const char msg[] = "tsan harness datagram";
+    while (!atomic_load(&g_stop)) {
+        pthread_mutex_lock(&g_fd_mx);
+        const int fd = g_udp_fd[k++ % NUDP];
+        pthread_mutex_unlock(&g_fd_mx);
+        struct sockaddr_in a;
+        sa_of(&a, inet_addr("10.2.0.9"), 7777);
+        if (nsendto(fd, msg, sizeof msg, 0, (struct sockaddr *)&a, sizeof(a)) >= 0)
+            atomic_fetch_add(&g_sent, 1);
+        sched_yield();
+    }
+    return NULL;
+}
+
 /* a thread closing UDP sockets and binding new ones to the same ports */
 static void *churn(void *arg) {
     (void)arg;
@@ -169,10 +191,18 @@ int main(void) {
     static uint16_t len[BURST];
     static rxg_verdict v[BURST];
     static uint32_t tseq[NTCP];
-    pthread_t th[3];
+    static const uint8_t peer_mac[6] = {2, 0, 0, 0, 0, 9}, my_mac[6] = {2, 0, 0, 0, 0, 1};
+    CHECK(nstack_set_local(g_local, my_mac) == 0);
+    CHECK(nstack_arp_insert(inet_addr("10.2.0.9"), peer_mac) == 1);
+    uint8_t *txb = aligned_alloc(4096, 1 << 20);
+    static uint32_t txo[512];
+    static uint16_t txl[512];
+    long long txf = 0;
+    pthread_t th[4];
     CHECK(pthread_create(&th[0], NULL, drainer, NULL) == 0);
     CHECK(pthread_create(&th[1], NULL, reader, NULL) == 0);
     CHECK(pthread_create(&th[2], NULL, churn, NULL) == 0);
+    CHECK(pthread_create(&th[3], NULL, sender, NULL) == 0);
     srand(5);
     long long delivered = 0;
     for (int b = 0; b < NBURST; b++) {
@@ -213,14 +243,22 @@ int main(void) {
         const int r = nstack_deliver(mp[j], BURST, v, gen, NULL);
         CHECK(r >= 0);
         delivered += r;
+        uint64_t span = 0; /* the TX pass: ACKs and datagrams framed (no GPU checksum) */
+        const int tx = nstack_tx_burst(txb, 1 << 20, txo, txl, 512, 0, &span);
+        CHECK(tx >= 0);
+        txf += tx;
     }
     atomic_store(&g_stop, 1);
-    for (int i = 0; i < 3; i++) pthread_join(th[i], NULL);
+    for (int i = 0; i < 4; i++) pthread_join(th[i], NULL);
     nstack_reclaim();
-    printf("bursts %d, UDP datagrams delivered %lld, items read %lld, frames released %lld\n", NBURST,
-           delivered, (long long)atomic_load(&g_read_items), (long long)atomic_load(&released));
+    printf("bursts %d, UDP datagrams delivered %lld, items read %lld, frames released %lld, "
+           "datagrams sent %lld, TX frames %lld\n", NBURST, delivered,
+           (long long)atomic_load(&g_read_items), (long long)atomic_load(&released),
+           (long long)atomic_load(&g_sent), txf);
+    CHECK(txf > 0);
     nstack_fini();
     free(pool);
+    free(txb);
     printf("TSAN OK\n");
     return 0;
 }
