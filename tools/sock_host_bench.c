@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "../include/nstack.h"
@@ -86,7 +87,18 @@ int main(int argc, char **argv) {
         if (nstack_tcb_add(sip[k], L, sport[k], htons(9999), 4) != 0) return 2;
     }
     /* the frames: Ether + IPv4 + TCP (PSH|ACK) + 1446 B, 1536-B slots */
-    pool = aligned_alloc(4096, (size_t)NSET * B * SLOT);
+    /* the frame pool: 2-MB pages when HUGE=1 (transparent huge pages by
+     * madvise, as a DPDK mempool sits on hugepages), else 4-KB pages */
+    const size_t pbytes = (size_t)NSET * B * SLOT;
+    if (getenv("HUGE") && atoi(getenv("HUGE"))) {
+        const size_t al = 2u << 20;
+        uint8_t *raw = mmap(NULL, pbytes + al, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (raw == MAP_FAILED) return 3;
+        pool = (uint8_t *)(((uintptr_t)raw + al - 1) & ~(uintptr_t)(al - 1));
+        madvise(pool, pbytes, MADV_HUGEPAGE);
+    } else {
+        pool = aligned_alloc(4096, pbytes);
+    }
     uint8_t *f0 = pool;
     srand(7);
     for (int i = 0; i < B; i++) {
