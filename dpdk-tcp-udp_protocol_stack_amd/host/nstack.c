@@ -312,8 +312,9 @@ static atomic_int g_drainers;
 static pthread_mutex_t g_pl_mx = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t g_pl_cv = PTHREAD_COND_INITIALIZER;
 static uint64_t g_pl_waits; /* submits that waited for a buffer (stat 11) */
-/* drain_all's time, ns (stats 8-10): waiting for the stack's lock, stepping
- * aside for the protocol thread, reading the taken-out fragments */
+/* drain_all's time, ns (stats 8-10): waiting for the id maps' lock (g_tab),
+ * stepping aside for the protocol thread (0: no longer done), reading out
+ * what it took from the blocks */
 static atomic_llong g_drain_ns[3];
 /* bursts delivered (nstack_rx_burst, nstack_deliver; stat 12): bumped with
  * release order after a burst's deliveries, so a polling application that
@@ -480,8 +481,9 @@ _Static_assert(offsetof(struct localhost, protocol) == offsetof(struct tcp_strea
 /* ---- control-block lifetime ----------------------------------------------
  * A block carries a reference count: one for being linked (lists, id and fd
  * maps, flow tables) and one per application call that uses it after the
- * stack's lock is released (nrecv / nrecvfrom / nsendto / naccept /
- * drain_all take theirs under the lock, where the block is still linked).
+ * stack's lock is released (naccept takes its reference under g_lock;
+ * nrecv / nrecvfrom / nsendto / drain_all under g_tab, the id maps' lock:
+ * either way where the block is still linked).
  * Freeing a block (nclose, the last ACK of LAST_ACK) unlinks it under the
  * lock, marks it dead and wakes its waiters, then drops the linked reference;
  * whoever drops the last one frees the memory.  So a reader blocked in nrecv
@@ -575,17 +577,10 @@ static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 static int g_rx_in_flight;      /* nstack_rx_burst waits for the GPU (g_lock released) */
-/* The protocol thread (rx / tx bursts) takes g_lock ahead of application
- * loops: a pthread mutex is not fair, and drain_all, which re-takes the lock
- * chunk after chunk, could otherwise keep the protocol thread out for a whole
- * pass over the sockets.  g_proto_waiting counts its waits; such loops step
- * aside (app_yield) before each re-take while it is non-zero. */
-static atomic_int g_proto_waiting;
-static void proto_lock(void) {
-    atomic_fetch_add_explicit(&g_proto_waiting, 1, memory_order_relaxed);
-    pthread_mutex_lock(&g_lock);
-    atomic_fetch_sub_explicit(&g_proto_waiting, 1, memory_order_relaxed);
-}
+/* The protocol thread's (rx / tx bursts) hold of the stack's lock.  No
+ * application loop takes g_lock any more (drain_all and the receive calls
+ * look blocks up under g_tab), so nothing has to step aside for it. */
+static void proto_lock(void) { pthread_mutex_lock(&g_lock); }
 /* bursts of at least 2 * g_half_min frames run as two halves in flight
  * (nstack_set_halves; 0 = never) */
 static uint32_t g_half_min;
