@@ -230,9 +230,10 @@ int nstack_set_halves(uint32_t min_half);
  * buffer was free, or for a segment cut short by its capture), 7 = fragment
  * batches now queued that hold such a buffer (read without the lock); 8-10 =
  * nstack_drain_all's time in ns (read without the lock): waiting for the
- * stack's lock, stepping aside for the protocol thread, reading out the
- * fragments it took from the tcbs (outside the lock); 11 = bursts that waited
- * for a pooled payload buffer while an application thread was draining (at
+ * id maps' lock (never the stack's), stepping aside for the protocol thread
+ * (0 since round 5: nothing to step aside from), reading out what it took
+ * from the blocks (outside every lock but the block's own); 11 = bursts
+ * that waited for a pooled payload buffer while an application thread was draining (at
  * most 20 ms each; the stack's lock released meanwhile); 12 = bursts
  * delivered (nstack_rx_burst, nstack_deliver), read without any lock: a
  * polling application that reads a value it has not seen finds that burst's
