@@ -233,9 +233,9 @@ int nstack_set_halves(uint32_t min_half);
  * id maps' lock (never the stack's), stepping aside for the protocol thread
  * (0 since round 5: nothing to step aside from), reading out what it took
  * from the blocks (outside every lock but the block's own); 11 = bursts
- * that waited for a pooled payload buffer while an application thread was draining (at
- * most 20 ms each; the stack's lock released meanwhile); 12 = bursts
- * delivered (nstack_rx_burst, nstack_deliver), read without any lock: a
+ * that waited for a pooled payload buffer while an application thread was
+ * draining (at most 20 ms each; the stack's lock released meanwhile); 12 =
+ * bursts delivered (nstack_rx_burst, nstack_deliver), read without any lock: a
  * polling application that reads a value it has not seen finds that burst's
  * items in its next nstack_drain_all (bumped with release order after the
  * deliveries, read with acquire).  Counter 1 also counts TX items dropped (a
