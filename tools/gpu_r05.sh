@@ -4,7 +4,9 @@
 # --kernel-trace --stats of the bench on the SAME box, and the table tying
 # each workload's roofline.kernel to the trace.  Optional: SWING=1 the cfg2
 # placement / clock probe (tools/cfg2_swing.py) first thing and again after
-# the tests; PMC=1 HBM bytes; N2=1 the N = 2 spawn rehearsal.  Each GPU step
+# the tests; PMC=1 HBM bytes; N2=1 the N = 2 spawn rehearsal; PROC=1 cfg2 per
+# context and process; MEMBW3=1, SWEEPBPC=1 bytes-in-flight sweeps; ABCS=1
+# the count stream A/B; SOCKHOST=1 the host socket path alone.  Each GPU step
 # has its own time limit; a failing step ends the script.
 #     TAG=r05a bash tools/gpu_r05.sh
 set -u
@@ -106,6 +108,13 @@ if [ "${AB2BUF:-0}" = 1 ]; then  # cfg4: three count-index buffers (default) vs 
     bench ab3buf$k 240 $Q || exit $?
     bench ab2buf$k 240 $Q --tune-tables 4 || exit $?
   done
+fi
+if [ "${SWEEPBPC:-0}" = 1 ]; then  # resident blocks per CU (bytes in flight): cfg3's G=8 kernel, cfg2's lane kernel
+  step sweep_bpc3 400 python bench.py --sweep cfg3 --steps 20 --warmup 3 --sweep-counts \
+      --sweep-variants "8,2,2,40,0;8,2,2,40,1;8,2,2,40,2;8,2,2,40,3;8,2,2,40,4;8,2,2,40,5;8,2,2,40,6" || exit $?
+  step sweep_bpc2 400 python bench.py --sweep cfg2 --steps 50 --warmup 5 --sweep-counts \
+      --sweep-variants "1,4,1,14,0;1,4,1,14,1;1,4,1,14,2;1,4,1,14,3;1,4,1,14,4" || exit $?
+  grep -h sweep $OUT/sweep_bpc3.log $OUT/sweep_bpc2.log > $OUT/sweep_bpc_$TAG.txt || true
 fi
 if [ "${ABCS:-0}" = 1 ]; then  # cfg4 (and cfg5): count passes on the count stream (default) vs after K1 on its stream
   Q="--workload cfg4,cfg5 --no-cpu --no-sockrate --no-cfg1 --no-tx --no-v8"
