@@ -312,6 +312,7 @@ static atomic_int g_drainers;
 static pthread_mutex_t g_pl_mx = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t g_pl_cv = PTHREAD_COND_INITIALIZER;
 static uint64_t g_pl_waits; /* submits that waited for a buffer (stat 11) */
+static atomic_int g_pl_waiting; /* the protocol thread is in pl_wait_free */
 /* drain_all's time, ns (stats 8-10): waiting for the id maps' lock (g_tab),
  * stepping aside for the protocol thread (0: no longer done), reading out
  * what it took from the blocks */
@@ -362,11 +363,22 @@ static void frag_item_free(struct tcp_fragment *f) {
         frag_item_free_now(f);
         return;
     }
+    const int pooled = f->batch && f->batch->pl_ref >= 0;
     struct tcp_fragment *old = atomic_load_explicit(&g_frag_garbage, memory_order_relaxed);
     do
         f->gnext = old;
-    while (!atomic_compare_exchange_weak_explicit(&g_frag_garbage, &old, f, memory_order_release,
+    while (!atomic_compare_exchange_weak_explicit(&g_frag_garbage, &old, f, memory_order_seq_cst,
                                                   memory_order_relaxed));
+    /* a batch holding a pooled buffer: wake a protocol thread waiting for one
+     * in pl_wait_free, which reclaims it at once (it waited for
+     * its next 1-ms timed wakeup).  The push and this load are seq_cst, as
+     * are the waiter's flag store and its look at the list: either this sees
+     * the flag or the waiter sees the push */
+    if (pooled && atomic_load_explicit(&g_pl_waiting, memory_order_seq_cst)) {
+        pthread_mutex_lock(&g_pl_mx);
+        pthread_cond_broadcast(&g_pl_cv);
+        pthread_mutex_unlock(&g_pl_mx);
+    }
 }
 /* the protocol thread frees what the application threads let go of */
 static void reclaim(void) {
@@ -849,6 +861,16 @@ int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
 void nstack_fini(void) {
     reclaim();
     pthread_mutex_lock(&g_lock);
+    /* unmap every block first (as nclose unregisters before its kill): an
+     * application call looks blocks up under g_tab alone, so once the maps
+     * are clear no fd_get_ref / drain_all can take a reference on a block the
+     * kills below may free */
+    pthread_mutex_lock(&g_tab);
+    memset(g_fd_cb, 0, sizeof(g_fd_cb));
+    free(s_udp_cb), free(s_tcb_cb);
+    s_udp_cb = NULL, s_tcb_cb = NULL;
+    s_udp_cap = s_tcb_cap = 0;
+    pthread_mutex_unlock(&g_tab);
     while (g_pstHost) {
         struct localhost *h = g_pstHost;
         LL_REMOVE(h, g_pstHost);
@@ -860,12 +882,6 @@ void nstack_fini(void) {
         tcb_kill(s);
     }
     memset(g_ucFdTable, 0, sizeof(g_ucFdTable));
-    pthread_mutex_lock(&g_tab);
-    memset(g_fd_cb, 0, sizeof(g_fd_cb));
-    free(s_udp_cb), free(s_tcb_cb);
-    s_udp_cb = NULL, s_tcb_cb = NULL;
-    s_udp_cap = s_tcb_cap = 0;
-    pthread_mutex_unlock(&g_tab);
     memset(g_fd_nblk, 0, sizeof(g_fd_nblk));
     free(s_udp), free(s_tcb), free(s_v), free(s_udp_id), free(s_tcb_id), free(s_handled);
     s_udp = NULL, s_tcb = NULL, s_v = NULL, s_udp_id = NULL, s_tcb_id = NULL, s_handled = NULL;
@@ -2050,12 +2066,13 @@ static void pl_wait_free(void) {
     if (!atomic_load_explicit(&g_drainers, memory_order_relaxed) || pl_free()) return;
     const double t0 = mono_ms();
     g_pl_waits++;
+    atomic_store_explicit(&g_pl_waiting, 1, memory_order_seq_cst);
     while (!pl_free() && atomic_load_explicit(&g_drainers, memory_order_relaxed) &&
            mono_ms() - t0 < 20.0) {
         pthread_mutex_unlock(&g_lock);
         reclaim(); /* (the batches the application let go of free their buffers here) */
         pthread_mutex_lock(&g_pl_mx);
-        if (!pl_free()) {
+        if (!pl_free() && !atomic_load_explicit(&g_frag_garbage, memory_order_seq_cst)) {
             struct timespec ts;
             clock_gettime(CLOCK_REALTIME, &ts);
             ts.tv_nsec += 1000000;
@@ -2065,6 +2082,7 @@ static void pl_wait_free(void) {
         pthread_mutex_unlock(&g_pl_mx);
         proto_lock();
     }
+    atomic_store_explicit(&g_pl_waiting, 0, memory_order_relaxed);
 }
 
 /* after a submit: the set it took and the pooled buffer (or -1) it holds */
@@ -2184,11 +2202,12 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     }
     g_rx_in_flight = 0;
     /* the first half delivered, the second not put through the GPU (a failed
-     * second submit or wait): its frames are reported, not delivered */
-    const int partial = rc != RXG_OK && parts > 1 && done[0] && !done[1];
+     * second submit or wait): its frames are reported, not delivered.  Only a
+     * caller that passed rc_out can see that per frame; without it the call
+     * returns the error code, as a whole-burst failure does */
+    const int partial = rc != RXG_OK && parts > 1 && done[0] && !done[1] && rc_out;
     if (partial) {
-        if (rc_out)
-            for (uint32_t i = nh; i < n; i++) rc_out[i] = rc;
+        for (uint32_t i = nh; i < n; i++) rc_out[i] = rc;
         if (v_out) memset(v_out + nh, 0, (size_t)(n - nh) * sizeof(rxg_verdict));
     }
     if (rc == RXG_OK || partial) {

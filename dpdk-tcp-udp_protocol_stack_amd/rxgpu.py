@@ -1007,6 +1007,10 @@ class NStack:
         r = self.lib.nstack_rx_burst(C.cast(arr, _vp), n, _ptr(rcs), None)
         if r < 0:
             _check(r, "nstack_rx_burst")
+        # a two-half burst whose second half failed returns the first half's
+        # count and reports the error per frame in rcs: raise it
+        if rcs is not None and n and int(rcs[:n].min()) < -3:  # (the reference's own codes are -3..1)
+            _check(int(rcs[:n].min()), "nstack_rx_burst (second half)")
         return r
 
     def drain_all(self, buf: np.ndarray):
@@ -1046,7 +1050,12 @@ _COMPILED = {}
 def compiled_variants(vs):
     """the variants of `vs` the loaded library has compiled in, in order
     (the product library: KERNEL_VARIANTS; the RX_DIAG build, RXGPU_LIB=
-    .../librxgpu_diag.so: also its tuning shapes and ablations)"""
+    .../librxgpu_diag.so: also its tuning shapes and ablations).  A variant
+    in none of the three lists is an error, not a silent skip"""
+    known = set(map(tuple, KERNEL_VARIANTS + DIAG_TUNING_VARIANTS + DIAG_ABLATIONS))
+    unknown = [tuple(v) for v in vs if tuple(v) not in known]
+    if unknown:
+        raise ValueError(f"variants in no build's table: {unknown}")
     out = []
     with Context(HOST_ONLY) as c:
         for v in vs:

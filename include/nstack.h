@@ -82,9 +82,10 @@ int nclose(int fd);
  * have returned (KNI frames: 1); v_out (nullable) = the verdicts.
  * Returns the number of UDP datagrams delivered, or a negative RXG_E* code.
  * A burst run as two halves whose second half could not go through the GPU
- * after the first was delivered returns the first half's count: the second
- * half's rc_out entries hold the (negative RXG_E*) error and its v_out
- * entries are zero, so the caller can pass those frames again.
+ * after the first was delivered returns, when rc_out is given, the first
+ * half's count: the second half's rc_out entries hold the (negative RXG_E*)
+ * error and its v_out entries are zero, so the caller can pass those frames
+ * again.  With rc_out NULL it returns the error code.
  * Called by one protocol thread, which also runs nstack_tx_burst (as
  * pkt_process runs udp_out / tcp_out); while the burst is on the GPU the
  * stack's lock is released, so application threads' socket calls run beside

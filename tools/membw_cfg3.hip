@@ -108,6 +108,58 @@ __global__ __launch_bounds__(256) void k_slotg8(const u32x4 *__restrict__ in, si
     }
 }
 
+// the decomposition: the G=8 slot shape of k_slotg8 with
+// one component taken out at a time.  ST: the 16-B store per slot; RED: the
+// cross-lane sum of the 8 lanes' partial sums (3 __shfl_xor); FULL: all 96
+// chunks of the slot read (no masked last pass, 2 extra chunks = 2% more bytes)
+template <bool ST, bool RED, bool FULL>
+__global__ __launch_bounds__(256) void k_slot(const u32x4 *__restrict__ in, size_t nslots,
+                                              u32x4 *__restrict__ out, unsigned *__restrict__ sink) {
+    const unsigned gl = threadIdx.x & 7u;
+    const size_t groups = (size_t)gridDim.x * 32;
+    for (size_t f = (size_t)blockIdx.x * 32 + (threadIdx.x >> 3); f < nslots; f += groups) {
+        const u32x4 *p = in + f * 96;
+        u32x4 v[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const unsigned c = q * 8 + gl;
+            v[q] = (FULL || c < 94) ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+        }
+        unsigned acc = 0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc += csum(v[q]);
+        if (RED) {
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+        }
+        if (ST && gl == 0) __builtin_nontemporal_store(u32x4{acc, (unsigned)f, 0, 0}, out + f);
+        else if (acc == 0x12345678u) sink[gl] = acc; // (keeps the sum live, never taken)
+    }
+}
+
+// the plain grid-stride read plus one 16-B non-temporal store per 96 chunks
+// (per 1536-B slot), issued by the lane that reads the slot's first chunk
+__global__ __launch_bounds__(256) void k_stream_st(const u32x4 *__restrict__ in, size_t n16,
+                                                   u32x4 *__restrict__ out, unsigned *__restrict__ sink) {
+    unsigned acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    // slot q and chunk r of index i, advanced incrementally (no division per trip)
+    size_t q = i / 96;
+    unsigned r = (unsigned)(i % 96);
+    const size_t qs = stride / 96;
+    const unsigned rs = (unsigned)(stride % 96);
+    for (; i < n16; i += stride) {
+        acc += csum(ldnt(in + i));
+        if (r == 0) __builtin_nontemporal_store(u32x4{acc, (unsigned)q, 0, 0}, out + q);
+        q += qs;
+        r += rs;
+        if (r >= 96) { r -= 96; ++q; }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 // a wave owns F consecutive slots per trip (F even: 1.5 * F loads per lane);
 // load j of lane l reads chunk 64 j + l of the wave-tile, which belongs to
 // slot (64 j + l) / 96; chunks 94, 95 of each slot are padding (not counted)
@@ -206,6 +258,26 @@ int main() {
             printf("s%d bpc=%d slotg8          %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
             ms = timeit([&] { k_slotg8_half<<<g, 256>>>(in, nslots, out); }, reps);
             printf("s%d bpc=%d slotg8 half     %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
+        }
+    }
+    // the decomposition, interleaved, 3 rounds: which component of the slot
+    // shape costs the 0.912 -> 1.042 ms
+    for (int round = 0; round < 3; ++round) {
+        for (int bpc : {4, 8}) {
+            const int g = cu * bpc;
+            float ms;
+#define D(name, launch, B)                                                                         \
+    ms = timeit([&] { launch; }, reps);                                                            \
+    printf("d%d bpc=%d %-26s %.4f ms %7.0f GB/s (read)\n", round, bpc, name, ms, (B) / ms / 1e6);
+            D("stream", (k_stream<<<g, 256>>>(in, bytes / 16, sink)), (double)bytes)
+            D("stream+store", (k_stream_st<<<g, 256>>>(in, bytes / 16, out, sink)), (double)bytes)
+            D("slot st red", (k_slot<true, true, false><<<g, 256>>>(in, nslots, out, sink)), nslots * 1504.0)
+            D("slot nost red", (k_slot<false, true, false><<<g, 256>>>(in, nslots, out, sink)), nslots * 1504.0)
+            D("slot st nored", (k_slot<true, false, false><<<g, 256>>>(in, nslots, out, sink)), nslots * 1504.0)
+            D("slot nost nored", (k_slot<false, false, false><<<g, 256>>>(in, nslots, out, sink)), nslots * 1504.0)
+            D("slot st red full96", (k_slot<true, true, true><<<g, 256>>>(in, nslots, out, sink)), (double)bytes)
+            D("slot nost nored full96", (k_slot<false, false, true><<<g, 256>>>(in, nslots, out, sink)), (double)bytes)
+#undef D
         }
     }
     for (int round = 0; round < 3; ++round) {
