@@ -138,6 +138,77 @@ __global__ __launch_bounds__(256) void k_slot(const u32x4 *__restrict__ in, size
     }
 }
 
+// store flavours for the slot shape's verdict: 0 nt, 1 plain (write-back,
+// the L2 absorbs the lines), 2 sc1 (write-through, K1's pipe 40)
+template <int SM>
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 w) {
+    if constexpr (SM == 0) __builtin_nontemporal_store(w, p);
+    else if constexpr (SM == 1) *p = w;
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
+}
+
+// the slot shape with the verdict store in flavour SM
+template <int SM>
+__global__ __launch_bounds__(256) void k_slot_sm(const u32x4 *__restrict__ in, size_t nslots,
+                                                 u32x4 *__restrict__ out) {
+    const unsigned gl = threadIdx.x & 7u;
+    const size_t groups = (size_t)gridDim.x * 32;
+    for (size_t f = (size_t)blockIdx.x * 32 + (threadIdx.x >> 3); f < nslots; f += groups) {
+        const u32x4 *p = in + f * 96;
+        u32x4 v[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const unsigned c = q * 8 + gl;
+            v[q] = c < 94 ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+        }
+        unsigned acc = 0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc += csum(v[q]);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (gl == 0) st16<SM>(out + f, u32x4{acc, (unsigned)f, 0, 0});
+    }
+}
+
+// a wave owns runs of 64 consecutive slots (8 trips of 8 slots, G=8 as
+// above); WIDE: the 64 verdicts are gathered into lane i (lane 8t+g takes
+// group g's sum at trip t over ds_bpermute) and leave as ONE 1-KiB store per
+// run; else each trip's 8 verdicts leave as one 128-B store (same mapping)
+template <int SM, bool WIDE>
+__global__ __launch_bounds__(256) void k_slotrun(const u32x4 *__restrict__ in, size_t nslots,
+                                                 u32x4 *__restrict__ out) {
+    const unsigned lane = threadIdx.x & 63u, gl = lane & 7u, g = lane >> 3;
+    const size_t nw = (size_t)gridDim.x * 4, nruns = nslots / 64;
+    for (size_t r = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < nruns; r += nw) {
+        unsigned keep = 0;
+#pragma unroll 1
+        for (unsigned t = 0; t < 8; ++t) {
+            const size_t f = r * 64 + t * 8 + g;
+            const u32x4 *p = in + f * 96;
+            u32x4 v[12];
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                const unsigned c = q * 8 + gl;
+                v[q] = c < 94 ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+            }
+            unsigned acc = 0;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) acc += csum(v[q]);
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+            if (WIDE) {
+                const unsigned x = __shfl(acc, (int)((lane & 7u) * 8u)); // group (lane & 7)'s sum
+                keep = (lane >> 3) == t ? x : keep;
+            } else if (gl == 0) {
+                st16<SM>(out + f, u32x4{acc, (unsigned)f, 0, 0});
+            }
+        }
+        if (WIDE) st16<SM>(out + r * 64 + lane, u32x4{keep, (unsigned)(r * 64 + lane), 0, 0});
+    }
+}
+
 // the plain grid-stride read plus one 16-B non-temporal store per 96 chunks
 // (per 1536-B slot), issued by the lane that reads the slot's first chunk
 __global__ __launch_bounds__(256) void k_stream_st(const u32x4 *__restrict__ in, size_t n16,
@@ -277,6 +348,12 @@ int main() {
             D("slot nost nored", (k_slot<false, false, false><<<g, 256>>>(in, nslots, out, sink)), nslots * 1504.0)
             D("slot st red full96", (k_slot<true, true, true><<<g, 256>>>(in, nslots, out, sink)), (double)bytes)
             D("slot nost nored full96", (k_slot<false, false, true><<<g, 256>>>(in, nslots, out, sink)), (double)bytes)
+            D("slot st plain", (k_slot_sm<1><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("slot st sc1", (k_slot_sm<2><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("run64 st nt 128B/trip", (k_slotrun<0, false><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("run64 st nt 1KiB/run", (k_slotrun<0, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("run64 st plain 1KiB/run", (k_slotrun<1, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("run64 st sc1 1KiB/run", (k_slotrun<2, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
 #undef D
         }
     }
