@@ -205,6 +205,23 @@ def collective_fn(group, nccl_group, nflows):
     return run
 
 
+def gather_rank_stats(world, el, steps, stream_ms, ar_ms, n):
+    """N > 1, every rank: each rank's wall step, kernel-stream step,
+    all-reduce time and frames (all_gather over the control plane, gloo), and
+    the max over ranks of the timed region's wall time, which `value` divides
+    by.  Returns (per_rank list, max wall seconds)."""
+    mine = torch.tensor([el / max(steps, 1) * 1e3, stream_ms, ar_ms, float(n)], dtype=torch.float64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    torch.distributed.all_gather(allr, mine)
+    per_rank = [dict(rank=r, ms_per_step=round(float(x[0]), 4),
+                     stream_ms_per_step=round(float(x[1]), 4),
+                     allreduce_ms=round(float(x[2]), 4), frames=int(x[3]))
+                for r, x in enumerate(allr)]
+    t = torch.tensor([el], dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return per_rank, float(t.item())
+
+
 def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_sample=4096,
                  oracle_threads=1, shard_mode="direct"):
     w = rxdist.WORKLOADS[name]
@@ -326,19 +343,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
         aev[1].record(cs)
         torch.cuda.synchronize(dev)
         ar_ms = aev[0].elapsed_time(aev[1]) / max(steps, 1)
-        # per-rank wall step, kernel-stream step and all-reduce times, then the
-        # max over ranks (gloo: control plane on the host)
-        mine = torch.tensor([el / max(steps, 1) * 1e3, kms[0], ar_ms, float(n)],
-                            dtype=torch.float64)
-        allr = [torch.zeros_like(mine) for _ in range(world)]
-        torch.distributed.all_gather(allr, mine)
-        per_rank = [dict(rank=r, ms_per_step=round(float(x[0]), 4),
-                         stream_ms_per_step=round(float(x[1]), 4),
-                         allreduce_ms=round(float(x[2]), 4), frames=int(x[3]))
-                    for r, x in enumerate(allr)]
-        t = torch.tensor([el], dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
+        per_rank, el = gather_rank_stats(world, el, steps, kms[0], ar_ms, n)
     kdisp = kernel_dispatches(ctx, pk, off, ln, n, ul, w["len_hint"], out, counts, stream, csh,
                               dev, alg_bytes, cs if use_cs else None)
     # counts: every delivered verdict counted once per step, on every rank
@@ -1029,14 +1034,20 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # delivery steps), median over the bursts
         res["rx_burst_phases_ms"] = {k: round(float(np.median([p[k] for p in phases])), 4)
                                      for k in phases[0]}
-        def ab_run():  # the sequential loop again, for an A/B
+        def ab_run(pipelined=False):  # the sequential loop again, for an A/B
             h_rx = h_dr = 0.0
             h_items = 0
             h_ph = []
-            for _ in range(K):
-                arr = next_set()
+            if pipelined:  # burst k+1 on the GPU while burst k is delivered and read
+                ns.rx_submit_mbufs(next_set(), B)
+            for k in range(K):
                 t0 = time.perf_counter()
-                ns.rx_burst_mbufs(arr, B)
+                if pipelined:
+                    if k + 1 < K:
+                        ns.rx_submit_mbufs(next_set(), B)
+                    ns.rx_complete_mbufs()
+                else:
+                    ns.rx_burst_mbufs(next_set(), B)
                 t1 = time.perf_counter()
                 h_ph.append(ns.last_burst_phases())
                 g, _ = ns.drain_all(rbuf)
@@ -1053,6 +1064,11 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         ns.set_rx_inplace(False)
         res["pooled_payload"] = ab_run()
         ns.set_rx_inplace(True)
+        # A/B: pipelined (nstack_rx_submit / nstack_rx_complete): burst k+1
+        # crosses PCIe and goes through the kernels while burst k is delivered
+        # and read (the first submit is outside the clock, as a loop's first
+        # burst would be in flight already)
+        res["pipelined"] = ab_run(pipelined=True)
         # A/B: each burst as two halves, both on the GPU at once
         # (nstack_set_halves; off by default)
         ns.set_halves(B // 2)
@@ -1077,7 +1093,7 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # lock hand-offs, not the stack
         applib = _appthread_lib()
 
-        def overlapped(cpus=None, unpin=False):
+        def overlapped(cpus=None, unpin=False, pipelined=False):
             main_aff = os.sched_getaffinity(0)
             if cpus:
                 os.sched_setaffinity(0, {cpus[0]})
@@ -1093,10 +1109,16 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             if applib.app_start(cpus[1] if cpus else -1, 0) != 0:
                 raise RuntimeError("app_start failed")
             try:
-                for _ in range(K):
-                    arr = next_set()
+                if pipelined:
+                    ns.rx_submit_mbufs(next_set(), B)
+                for k in range(K):
                     a0 = time.perf_counter()
-                    ns.rx_burst_mbufs(arr, B)
+                    if pipelined:
+                        if k + 1 < K:
+                            ns.rx_submit_mbufs(next_set(), B)
+                        ns.rx_complete_mbufs()
+                    else:
+                        ns.rx_burst_mbufs(next_set(), B)
                     ov_rx.append(time.perf_counter() - a0)
                     ov_ph.append(ns.last_burst_phases())
                     ov_cp.append(int(ns.stat(6)))
@@ -1128,8 +1150,11 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         cpus=list(cpus) if cpus else None,
                         note="application thread draining while the protocol thread runs "
                              "the bursts" + ("; the two threads on the lcores above" if cpus else
-                                             "; threads not pinned"))
+                                             "; threads not pinned")
+                             + ("; pipelined: burst k+1 submitted before burst k is delivered "
+                                "(nstack_rx_submit / nstack_rx_complete)" if pipelined else ""))
         res["overlapped"] = overlapped(pair)
+        res["overlapped_pipelined"] = overlapped(pair, pipelined=True)
         res["overlapped_unpinned"] = overlapped(None, unpin=True)
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
@@ -1451,7 +1476,10 @@ def _sock_summary(s):
                pooled_mpps=_g(s, "pooled_payload", "mpps"),
                d2h_ms=_g(s, "rx_burst_phases_ms", "d2h"),
                app_lock_wait_ms=_g(s, "overlapped", "app_ms_per_burst", "lock_wait"),
-               received_equal=_g(s, "overlapped", "received_equal"))
+               received_equal=_g(s, "overlapped", "received_equal"),
+               pipelined_mpps=_g(s, "pipelined", "mpps"),
+               overlapped_pipelined_mpps=_g(s, "overlapped_pipelined", "mpps"),
+               pipelined_received_equal=_g(s, "overlapped_pipelined", "received_equal"))
     return {k: v for k, v in out.items() if v is not None}
 
 
@@ -1486,7 +1514,8 @@ def compact_line(full, limit=LINE_MAX):
     if "per_rank" in full:
         pr = full["per_rank"] or []
         ms = [p["ms_per_step"] for p in pr]
-        out["ranks"] = dict(n=len(pr), ms_per_step_max=max(ms) if ms else None,
+        out["ranks"] = dict(n=len(pr), rccl_nranks=full.get("rccl_nranks"),
+                            ms_per_step_max=max(ms) if ms else None,
                             ms_per_step_min=min(ms) if ms else None,
                             frames_min=min((p["frames"] for p in pr), default=None),
                             frames_max=max((p["frames"] for p in pr), default=None),
@@ -1522,6 +1551,67 @@ def compact_line(full, limit=LINE_MAX):
             out.pop(drop)
             out.setdefault("dropped", []).append(drop)
     return out
+
+
+def build_line(names, results, steps, warmup, ramp_ms, world, ndev, collective, rccl_nranks=None,
+               ceiling=None, cfg1=None, sock=None):
+    """rank 0: the full result line (before compact_line) from the workloads'
+    results; the first workload is the headline.  rccl_nranks: the rank count
+    the RCCL communicator itself reports (rxg_group_size), None without one"""
+    head = results[names[0]]
+    line = {
+        "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
+        "value": round(head["mpps"], 2),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ramp_ms": ramp_ms,
+        "ms_per_step": round(head["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (deterministic counter-based pktgen, generated in HBM; cfg1 "
+                "through a pcap file)",
+        "config": {"workload": f"{names[0]}: {head['desc']}",
+                   "frames_per_step": head["frames_per_step"], "flows": head["nflows"],
+                   "parallelism": f"rss-split x{world}" if world > 1 else "1 GPU",
+                   "collective": collective,
+                   # ranks time-slicing one GPU (a rehearsal of the N-rank logic on a
+                   # one-GPU box): their step times measure the sharing, not the kernels
+                   "ranks_share_gpus": bool(world > max(ndev, 1))},
+        "gb_per_s": round(head["gbps"], 2),
+        "roofline": head["roofline"],
+        "cpu_baseline": head.get("cpu_baseline"),
+        "parity": head["parity"],
+        "digest": head["digest"],
+        "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
+        "counts_ok": head["counts_ok"],
+        "counts_match": head["counts_match"],
+        "hbm_read_ceiling_gbs": ceiling,
+        "librxgpu_sha256": lib_sha256()[:16],
+    }
+    if world > 1:
+        line["rccl_nranks"] = rccl_nranks
+        line["allreduce_ms"] = head["allreduce_ms"]
+        line["allreduce_bytes"] = head["allreduce_bytes"]
+        line["per_rank"] = head["per_rank"]
+    if "verdict8" in head:
+        line["verdict8"] = head["verdict8"]
+    if "tx_cksum" in head:
+        line["tx_cksum"] = head["tx_cksum"]
+    if "e2e_pcie" in head:
+        line["e2e_pcie"] = head["e2e_pcie"]
+        line["pcie_peaks"] = head["pcie_peaks"]
+    if cfg1:
+        line["cfg1"] = cfg1
+    if sock:
+        line["socket_api"] = sock
+    for nm in names[1:]:
+        r = results[nm]
+        line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+    return line
 
 
 def main():
@@ -1612,6 +1702,7 @@ def main():
         local = local % max(ndev, 1)
     group = nccl_group = None
     collective = None
+    rccl_nranks = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -1623,6 +1714,8 @@ def main():
                 torch.distributed.broadcast_object_list(obj, src=0)
                 stage(rank, "rxg_group_open (RCCL communicator)")
                 group = R.Group(local, world, rank, obj[0])
+                rccl_nranks = group.size()[0]
+                log(f"rank {rank}: RCCL communicator reports {rccl_nranks} ranks")
                 collective = "rccl (rxg_group_open / rxg_counts_allreduce, C ABI)"
             except Exception as e:  # reported in the line, never silent
                 log(f"rank {rank}: rxg_group_open failed ({e}); using torch.distributed nccl")
@@ -1701,57 +1794,8 @@ def main():
         sum(("verdict8" in r and (not r["verdict8"]["equals_projection"]
                                   or r["verdict8"]["digest_ok"] is False)) for r in results.values())
     if rank == 0:
-        line = {
-            "metric": "Mpps (device-resident rx parse+cksum+classify, 64 B frames)",
-            "value": round(head["mpps"], 2),
-            "unit": "Mpps",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ramp_ms": a.ramp_ms,
-            "ms_per_step": round(head["ms_per_step"], 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (deterministic counter-based pktgen, generated in HBM; cfg1 "
-                    "through a pcap file)",
-            "config": {"workload": f"{names[0]}: {head['desc']}",
-                       "frames_per_step": head["frames_per_step"], "flows": head["nflows"],
-                       "parallelism": f"rss-split x{world}" if world > 1 else "1 GPU",
-                       "collective": collective,
-                       # ranks time-slicing one GPU (a rehearsal of the N-rank logic on a
-                       # one-GPU box): their step times measure the sharing, not the kernels
-                       "ranks_share_gpus": bool(world > max(ndev, 1))},
-            "gb_per_s": round(head["gbps"], 2),
-            "roofline": head["roofline"],
-            "cpu_baseline": head.get("cpu_baseline"),
-            "parity": head["parity"],
-            "digest": head["digest"],
-            "kernel_ms_avg": round(head["kernel_ms_avg"], 4),
-            "counts_ok": head["counts_ok"],
-            "counts_match": head["counts_match"],
-            "hbm_read_ceiling_gbs": ceiling,
-            "librxgpu_sha256": lib_sha256()[:16],
-        }
-        if world > 1:
-            line["allreduce_ms"] = head["allreduce_ms"]
-            line["allreduce_bytes"] = head["allreduce_bytes"]
-            line["per_rank"] = head["per_rank"]
-        if "verdict8" in head:
-            line["verdict8"] = head["verdict8"]
-        if "tx_cksum" in head:
-            line["tx_cksum"] = head["tx_cksum"]
-        if "e2e_pcie" in head:
-            line["e2e_pcie"] = head["e2e_pcie"]
-            line["pcie_peaks"] = head["pcie_peaks"]
-        if cfg1:
-            line["cfg1"] = cfg1
-        if sock:
-            line["socket_api"] = sock
-        for nm in names[1:]:
-            r = results[nm]
-            line[nm] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+        line = build_line(names, results, a.steps, a.warmup, a.ramp_ms, world, ndev, collective,
+                          rccl_nranks, ceiling, cfg1, sock)
         # stdout: the compact line (the driver parses a bounded tail of
         # stdout); every measured detail goes to the detail file
         path = write_detail(line)

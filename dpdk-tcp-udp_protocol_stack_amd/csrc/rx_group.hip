@@ -101,6 +101,17 @@ void rxg_group_close(rxg_group *g) {
     delete g;
 }
 
+int rxg_group_size(const rxg_group *g, uint32_t *nranks, uint32_t *rank) {
+    if (!g || !g->comm) return RXG_EINVAL;
+    int c = 0, r = 0; // what the communicator itself reports, not what was asked for
+    ncclResult_t e = ncclCommCount(g->comm, &c);
+    if (e == ncclSuccess) e = ncclCommUserRank(g->comm, &r);
+    if (e != ncclSuccess) return comm_error(e, g->comm, "ncclCommCount");
+    if (nranks) *nranks = (uint32_t)c;
+    if (rank) *rank = (uint32_t)r;
+    return RXG_OK;
+}
+
 int rxg_counts_allreduce(rxg_group *g, uint64_t *d_counts, uint32_t n, void *stream) {
     return rx_group_allreduce_u64(g, d_counts, n, (hipStream_t)stream);
 }

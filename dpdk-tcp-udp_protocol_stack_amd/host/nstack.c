@@ -589,6 +589,22 @@ static uint8_t g_local_mac[6];
 static const uint8_t k_default_arp_mac[6] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF}; /* netfamily.c:20 */
 static int g_burst_mutated;     /* the tcb list changed during this burst's delivery */
 static int g_rx_in_flight;      /* nstack_rx_burst waits for the GPU (g_lock released) */
+static uint32_t g_pend_n;      /* bursts nstack_rx_submit queued, not yet completed */
+struct rx_pend {
+    rxg_mbuf *const *m;
+    uint32_t n;
+    int *rc_out;
+    rxg_verdict *v_out;
+    rxg_verdict *v; /* the verdicts (the library's copy out lands here) */
+    uint32_t v_cap;
+    uint8_t *handled;
+    uint32_t h_cap;
+    rxg_delivery d;
+    uint64_t gen0;   /* g_snap_gen at the submit */
+    double lib_ms;   /* the submit's library time */
+};
+static struct rx_pend g_pend[RXG_DELIVER_DEPTH];
+static uint32_t g_pend_head; /* the oldest pending burst */
 /* The protocol thread's (rx / tx bursts) hold of the stack's lock.  No
  * application loop takes g_lock any more (drain_all and the receive calls
  * look blocks up under g_tab), so nothing has to step aside for it. */
@@ -859,6 +875,19 @@ int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
 }
 
 void nstack_fini(void) {
+    /* bursts submitted and never completed: waited for, not delivered */
+    while (g_pend_n && g_ctx) {
+        float ms[8];
+        (void)rxg_deliver_wait(g_ctx, &g_pend[g_pend_head].d, ms);
+        g_pend_head = (g_pend_head + 1) % RXG_DELIVER_DEPTH;
+        g_pend_n--;
+    }
+    g_pend_n = g_pend_head = 0;
+    for (uint32_t j = 0; j < RXG_DELIVER_DEPTH; j++) {
+        free(g_pend[j].v), free(g_pend[j].handled);
+        g_pend[j].v = NULL, g_pend[j].handled = NULL;
+        g_pend[j].v_cap = g_pend[j].h_cap = 0;
+    }
     reclaim();
     pthread_mutex_lock(&g_lock);
     /* unmap every block first (as nclose unregisters before its kill): an
@@ -2099,6 +2128,36 @@ int nstack_set_halves(uint32_t min_half) {
     return RXG_OK;
 }
 
+/* g_lock held: deliver one part of a burst the GPU has classified (`d`, its
+ * verdicts `v`), submitted when the lookups' snapshot generation was gen0 —
+ * the UDP batches, the sorted TCP connections, then the frame-by-frame rest;
+ * ph[3] += the three phases' times.  Returns the UDP datagrams delivered. */
+static int deliver_part(rxg_mbuf *const *m, uint32_t k, const rxg_verdict *v, uint8_t *handled,
+                        int *rco, rxg_delivery *d, uint64_t gen0, double ph[3]) {
+    int delivered = 0;
+    const double t1 = mono_ms();
+    g_burst_mutated = 0;
+    g_burst_stale = gen0 != g_snap_gen;
+    if (g_burst_stale) { /* (ids may name other blocks now) */
+        d->first = NULL, d->nseg = 0;
+        g_stale_parts++;
+    }
+    if (d->first) {
+        delivered += deliver_udp_batches(m, d->dgram, d->first, d->udp_payload, rxg_num_udp_ids(g_ctx));
+        g_udp_done = 1; /* the per-frame loop leaves UDP alone */
+    }
+    const double t2 = mono_ms();
+    memset(handled, 0, k);
+    if (d->nseg) deliver_tcp_sorted(d->seg, d->nseg, d->tcp_payload, d->tcp_payload_ref, m, handled, rco);
+    const double t3 = mono_ms();
+    delivered += deliver_burst(m, k, v, rco, handled);
+    g_udp_done = 0;
+    g_burst_stale = 0;
+    const double t4 = mono_ms();
+    ph[0] += t2 - t1, ph[1] += t3 - t2, ph[2] += t4 - t3;
+    return delivered;
+}
+
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
     t_proto = 1;
@@ -2111,7 +2170,7 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     const double t0 = mono_ms();
     /* one protocol thread (the reference's pkt_process lcore): a second
      * rx_burst while one waits for the GPU is refused */
-    int rc = g_ctx && !g_rx_in_flight ? RXG_OK : RXG_EINVAL;
+    int rc = g_ctx && !g_rx_in_flight && !g_pend_n ? RXG_OK : RXG_EINVAL;
     if (rc == RXG_OK && grow((void **)&s_v, &s_v_cap, n ? n : 1, sizeof(rxg_verdict)))
         rc = RXG_ENOMEM;
     if (rc == RXG_OK && grow((void **)&s_handled, &s_handled_cap, n ? n : 1, 1)) rc = RXG_ENOMEM;
@@ -2174,31 +2233,9 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
         proto_lock();
         if (rc == RXG_OK) rc = wrc;
         if (rc != RXG_OK) continue; /* (a submitted half is still waited for) */
-        const double t1 = mono_ms();
-        int *rco = rc_out ? rc_out + o : NULL;
-        g_burst_mutated = 0;
-        g_burst_stale = gen0 != g_snap_gen;
-        if (g_burst_stale) { /* (ids may name other blocks now) */
-            d[h].first = NULL, d[h].nseg = 0;
-            g_stale_parts++;
-        }
-        if (d[h].first) {
-            delivered += deliver_udp_batches(m + o, d[h].dgram, d[h].first, d[h].udp_payload,
-                                             rxg_num_udp_ids(g_ctx));
-            g_udp_done = 1; /* the per-frame loop leaves UDP alone */
-        }
-        const double t2 = mono_ms();
-        memset(s_handled + o, 0, k);
-        if (d[h].nseg)
-            deliver_tcp_sorted(d[h].seg, d[h].nseg, d[h].tcp_payload, d[h].tcp_payload_ref, m + o,
-                               s_handled + o, rco);
-        const double t3 = mono_ms();
-        delivered += deliver_burst(m + o, k, s_v + o, rco, s_handled + o);
-        g_udp_done = 0;
-        g_burst_stale = 0;
+        delivered += deliver_part(m + o, k, s_v + o, s_handled + o, rc_out ? rc_out + o : NULL,
+                                  &d[h], gen0, ph);
         done[h] = 1;
-        const double t4 = mono_ms();
-        ph[0] += t2 - t1, ph[1] += t3 - t2, ph[2] += t4 - t3;
     }
     g_rx_in_flight = 0;
     /* the first half delivered, the second not put through the GPU (a failed
@@ -2224,6 +2261,88 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
     if (done[0]) atomic_fetch_add_explicit(&g_deliveries, 1, memory_order_release);
     pthread_mutex_unlock(&g_lock);
     return rc == RXG_OK || partial ? delivered : rc;
+}
+
+/* ---- pipelined receive: one burst on the GPU while the last is delivered --
+ * The reference's protocol lcore takes a burst and runs every frame through
+ * udp_process / tcp_process before it takes the next (netfamily.c:147-200).
+ * nstack_rx_submit / nstack_rx_complete keep that order of delivery but let
+ * burst k+1 cross PCIe and go through K1/K3/K4 while burst k is delivered
+ * (the library's delivery sets, RXG_DELIVER_DEPTH).  A burst submitted before
+ * the previous one was delivered was classified against the lookups of its
+ * submit: when that delivery (a SYN, a last ACK) or a socket call moved a
+ * lookup, the burst is delivered frame by frame on the live lists
+ * (deliver_part's stale path), the reference's sequential outcome. */
+
+int nstack_rx_submit(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
+    if (!m && n) return RXG_EINVAL;
+    t_proto = 1;
+    if (!g_inplace) reclaim();
+    proto_lock();
+    pl_wait_free();
+    int rc = g_ctx && !g_rx_in_flight && g_pend_n < RXG_DELIVER_DEPTH ? RXG_OK : RXG_EINVAL;
+    struct rx_pend *p = &g_pend[(g_pend_head + g_pend_n) % RXG_DELIVER_DEPTH];
+    if (rc == RXG_OK && (grow((void **)&p->v, &p->v_cap, n ? n : 1, sizeof(rxg_verdict)) ||
+                         grow((void **)&p->handled, &p->h_cap, n ? n : 1, 1)))
+        rc = RXG_ENOMEM;
+    if (rc == RXG_OK) {
+        p->m = m, p->n = n, p->rc_out = rc_out, p->v_out = v_out;
+        p->gen0 = g_snap_gen;
+        const double a = mono_ms();
+        rc = rxg_deliver_submit(g_ctx, m, n, p->v, &p->d);
+        p->lib_ms = mono_ms() - a;
+        pl_note_submit(&p->d);
+        if (rc == RXG_OK) g_pend_n++;
+    }
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+int nstack_rx_pending(void) {
+    proto_lock();
+    const int k = (int)g_pend_n;
+    pthread_mutex_unlock(&g_lock);
+    return k;
+}
+
+int nstack_rx_complete(void) {
+    t_proto = 1;
+    const double t0 = mono_ms();
+    proto_lock();
+    if (!g_pend_n || !g_ctx) {
+        pthread_mutex_unlock(&g_lock);
+        return RXG_EINVAL;
+    }
+    struct rx_pend *p = &g_pend[g_pend_head];
+    pthread_mutex_unlock(&g_lock);
+    /* what the application threads let go of is freed while the burst (and
+     * the one submitted after it) is on the GPU */
+    reclaim();
+    float gms[8] = {0};
+    const double a = mono_ms();
+    const int wrc = rxg_deliver_wait(g_ctx, &p->d, gms);
+    const double lib_ms = p->lib_ms + (mono_ms() - a);
+    proto_lock();
+    g_pend_head = (g_pend_head + 1) % RXG_DELIVER_DEPTH;
+    g_pend_n--;
+    if (wrc != RXG_OK) { /* the burst is not delivered: the caller may pass its frames again */
+        pthread_mutex_unlock(&g_lock);
+        return wrc;
+    }
+    double ph[3] = {0, 0, 0};
+    const int delivered = deliver_part(p->m, p->n, p->v, p->handled, p->rc_out, &p->d, p->gen0, ph);
+    if (p->v_out) memcpy(p->v_out, p->v, (size_t)p->n * sizeof(rxg_verdict));
+    for (int j = 0; j < 5; j++) g_phase_ms[j] = gms[j];
+    g_phase_ms[5] = (float)lib_ms;
+    g_phase_ms[6] = (float)ph[0];
+    g_phase_ms[7] = (float)ph[1];
+    g_phase_ms[8] = (float)ph[2];
+    g_phase_ms[9] = (float)(mono_ms() - t0); /* this call (the submit is the caller's) */
+    g_phase_ms[10] = (float)p->d.nseg;
+    g_phase_ms[11] = (float)p->d.ndgram;
+    atomic_fetch_add_explicit(&g_deliveries, 1, memory_order_release);
+    pthread_mutex_unlock(&g_lock);
+    return delivered;
 }
 
 int nstack_last_burst_phases(float ms[12]) {

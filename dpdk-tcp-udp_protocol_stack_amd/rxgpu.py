@@ -220,6 +220,7 @@ _gather_dev = _sig("rxg_gather_dev", _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u32, 
 _group_id = _sig("rxg_group_id", _i32, _vp)
 _group_open = _sig("rxg_group_open", _i32, C.POINTER(_vp), _i32, _u32, _u32, _vp)
 _group_close = _sig("rxg_group_close", None, _vp)
+_group_size = _sig("rxg_group_size", _i32, _vp, C.POINTER(_u32), C.POINTER(_u32))
 _counts_allreduce = _sig("rxg_counts_allreduce", _i32, _vp, _vp, _u32, _vp)
 _ctx_counts_allreduce = _sig("rxg_ctx_counts_allreduce", _i32, _vp, _vp)
 PIPE_DEPTH = 3
@@ -239,7 +240,7 @@ EXPORTED = ["rxg_open", "rxg_close", "rxg_strerror", "rxg_last_hip_error", "rxg_
             "rxg_pcap_open", "rxg_pcap_close", "rxg_pcap_rewind", "rxg_pcap_read_burst",
             "rxg_pcap_write", "rxg_tx_cksum_dev", "rxg_tx_cksum", "rxg_rss_split",
             "rxg_rss_split_dev", "rxg_gather_dev", "rxg_group_id", "rxg_group_open",
-            "rxg_group_close", "rxg_counts_allreduce", "rxg_ctx_counts_allreduce"]
+            "rxg_group_close", "rxg_group_size", "rxg_counts_allreduce", "rxg_ctx_counts_allreduce"]
 
 
 class RxgError(RuntimeError):
@@ -664,6 +665,12 @@ class Group:
         _check(_group_open(C.byref(h), device, nranks, rank, buf), "rxg_group_open")
         self._h = h
 
+    def size(self):
+        """rxg_group_size: (nranks, rank) as the RCCL communicator reports them"""
+        nr, rk = C.c_uint32(), C.c_uint32()
+        _check(_group_size(self._h, C.byref(nr), C.byref(rk)), "rxg_group_size")
+        return nr.value, rk.value
+
     def allreduce(self, d_counts, n: int, stream=None):
         """in-place sum of a device u64[n] vector over the ranks, async on stream"""
         p = d_counts if isinstance(d_counts, int) else d_counts.data_ptr()
@@ -757,6 +764,9 @@ class NStack:
                    ("nsendto", ssz, [_i32, _vp, C.c_size_t, _i32, _vp, _u32]),
                    ("nclose", _i32, [_i32]),
                    ("nstack_rx_burst", _i32, [_vp, _u32, _vp, _vp]),
+                   ("nstack_rx_submit", _i32, [_vp, _u32, _vp, _vp]),
+                   ("nstack_rx_complete", _i32, []),
+                   ("nstack_rx_pending", _i32, []),
                    ("nstack_deliver", _i32, [_vp, _u32, _vp, _u64, _vp]),
                    ("nstack_tcb_add", _i32, [_u32, _u32, _u16, _u16, _i32]),
                    ("nstack_flows", _i32, [_vp, _u32, _vp, _vp, _u32, _vp, _vp]),
@@ -957,6 +967,46 @@ class NStack:
         if r < 0:
             _check(r, "nstack_rx_burst")
         return r, rcs, v
+
+    def rx_submit(self, frames: list[bytes]):
+        """nstack_rx_submit: the burst goes to the GPU; rx_complete delivers it"""
+        arr, keep = self.mbufs(frames)
+        rcs = np.zeros(len(frames), np.int32)
+        v = np.zeros(len(frames), VERDICT_DTYPE)
+        r = self.lib.nstack_rx_submit(C.cast(arr, _vp), len(frames), _ptr(rcs), _ptr(v))
+        if r < 0:
+            _check(r, "nstack_rx_submit")
+        if not hasattr(self, "_pend"):
+            self._pend = []
+        self._pend.append((arr, len(frames), keep, rcs, v))
+        return r
+
+    def rx_complete(self):
+        """nstack_rx_complete: deliver the oldest submitted burst: (delivered, rcs, verdicts)
+        of that burst, as rx_burst returns them"""
+        r = self.lib.nstack_rx_complete()
+        arr, n, keep, rcs, v = self._pend.pop(0)
+        self._let_go(arr, n, keep)
+        if r < 0:
+            _check(r, "nstack_rx_complete")
+        return r, rcs, v
+
+    def rx_pending(self) -> int:
+        return int(self.lib.nstack_rx_pending())
+
+    def rx_submit_mbufs(self, arr, n: int, rcs: np.ndarray | None = None) -> int:
+        """nstack_rx_submit over prebuilt descriptors (mbufs_over); keep arr
+        (and rcs) alive until rx_complete_mbufs"""
+        r = self.lib.nstack_rx_submit(C.cast(arr, _vp), n, _ptr(rcs), None)
+        if r < 0:
+            _check(r, "nstack_rx_submit")
+        return r
+
+    def rx_complete_mbufs(self) -> int:
+        r = self.lib.nstack_rx_complete()
+        if r < 0:
+            _check(r, "nstack_rx_complete")
+        return r
 
     def _let_go(self, arr, n, keep):
         """after a burst call: in place, the frames stay alive while the stack

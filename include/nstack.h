@@ -92,6 +92,26 @@ int nclose(int fd);
  * it (a second concurrent nstack_rx_burst gets RXG_EINVAL). */
 int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 
+/* Pipelined receive: the same delivery as nstack_rx_burst, with the next
+ * burst on the GPU (copy in, K1/K3/K4, copy out) while the protocol thread
+ * delivers the previous one.  nstack_rx_submit queues a burst and returns at
+ * once (RXG_DELIVER_DEPTH = 2 bursts submitted and not completed at most;
+ * RXG_EINVAL past that, or while an nstack_rx_burst runs); nstack_rx_complete
+ * waits for the oldest submitted burst and delivers it, frame order and
+ * outcomes as nstack_rx_burst's, and returns its UDP datagrams delivered (or
+ * a negative RXG_E* code: the burst was not delivered, RXG_EINVAL when none
+ * is pending).  A burst's frames, rc_out and v_out must stay valid until its
+ * complete.  A burst classified before the previous one was delivered is
+ * delivered frame by frame on the live lists when that delivery or a socket
+ * call changed a lookup (the reference's sequential outcome, netfamily.c:
+ * 147-200 taking burst k+1 only after burst k).  The loop:
+ *     nstack_rx_submit(b0); for (k...) { nstack_rx_submit(b[k+1]); nstack_rx_complete(); }
+ * nstack_rx_pending: bursts submitted and not completed.  nstack_rx_burst is
+ * refused while any is pending; nstack_fini waits for them and drops them. */
+int nstack_rx_submit(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
+int nstack_rx_complete(void);
+int nstack_rx_pending(void);
+
 /* Delivery half only: apply verdicts computed by rxg_* to the frames (UDP ->
  * socket receive rings, TCP -> state machine).  Verdict flow ids are the
  * blocks' stable ids (nstack_flow_ids).  `gen` = the generation nstack_flows

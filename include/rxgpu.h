@@ -614,6 +614,9 @@ int rxg_group_id(uint8_t id[RXG_GROUP_ID_BYTES]);
 int rxg_group_open(rxg_group **g, int device, uint32_t nranks, uint32_t rank,
                    const uint8_t id[RXG_GROUP_ID_BYTES]);
 void rxg_group_close(rxg_group *g);
+/* The communicator's size and this process's rank as RCCL reports them
+ * (ncclCommCount / ncclCommUserRank); either pointer may be NULL. */
+int rxg_group_size(const rxg_group *g, uint32_t *nranks, uint32_t *rank);
 /* Sum of a device u64 count vector over the ranks, in place, asynchronous on
  * `stream` (every rank must call it with the same n). */
 int rxg_counts_allreduce(rxg_group *g, uint64_t *d_counts, uint32_t n, void *stream);

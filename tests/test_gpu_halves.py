@@ -14,7 +14,10 @@ tcp.c:373-415), so the halves must not change anything an application sees:
     (SYN) that the second half's segments complete (ACK) and use (data), so
     the second half's verdicts are stale by the time it is delivered, against
     oracle/ref_stack.c frame by frame: every return code, accepted
-    connection, nrecv / nrecvfrom result and what the application drains."""
+    connection, nrecv / nrecvfrom result and what the application drains;
+  - the pipelined pair (nstack_rx_submit / nstack_rx_complete): whole bursts,
+    burst k+1 on the GPU while burst k is delivered, against the same oracle
+    run sequentially, and with an application thread draining beside it."""
 import numpy as np
 import pytest
 
@@ -196,6 +199,84 @@ def test_socket_layer_halves_match_oracle(torch_dev):
         st.ns.fini()
 
 
+def _mixed_frames(rng, st, n, b, syn):
+    """n frames to the stack of `st`: data to its established connections and
+    datagrams to its sockets; with syn, 60 SYNs to the listener (burst b)
+    whose ACK and first data come in the NEXT burst (made by _syn_followups)"""
+    frames = []
+    for _ in range(n - (60 if syn else 0)):
+        if rng.random() < 0.5:
+            frames.append(_est_seg(rng, *st.est[int(rng.integers(len(st.est)))]))
+        else:
+            k = int(rng.integers(48))  # 8 ports without a socket
+            pl = bytes(rng.integers(0, 256, int(rng.choice([0, 5, 100, 1000])), np.uint8))
+            frames.append(F.udp_frame(f"10.5.{k}.1", 7000 + k, L, 30000 + k, pl))
+    if syn:
+        for i in range(60):
+            frames.insert(int(rng.integers(0, len(frames))),
+                          F.tcp_frame(f"10.251.{b}.{i + 1}", 62000 + i, L, 9999, b"", flags=0x02,
+                                      seq=2000 + i))
+    return frames
+
+
+def _syn_followups(rng, frames, b):
+    for i in range(60):
+        cip, cport = f"10.251.{b}.{i + 1}", 62000 + i
+        frames.insert(int(rng.integers(0, len(frames) // 2)), F.tcp_frame(cip, cport, L, 9999, b"", flags=0x10))
+        frames.append(F.tcp_frame(cip, cport, L, 9999, b"piped %d" % i, flags=0x18))
+    return frames
+
+
+def test_socket_layer_pipelined_match_oracle(torch_dev):
+    """nstack_rx_submit / nstack_rx_complete with burst k+1 on the GPU while
+    burst k is delivered: every return code of every burst equals the oracle's
+    sequential run (burst k wholly before burst k+1, netfamily.c:147-200).
+    Bursts 1 and 3 carry SYNs whose ACK and data arrive in bursts 2 and 4,
+    which were classified before those SYNs were delivered: they must be
+    delivered frame by frame on the live lists (stat 5, a stale part each);
+    the others go through the per-connection and per-socket batches."""
+    rng = np.random.default_rng(35)
+    st = Stacks(2000)
+    st.ns.set_halves(0)
+    try:
+        bursts = []
+        for b in range(6):
+            fr = _mixed_frames(rng, st, 6000, b, syn=b in (1, 3))
+            if b in (2, 4):
+                fr = _syn_followups(rng, fr, b - 1)
+            bursts.append(fr)
+        stale0 = st.ns.stat(5)
+        st.ns.rx_submit(bursts[0])
+        stale = []
+        for b in range(6):
+            if b + 1 < 6:
+                st.ns.rx_submit(bursts[b + 1])
+                assert st.ns.rx_pending() == 2
+                with pytest.raises(R.RxgError):  # both delivery sets in flight
+                    st.ns.rx_submit(bursts[b + 1][:10])
+                with pytest.raises(R.RxgError):  # the one-shot call is refused meanwhile
+                    st.ns.rx_burst(bursts[b][:10])
+            s0 = st.ns.stat(5)
+            want = [st.os.rx(f) for f in bursts[b]]
+            n, rcs, _ = st.ns.rx_complete()
+            bad = [(i, int(rcs[i]), want[i]) for i in range(len(want)) if rcs[i] != want[i]]
+            assert not bad, (b, bad[:10])
+            stale.append(st.ns.stat(5) - s0)
+            st.accept_all()
+            st.read_all(int(rng.choice([7, 4096])))
+            buf = np.zeros(65536, np.uint8)
+            assert st.ns.drain_all(buf) == st.os.drain_all(buf), b
+        assert st.ns.rx_pending() == 0
+        assert st.ns.lib.nstack_rx_complete() == -22  # RXG_EINVAL: nothing pending
+        assert stale == [0, 0, 1, 0, 1, 0], stale
+        assert st.ns.stat(5) == stale0 + 2
+        assert len(st.conns) >= 100
+        # bursts left pending are dropped by fini (waited for, not delivered)
+        st.ns.rx_submit(bursts[0][:100])
+    finally:
+        st.ns.fini()
+
+
 def _split_model(lens, cap):
     """drain_all's count through nrecv's split path (common.c:483-496): a
     fragment longer than cap gives cap bytes, re-queues the rest at the tail
@@ -256,7 +337,7 @@ def _fnv_sum(payloads):
         return int(h[lens > 0].sum(dtype=np.uint64))
 
 
-@pytest.mark.parametrize("mode", ["pooled", "inplace"])
+@pytest.mark.parametrize("mode", ["pooled", "inplace", "inplace_pipelined", "pooled_pipelined"])
 def test_two_threads_receive_every_byte(torch_dev, mode):
     """The reference's arrangement: the protocol loop on one thread
     (nstack_rx_burst), the application on another draining every socket
@@ -271,7 +352,7 @@ def test_two_threads_receive_every_byte(torch_dev, mode):
     import threading
     ns = R.NStack(0, max_burst=4096, max_bytes=4096 * 1536)
     try:
-        if mode == "inplace":
+        if mode.startswith("inplace"):
             ns.set_rx_inplace(True)
         conns = []
         for k in range(512):
@@ -310,10 +391,19 @@ def test_two_threads_receive_every_byte(torch_dev, mode):
         th = threading.Thread(target=app)
         th.start()
         try:
-            for arr, n, _keep, _buf in bursts:
-                assert ns.rx_burst_mbufs(arr, n) >= 0
-                if mode == "inplace":
-                    ns.mbufs_put(arr, n)  # the caller's reference
+            if mode.endswith("pipelined"):  # burst k+1 on the GPU while burst k is delivered
+                ns.rx_submit_mbufs(bursts[0][0], bursts[0][1])
+                for k, (arr, n, _keep, _buf) in enumerate(bursts):
+                    if k + 1 < len(bursts):
+                        ns.rx_submit_mbufs(bursts[k + 1][0], bursts[k + 1][1])
+                    assert ns.rx_complete_mbufs() >= 0
+                    if mode.startswith("inplace"):
+                        ns.mbufs_put(arr, n)
+            else:
+                for arr, n, _keep, _buf in bursts:
+                    assert ns.rx_burst_mbufs(arr, n) >= 0
+                    if mode == "inplace":
+                        ns.mbufs_put(arr, n)  # the caller's reference
         finally:
             stop.set()
             th.join()
@@ -321,7 +411,7 @@ def test_two_threads_receive_every_byte(torch_dev, mode):
         assert (got[0], got[1]) == (want_items, want_bytes)
         assert got[2] == want_sum
         assert ns.stat(7) == 0  # no batch left holding a payload buffer
-        if mode == "inplace":  # every hold on a frame let go, exactly once
+        if mode.startswith("inplace"):  # every hold on a frame let go, exactly once
             for _arr, _n, keep, _buf in bursts:
                 assert all(keep[i].refcnt == 0 for i in range(len(keep)))
             assert ns.stat(6) == c0  # nothing copied

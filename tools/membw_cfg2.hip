@@ -23,7 +23,8 @@
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int MODE, int U> // MODE 0 = R, 1 = RD, 2 = RDW (nt store), 3 = RDW (plain store),
-                           // 4 = RDW8 (8-B nt store), 5 = RDW4 (4-B nt store)
+                           // 4 = RDW8 (8-B nt store), 5 = RDW4 (4-B nt store),
+                           // 6 = RDW (sc1 write-through store)
 __global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
                                               const unsigned *__restrict__ off,
                                               const unsigned short *__restrict__ len, size_t n,
@@ -62,6 +63,9 @@ __global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
                                                 reinterpret_cast<unsigned long long *>(out) + f);
                 else if (MODE == 5)
                     __builtin_nontemporal_store(r.x ^ r.z, reinterpret_cast<unsigned *>(out) + f);
+                else if (MODE == 6)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(out + f), "v"(r)
+                                 : "memory");
                 else
                     out[f] = r;
             } else {
@@ -111,6 +115,15 @@ int main() {
     // warm the clocks
     for (int i = 0; i < 200; ++i) hipLaunchKernelGGL((k_cfg2<2, 2>), dim3(cu * 4), dim3(256), 0, 0, fr, off, len, n, out, sink);
     CHK(hipDeviceSynchronize());
+    // store flavours at the lane kernel's 2 blocks/CU, interleaved, 3 rounds (r06)
+    for (int round = 0; round < 3; ++round)
+        for (int bpc : {2, 3}) {
+            run<1, 2>("RD", fr, off, len, n, out, sink, cu, bpc, r + d);
+            run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            run<6, 2>("RDWs", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            run<3, 2>("RDWp", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            run<4, 2>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
+        }
     for (int bpc : {2, 3, 4, 6, 8}) {
         run<0, 1>("R", fr, off, len, n, out, sink, cu, bpc, r);
         run<0, 2>("R", fr, off, len, n, out, sink, cu, bpc, r);

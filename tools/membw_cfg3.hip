@@ -209,6 +209,58 @@ __global__ __launch_bounds__(256) void k_slotrun(const u32x4 *__restrict__ in, s
     }
 }
 
+// time-batched verdict writes: a block owns a contiguous range of slots
+// (CONTIG) or strided 32-slot tiles, keeps the verdicts of T consecutive trips
+// in LDS and writes them out together (T * 512 B; T = 1: every trip).  If the
+// cost of the sparse verdict stream is in the memory controller's read/write
+// turnarounds, writes bunched in time across the chip should cost less
+template <int T, int SM, bool CONTIG>
+__global__ __launch_bounds__(256) void k_slotbuf(const u32x4 *__restrict__ in, size_t nslots,
+                                                 u32x4 *__restrict__ out) {
+    __shared__ u32x4 buf[T * 32];
+    const unsigned gl = threadIdx.x & 7u, grp = threadIdx.x >> 3;
+    const size_t ntiles = nslots / 32;
+    const size_t per = (ntiles + gridDim.x - 1) / gridDim.x; // CONTIG: tiles per block
+    const size_t t0 = CONTIG ? blockIdx.x * per : blockIdx.x;
+    const size_t t1 = CONTIG ? (t0 + per < ntiles ? t0 + per : ntiles) : ntiles;
+    const size_t tstep = CONTIG ? 1 : gridDim.x;
+    unsigned k = 0;
+    size_t first = t0; // first tile of the batch in LDS (CONTIG)
+    for (size_t t = t0; t < t1; t += tstep) {
+        const size_t f = t * 32 + grp;
+        const u32x4 *p = in + f * 96;
+        u32x4 v[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const unsigned c = q * 8 + gl;
+            v[q] = c < 94 ? ldnt(p + c) : u32x4{0, 0, 0, 0};
+        }
+        unsigned acc = 0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc += csum(v[q]);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (T == 1) {
+            if (gl == 0) st16<SM>(out + f, u32x4{acc, (unsigned)f, 0, 0});
+            continue;
+        }
+        if (gl == 0) buf[k * 32 + grp] = u32x4{acc, (unsigned)f, 0, 0};
+        if (++k == T || t + tstep >= t1) {
+            __syncthreads();
+            const unsigned m = k * 32; // verdicts in the batch
+            for (unsigned i = threadIdx.x; i < m; i += 256) {
+                // CONTIG: one contiguous run; else tile i/32 of the batch is t - (k-1-i/32) * tstep
+                const size_t tt = CONTIG ? first + i / 32 : t - (size_t)(k - 1 - i / 32) * tstep;
+                st16<SM>(out + tt * 32 + (i & 31u), buf[i]);
+            }
+            __syncthreads();
+            k = 0;
+            first = t + tstep;
+        }
+    }
+}
+
 // the plain grid-stride read plus one 16-B non-temporal store per 96 chunks
 // (per 1536-B slot), issued by the lane that reads the slot's first chunk
 __global__ __launch_bounds__(256) void k_stream_st(const u32x4 *__restrict__ in, size_t n16,
@@ -314,23 +366,7 @@ int main() {
     int cu = 0;
     CHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
     const int reps = 20;
-    // in-flight sweep: the plain read with 1/2/4/8 loads per lane and the G=8
-    // slot shape at 1-8 blocks per CU, full and half passes
-    for (int round = 0; round < 2; ++round) {
-        for (int bpc : {1, 2, 3, 4, 6, 8}) {
-            const int g = cu * bpc;
-            float ms;
-#define SU(U)                                                                                      \
-    ms = timeit([&] { k_stream_u<U><<<g, 256>>>(in, bytes / 16, sink); }, reps);                   \
-    printf("s%d bpc=%d stream U=%d      %.4f ms %7.0f GB/s (read)\n", round, bpc, U, ms, bytes / ms / 1e6);
-            SU(1) SU(2) SU(4) SU(8)
-#undef SU
-            ms = timeit([&] { k_slotg8<<<g, 256>>>(in, nslots, out); }, reps);
-            printf("s%d bpc=%d slotg8          %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
-            ms = timeit([&] { k_slotg8_half<<<g, 256>>>(in, nslots, out); }, reps);
-            printf("s%d bpc=%d slotg8 half     %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
-        }
-    }
+    // (the in-flight sweep of r06b: profiles/r06b/membw_cfg3_r06b.txt)
     // the decomposition, interleaved, 3 rounds: which component of the slot
     // shape costs the 0.912 -> 1.042 ms
     for (int round = 0; round < 3; ++round) {
@@ -354,24 +390,17 @@ int main() {
             D("run64 st nt 1KiB/run", (k_slotrun<0, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
             D("run64 st plain 1KiB/run", (k_slotrun<1, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
             D("run64 st sc1 1KiB/run", (k_slotrun<2, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf strided T1 sc1", (k_slotbuf<1, 2, false><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf strided T8 sc1", (k_slotbuf<8, 2, false><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf strided T32 sc1", (k_slotbuf<32, 2, false><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf contig T1 sc1", (k_slotbuf<1, 2, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf contig T8 sc1", (k_slotbuf<8, 2, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf contig T32 sc1", (k_slotbuf<32, 2, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf contig T32 nt", (k_slotbuf<32, 0, true><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
+            D("buf strided T32 nt", (k_slotbuf<32, 0, false><<<g, 256>>>(in, nslots, out)), nslots * 1504.0)
 #undef D
         }
     }
-    for (int round = 0; round < 3; ++round) {
-        for (int bpc : {4, 8}) {
-            const int g = cu * bpc;
-            float ms = timeit([&] { k_stream<<<g, 256>>>(in, bytes / 16, sink); }, reps);
-            printf("r%d bpc=%d stream          %.4f ms %7.0f GB/s (read)\n", round, bpc, ms,
-                   bytes / ms / 1e6);
-            ms = timeit([&] { k_slotg8<<<g, 256>>>(in, nslots, out); }, reps);
-            printf("r%d bpc=%d slotg8          %.4f ms %7.0f GB/s (alg)\n", round, bpc, ms, alg / ms / 1e6);
-#define W(F, P)                                                                                    \
-    ms = timeit([&] { k_wave<F, P><<<g, 256>>>(in, nslots, out); }, reps);                         \
-    printf("r%d bpc=%d wave F=%d pipe=%d   %.4f ms %7.0f GB/s (alg)\n", round, bpc, F, (int)P, ms,   \
-           alg / ms / 1e6);
-            W(2, false) W(2, true) W(4, false) W(4, true) W(8, false)
-#undef W
-        }
-    }
+    // (the wave-contiguous shapes: profiles/r05c, r06c)
     return 0;
 }
