@@ -1069,6 +1069,9 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # and read (the first submit is outside the clock, as a loop's first
         # burst would be in flight already)
         res["pipelined"] = ab_run(pipelined=True)
+        ns.set_rx_inplace(False)
+        res["pooled_pipelined"] = ab_run(pipelined=True)
+        ns.set_rx_inplace(True)
         # A/B: each burst as two halves, both on the GPU at once
         # (nstack_set_halves; off by default)
         ns.set_halves(B // 2)
@@ -1155,6 +1158,11 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                                 "(nstack_rx_submit / nstack_rx_complete)" if pipelined else ""))
         res["overlapped"] = overlapped(pair)
         res["overlapped_pipelined"] = overlapped(pair, pipelined=True)
+        # the in-place vs pooled-payload A/B in the two-thread forms too
+        ns.set_rx_inplace(False)
+        res["overlapped_pooled"] = overlapped(pair)
+        res["overlapped_pipelined_pooled"] = overlapped(pair, pipelined=True)
+        ns.set_rx_inplace(True)
         res["overlapped_unpinned"] = overlapped(None, unpin=True)
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
@@ -1478,6 +1486,9 @@ def _sock_summary(s):
                app_lock_wait_ms=_g(s, "overlapped", "app_ms_per_burst", "lock_wait"),
                received_equal=_g(s, "overlapped", "received_equal"),
                pipelined_mpps=_g(s, "pipelined", "mpps"),
+               pooled_pipelined_mpps=_g(s, "pooled_pipelined", "mpps"),
+               overlapped_pooled_mpps=_g(s, "overlapped_pooled", "mpps"),
+               overlapped_pipelined_pooled_mpps=_g(s, "overlapped_pipelined_pooled", "mpps"),
                overlapped_pipelined_mpps=_g(s, "overlapped_pipelined", "mpps"),
                pipelined_received_equal=_g(s, "overlapped_pipelined", "received_equal"))
     return {k: v for k, v in out.items() if v is not None}

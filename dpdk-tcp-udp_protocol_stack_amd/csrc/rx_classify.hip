@@ -178,7 +178,8 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
                                               int32_t s0, const rx_ft_dev &ft,
                                               uint4 *__restrict__ out,
                                               unsigned long long *__restrict__ counts,
-                                              uint32_t *hist, uint32_t lds_bins) {
+                                              uint32_t *hist, uint32_t lds_bins,
+                                              uint4 *vb = nullptr) {
     constexpr int32_t STEP = 16 * G;
     // ---- phase C: parse + checksum per frame
     uint32_t cls[FPG], ck[FPG], stored[FPG], tl[FPG], dgl[FPG], hl[FPG], need[FPG];
@@ -412,7 +413,10 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             v.y = (poff & 0xFFFFu) | (plen << 16);
             v.z = ck[f] | (cls[f] << 16) | (((uint32_t)rc & 0xFFu) << 24);
             v.w = (ok[f] ? 1u : 0u) | (flags << 8) | (stored[f] << 16);
-            st_verdict<WT>(ft, out, S.pf[f], v);
+            if (vb) // write-batched (WB): the trip's slot in the block's LDS batch
+                vb[(uint32_t)f * (256u / G) + threadIdx.x / G] = v;
+            else
+                st_verdict<WT>(ft, out, S.pf[f], v);
             const bool counted = rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE;
             const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
             if (counts && counted) {
@@ -430,7 +434,16 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
 // bytes are issued before trip t is processed (one extra frame set of
 // registers), so both HBM round trips overlap the previous trip's work.
 // WT: write-through (sc1) verdict stores, which leave the XCD's L2 (A/B, pipe 40)
-template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1, bool WT = false>
+// WB > 0 (write-batched, PIPE 0, not in index-list mode): block b owns the
+// contiguous tiles [b*per, (b+1)*per) instead of every gridDim-th tile, keeps
+// the verdicts of WB consecutive tiles in LDS and writes them out together,
+// WB * TILE * 16 contiguous bytes (sc1 when WT).  The verdicts are a sparse
+// write stream beside 1500-B frames (1% of the bytes): a burst read with one
+// 16-B store per slot ran 12-14% slower than the same read without it, and
+// the same stores bunched per block 2-3% faster than per trip
+// (tools/membw_cfg3, profiles/r06c, r06d).
+template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1, bool WT = false,
+          int WB = 0>
 __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -454,6 +467,49 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
         __syncthreads();
     }
 
+    if constexpr (WB > 0) {
+        if (!idx) { // block-uniform
+            uint4 *vb = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u));
+            const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
+            const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+            const uint64_t t0 = (uint64_t)blockIdx.x * per;
+            const uint64_t t1 = t0 + per < tiles ? t0 + per : tiles;
+            group_frames<FPG, P> A;
+            if (t0 < t1) {
+                group_desc<G>(A, t0, n, grp, pkts, off, len, unit_log2);
+                group_load<G, FPG, P, NTL>(A, s0);
+            }
+            uint32_t k = 0;
+            uint64_t first = t0;
+            for (uint64_t tile = t0; tile < t1; ++tile) { // block-uniform trips
+                group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins,
+                                                      vb + k * TILE);
+                if (tile + 1 < t1) { // the next tile's loads go out before the batch is written
+                    group_desc<G>(A, tile + 1, n, grp, pkts, off, len, unit_log2);
+                    group_load<G, FPG, P, NTL>(A, s0);
+                }
+                if (++k == (uint32_t)WB || tile + 1 == t1) {
+                    __syncthreads();
+                    const uint64_t b0 = first * TILE;
+                    const uint64_t m64 = (uint64_t)k * TILE < (uint64_t)n - b0 ? (uint64_t)k * TILE
+                                                                              : (uint64_t)n - b0;
+                    const uint32_t m = (uint32_t)m64;
+                    for (uint32_t i = tid; i < m; i += 256) st_verdict<WT>(ft, out, b0 + i, vb[i]);
+                    __syncthreads();
+                    k = 0;
+                    first = tile + 1;
+                }
+            }
+            if (lds_bins) {
+                __syncthreads();
+                for (uint32_t i = tid; i < lds_bins; i += 256) {
+                    const uint32_t c = hist[i];
+                    if (c) atomicAdd(&counts[i], (unsigned long long)c);
+                }
+            }
+            return;
+        }
+    }
     uint64_t tile = blockIdx.x;
     group_frames<FPG, P> A;
     if (tile * TILE < n) {
@@ -487,17 +543,18 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
 }
 
 template <int G, int P, int FPG, int PIPE = 0, bool NTL = true, int RI = 0, int MINW = 1,
-          bool WT = false>
+          bool WT = false, int WB = 0>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s, const uint32_t *idx = nullptr,
                     const uint32_t *n_dev = nullptr) {
+    static_assert(WB == 0 || PIPE == 0, "write batching: PIPE 0 only");
     constexpr uint32_t TILE = (256 / G) * FPG;
-    const size_t lds = (size_t)lds_bins * 4u;
+    const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u + (size_t)WB * TILE * 16u;
     // resident blocks: one wave of blocks, equal shares, no tail
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
-        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT>), 256,
+        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB>), 256,
         lds, &cu, &bpc);
     if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
@@ -506,7 +563,7 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
@@ -2931,6 +2988,10 @@ static const variant_entry k_variants[] = {
     // 40 (the 1500-B default): G=8 with write-through verdict stores (sc1:
     // the lines leave the L2 instead of staying in it)
     {8, 2, 2, 40, launch_v<8, 2, 2, 0, true, 0, 1, true>},
+    // 41 / 42: 40 write-batched (WB): each block owns contiguous tiles and
+    // writes the verdicts of 16 / 32 of them (16 / 32 KiB) at once (sc1)
+    {8, 2, 2, 41, launch_v<8, 2, 2, 0, true, 0, 1, true, 16>},
+    {8, 2, 2, 42, launch_v<8, 2, 2, 0, true, 0, 1, true, 32>},
     {8, 2, 1, 0, launch_v<8, 2, 1, 0>},
     {16, 2, 2, 0, launch_v<16, 2, 2, 0>},
     {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
@@ -2952,6 +3013,11 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6}, // 12 without the LDS UDP table
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
     {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
+    // write-batched G=8 around pipe 41 (WB 16, sc1): WB 8 / 12 / 24 (sc1), 16 (nt)
+    {8, 2, 2, 43, launch_v<8, 2, 2, 0, true, 0, 1, true, 8>},
+    {8, 2, 2, 44, launch_v<8, 2, 2, 0, true, 0, 1, true, 12>},
+    {8, 2, 2, 45, launch_v<8, 2, 2, 0, true, 0, 1, false, 16>},
+    {8, 2, 2, 46, launch_v<8, 2, 2, 0, true, 0, 1, true, 24>},
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>}, // heads gathered 4 lanes/head
     {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>},              // 12-KiB tiles
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},        // partial sums in the stream

@@ -601,10 +601,13 @@ struct rx_pend {
     uint32_t h_cap;
     rxg_delivery d;
     uint64_t gen0;   /* g_snap_gen at the submit */
-    double lib_ms;   /* the submit's library time */
+    double lib_ms;   /* the library's time for this burst (submit, wait) */
+    int waited, wrc; /* rxg_deliver_wait done, its result */
+    float gms[8];    /* its phase times */
 };
 static struct rx_pend g_pend[RXG_DELIVER_DEPTH];
 static uint32_t g_pend_head; /* the oldest pending burst */
+static void pend_wait(struct rx_pend *p);
 /* The protocol thread's (rx / tx bursts) hold of the stack's lock.  No
  * application loop takes g_lock any more (drain_all and the receive calls
  * look blocks up under g_tab), so nothing has to step aside for it. */
@@ -877,8 +880,7 @@ int nstack_init(int device, uint32_t max_burst, uint64_t max_bytes) {
 void nstack_fini(void) {
     /* bursts submitted and never completed: waited for, not delivered */
     while (g_pend_n && g_ctx) {
-        float ms[8];
-        (void)rxg_deliver_wait(g_ctx, &g_pend[g_pend_head].d, ms);
+        pend_wait(&g_pend[g_pend_head]);
         g_pend_head = (g_pend_head + 1) % RXG_DELIVER_DEPTH;
         g_pend_n--;
     }
@@ -2274,9 +2276,26 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
  * lookup, the burst is delivered frame by frame on the live lists
  * (deliver_part's stale path), the reference's sequential outcome. */
 
+/* the protocol thread: wait for a pending burst's device half (no lock:
+ * only this thread touches the pending bursts) */
+static void pend_wait(struct rx_pend *p) {
+    if (p->waited) return;
+    const double a = mono_ms();
+    p->wrc = rxg_deliver_wait(g_ctx, &p->d, p->gms);
+    p->lib_ms += mono_ms() - a;
+    p->waited = 1;
+}
+
 int nstack_rx_submit(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out) {
     if (!m && n) return RXG_EINVAL;
     t_proto = 1;
+    /* the bursts already on the GPU are waited for first: their results'
+     * copies back were queued behind their kernels, and this burst's copy in
+     * (0.57 ms at cfg3) would otherwise go ahead of them, so their
+     * completes waited for it (r06d: lib_call 0.66 ms per pipelined burst).
+     * A burst submitted one delivery earlier is normally done by now. */
+    if (g_ctx)
+        for (uint32_t j = 0; j < g_pend_n; j++) pend_wait(&g_pend[(g_pend_head + j) % RXG_DELIVER_DEPTH]);
     if (!g_inplace) reclaim();
     proto_lock();
     pl_wait_free();
@@ -2288,6 +2307,8 @@ int nstack_rx_submit(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v
     if (rc == RXG_OK) {
         p->m = m, p->n = n, p->rc_out = rc_out, p->v_out = v_out;
         p->gen0 = g_snap_gen;
+        p->waited = 0;
+        memset(p->gms, 0, sizeof(p->gms));
         const double a = mono_ms();
         rc = rxg_deliver_submit(g_ctx, m, n, p->v, &p->d);
         p->lib_ms = mono_ms() - a;
@@ -2318,10 +2339,10 @@ int nstack_rx_complete(void) {
     /* what the application threads let go of is freed while the burst (and
      * the one submitted after it) is on the GPU */
     reclaim();
-    float gms[8] = {0};
-    const double a = mono_ms();
-    const int wrc = rxg_deliver_wait(g_ctx, &p->d, gms);
-    const double lib_ms = p->lib_ms + (mono_ms() - a);
+    pend_wait(p);
+    const int wrc = p->wrc;
+    const float *gms = p->gms;
+    const double lib_ms = p->lib_ms;
     proto_lock();
     g_pend_head = (g_pend_head + 1) % RXG_DELIVER_DEPTH;
     g_pend_n--;

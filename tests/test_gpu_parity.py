@@ -204,6 +204,33 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got8.tobytes() == want8.tobytes(), (variant, "v8", _mismatch_report(got8, want8))
 
 
+@pytest.mark.parametrize("variant", R.compiled_variants([(8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42)]))
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1025, 64 * 16 * 3 + 17, 65536, 300001])
+@pytest.mark.parametrize("v8", [False, True])
+def test_group_write_batched(ctx, torch_dev, variant, n, v8):
+    """the write-batched G=8 kernels (41, 42: each block owns contiguous
+    64-frame tiles and writes the verdicts of 16 / 32 tiles at once from LDS)
+    against the oracle on 1500-B slotted bursts with counts: bursts of one
+    frame, of less than, exactly and just over one tile, a batch cut short by
+    the block's last tile, bursts where most blocks own no tile, and a burst
+    whose blocks own several batches (300001 frames); 16-B and 8-B verdicts;
+    nothing written past the burst (_dev_classify's guard bytes)"""
+    cfg = rxdist.gen_cfg("cfg3")
+    pk, off, ln = R.gen_host(cfg, 99, n, 6)
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 1500, counts=True, v8=v8)
+    finally:
+        ctx.tune(0)
+    if v8:
+        want = R.verdict8_of(want)
+    assert got.tobytes() == want.tobytes(), (variant, n, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), (variant, n)
+
+
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):

@@ -76,6 +76,90 @@ __global__ __launch_bounds__(256) void k_cfg2(const u32x4 *__restrict__ fr,
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// RDW with time-batched verdict writes (r06): block b owns the contiguous
+// 256-frame tiles [b*per, (b+1)*per) (U = 2 tiles per trip), keeps the
+// verdicts of T trips in LDS (T * 8 KiB) and writes them out together
+// (SM 0 nt, 2 sc1); T = 0: the plain per-trip stores, contiguous mapping
+template <int T, int SM>
+__global__ __launch_bounds__(256) void k_cfg2b(const u32x4 *__restrict__ fr,
+                                               const unsigned *__restrict__ off,
+                                               const unsigned short *__restrict__ len, size_t n,
+                                               u32x4 *__restrict__ out, unsigned *__restrict__ sink) {
+    constexpr int U = 2;
+    __shared__ u32x4 buf[(T > 0 ? T : 1) * 256 * U];
+    const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const size_t ntr = (n + 256 * U - 1) / (256 * U); // trips of 512 frames
+    const size_t per = (ntr + gridDim.x - 1) / gridDim.x;
+    const size_t r0 = blockIdx.x * per, r1 = r0 + per < ntr ? r0 + per : ntr;
+    unsigned k = 0;
+    size_t first = r0;
+    for (size_t r = r0; r < r1; ++r) {
+        const size_t t0 = r * 256 * U;
+        u32x4 v[U][4];
+        unsigned o[U], l[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t f = t0 + (size_t)u * 256 + threadIdx.x;
+            const size_t fq = f < n ? f : 0;
+            const size_t w0 = t0 + (size_t)u * 256 + wv * 64;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const size_t c = w0 * 4 + q * 64 + lane;
+                v[u][q] = __builtin_nontemporal_load(fr + (c < n * 4 ? c : 0));
+            }
+            o[u] = off[fq];
+            l[u] = len[fq];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t f = t0 + (size_t)u * 256 + threadIdx.x;
+            u32x4 x = v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+            x.x += o[u], x.y += l[u];
+            if (T == 0) {
+                if (f < n) __builtin_nontemporal_store(x, out + f);
+            } else {
+                buf[k * 256 * U + u * 256 + threadIdx.x] = x;
+            }
+        }
+        if (T > 0 && (++k == (unsigned)T || r + 1 == r1)) {
+            __syncthreads();
+            const size_t b0 = first * 256 * U;
+            const size_t m = (size_t)k * 256 * U < n - b0 ? (size_t)k * 256 * U : n - b0;
+            for (unsigned i = threadIdx.x; i < m; i += 256) {
+                if (SM == 0)
+                    __builtin_nontemporal_store(buf[i], out + b0 + i);
+                else
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(out + b0 + i),
+                                 "v"(buf[i])
+                                 : "memory");
+            }
+            __syncthreads();
+            k = 0;
+            first = r + 1;
+        }
+    }
+}
+
+template <int T, int SM>
+static void runb(const char *name, const u32x4 *fr, const unsigned *off, const unsigned short *len,
+                 size_t n, u32x4 *out, unsigned *sink, int cu, int bpc, double bytes) {
+    const int grid = cu * bpc;
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_cfg2b<T, SM>), dim3(grid), dim3(256), 0, 0, fr, off, len, n, out, sink);
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    const int reps = 50;
+    CHK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((k_cfg2b<T, SM>), dim3(grid), dim3(256), 0, 0, fr, off, len, n, out, sink);
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    printf("%-12s T=%d bpc=%d: %.4f ms  %.0f GB/s (of the bytes this variant moves)\n", name, T, bpc,
+           ms, bytes / ms / 1e6);
+}
+
 template <int MODE, int U>
 static void run(const char *name, const u32x4 *fr, const unsigned *off, const unsigned short *len,
                 size_t n, u32x4 *out, unsigned *sink, int cu, int bpc, double bytes) {
@@ -115,8 +199,17 @@ int main() {
     // warm the clocks
     for (int i = 0; i < 200; ++i) hipLaunchKernelGGL((k_cfg2<2, 2>), dim3(cu * 4), dim3(256), 0, 0, fr, off, len, n, out, sink);
     CHK(hipDeviceSynchronize());
-    // store flavours at the lane kernel's 2 blocks/CU, interleaved, 3 rounds (r06)
+    // time-batched verdict writes (block-contiguous tiles), interleaved, 3 rounds
     for (int round = 0; round < 3; ++round)
+        for (int bpc : {2, 3}) {
+            run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            runb<0, 0>("RDWcontig", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            runb<2, 0>("RDWbatch nt", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            runb<4, 0>("RDWbatch nt", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+            runb<4, 2>("RDWbatch sc1", fr, off, len, n, out, sink, cu, bpc, r + d + w);
+        }
+    // store flavours at the lane kernel's 2 blocks/CU, interleaved, 3 rounds (r06)
+    for (int round = 0; round < 1; ++round)
         for (int bpc : {2, 3}) {
             run<1, 2>("RD", fr, off, len, n, out, sink, cu, bpc, r + d);
             run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
@@ -124,19 +217,6 @@ int main() {
             run<3, 2>("RDWp", fr, off, len, n, out, sink, cu, bpc, r + d + w);
             run<4, 2>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
         }
-    for (int bpc : {2, 3, 4, 6, 8}) {
-        run<0, 1>("R", fr, off, len, n, out, sink, cu, bpc, r);
-        run<0, 2>("R", fr, off, len, n, out, sink, cu, bpc, r);
-        run<1, 2>("RD", fr, off, len, n, out, sink, cu, bpc, r + d);
-        run<2, 1>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
-        run<2, 2>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
-        run<2, 4>("RDW", fr, off, len, n, out, sink, cu, bpc, r + d + w);
-        run<3, 2>("RDWp", fr, off, len, n, out, sink, cu, bpc, r + d + w);
-        run<4, 1>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
-        run<4, 2>("RDW8", fr, off, len, n, out, sink, cu, bpc, r + d + w / 2);
-        run<5, 1>("RDW4", fr, off, len, n, out, sink, cu, bpc, r + d + w / 4);
-        run<5, 2>("RDW4", fr, off, len, n, out, sink, cu, bpc, r + d + w / 4);
-    }
     printf("(cfg2 algorithmic bytes per launch: %.3f GB)\n", (r + d + w) / 1e9);
     return 0;
 }
