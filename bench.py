@@ -972,11 +972,14 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         # same bytes in each), registered with the stack once, as a DPDK
         # application registers its mempool (rte_mempool_mem_iter): the GPU
         # pulls each burst's frames over PCIe instead of a host gather + copy.
-        # In place (the default here, nstack_set_rx_inplace), a connection's
+        # In place (nstack_set_rx_inplace, the A/B here), a connection's
         # receive fragments point into these frames and hold their mbufs
         # (refcnt) until the application has read them, so a set is reused
         # only once every one of its counts is back to 0 (the NIC refilling
-        # its ring from free mbufs)
+        # its ring from free mbufs).  The default is the pooled payload
+        # buffers: measured faster at cfg3 in every arrangement (r06d:
+        # sequential 6.51 vs 5.81 Mpps, two threads 8.62 vs 7.45, pipelined
+        # two threads 10.73 vs 6.80)
         NSET = 4
         span = len(pk)
         pool = np.empty(NSET * span, np.uint8)
@@ -993,8 +996,8 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
             res["pool_registered"] = True
         except R.RxgError as e:  # reported, and the host gather carries the bursts
             res["pool_registered"] = repr(e)
-        ns.set_rx_inplace(True)
-        res["tcp_inplace"] = True
+        ns.set_rx_inplace(False)
+        res["tcp_inplace"] = False
         kset = [0]
         pool_waits = [0]
 
@@ -1059,19 +1062,19 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
                         received_equal=h_items == items,
                         rx_burst_phases_ms={k: round(float(np.median([p[k] for p in h_ph])), 4)
                                             for k in h_ph[0]})
-        # A/B: payloads gathered on the GPU and copied back into pooled pinned
-        # buffers (the round-4 default)
-        ns.set_rx_inplace(False)
-        res["pooled_payload"] = ab_run()
+        # A/B: in place (the round-5 default): no payload gathered or copied
+        # back; the fragments point into the frames and hold their mbufs
         ns.set_rx_inplace(True)
+        res["inplace"] = ab_run()
+        ns.set_rx_inplace(False)
         # A/B: pipelined (nstack_rx_submit / nstack_rx_complete): burst k+1
         # crosses PCIe and goes through the kernels while burst k is delivered
         # and read (the first submit is outside the clock, as a loop's first
         # burst would be in flight already)
         res["pipelined"] = ab_run(pipelined=True)
-        ns.set_rx_inplace(False)
-        res["pooled_pipelined"] = ab_run(pipelined=True)
         ns.set_rx_inplace(True)
+        res["inplace_pipelined"] = ab_run(pipelined=True)
+        ns.set_rx_inplace(False)
         # A/B: each burst as two halves, both on the GPU at once
         # (nstack_set_halves; off by default)
         ns.set_halves(B // 2)
@@ -1159,10 +1162,10 @@ def socket_api(local, name, budget_s, cores, with_cpu=True):
         res["overlapped"] = overlapped(pair)
         res["overlapped_pipelined"] = overlapped(pair, pipelined=True)
         # the in-place vs pooled-payload A/B in the two-thread forms too
-        ns.set_rx_inplace(False)
-        res["overlapped_pooled"] = overlapped(pair)
-        res["overlapped_pipelined_pooled"] = overlapped(pair, pipelined=True)
         ns.set_rx_inplace(True)
+        res["overlapped_inplace"] = overlapped(pair)
+        res["overlapped_pipelined_inplace"] = overlapped(pair, pipelined=True)
+        ns.set_rx_inplace(False)
         res["overlapped_unpinned"] = overlapped(None, unpin=True)
         frame_bytes = int(ln.astype(np.int64).sum())
         res.update(bursts=K, mpps=round(B * K / (t_rx + t_dr) / 1e6, 3),
@@ -1481,14 +1484,14 @@ def _sock_summary(s):
         return dict(error=str(s["error"])[:120])
     out = dict(mpps=_g(s, "mpps"), overlapped_mpps=_g(s, "overlapped", "mpps"),
                cpu_mpps=_g(s, "cpu_baseline", "mpps"),
-               pooled_mpps=_g(s, "pooled_payload", "mpps"),
+               inplace_mpps=_g(s, "inplace", "mpps"),
                d2h_ms=_g(s, "rx_burst_phases_ms", "d2h"),
                app_lock_wait_ms=_g(s, "overlapped", "app_ms_per_burst", "lock_wait"),
                received_equal=_g(s, "overlapped", "received_equal"),
                pipelined_mpps=_g(s, "pipelined", "mpps"),
-               pooled_pipelined_mpps=_g(s, "pooled_pipelined", "mpps"),
-               overlapped_pooled_mpps=_g(s, "overlapped_pooled", "mpps"),
-               overlapped_pipelined_pooled_mpps=_g(s, "overlapped_pipelined_pooled", "mpps"),
+               inplace_pipelined_mpps=_g(s, "inplace_pipelined", "mpps"),
+               overlapped_inplace_mpps=_g(s, "overlapped_inplace", "mpps"),
+               overlapped_pipelined_inplace_mpps=_g(s, "overlapped_pipelined_inplace", "mpps"),
                overlapped_pipelined_mpps=_g(s, "overlapped_pipelined", "mpps"),
                pipelined_received_equal=_g(s, "overlapped_pipelined", "received_equal"))
     return {k: v for k, v in out.items() if v is not None}

@@ -3081,8 +3081,11 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         *g = 0, *p = 0, *fpg = 0, *pipe = 67;
     } else if (len_hint <= 1536) { // cfg3: 1500 B.  Write-through verdict stores (pipe 40):
         // 1.0191 vs 1.0322 ms for pipe 0 (interleaved sweep, profiles/r03c/sweep_cfg3_wt.txt),
-        // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt)
-        *g = 8, *p = 2, *fpg = 2, *pipe = 40;
+        // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt); written
+        // in batches of 16 tiles per block (pipe 41): 0.9992-1.0046 vs 1.0243-1.0280 ms for
+        // 40 on two boxes (WB 8 / 12 / 24: 1.038 / 1.024 / 1.054; WB 16 nt 1.013;
+        // profiles/r06e, r06f)
+        *g = 8, *p = 2, *fpg = 2, *pipe = 41;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), pipe 38
         // (vs 30: 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms, r01g, r01j) with 16 frames per block:
         // 32 frames 1.6746 vs 1.7833 ms for 256 (64: 1.6810, 128: 1.7139; profiles/r03f/sweep_cfg5_fpb.txt),
