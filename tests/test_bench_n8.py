@@ -115,6 +115,7 @@ def test_eight_rank_line_on_cpu():
     r0 = got[0]
     line, short = r0["line"], json.loads(r0["short"])
     assert len(r0["short"]) < r0["limit"], len(r0["short"])
+    print("N = 8 compact line:", len(r0["short"]), "bytes")
     assert "dropped" not in short, short.get("dropped")
     assert line["n_gpus"] == WORLD and len(line["per_rank"]) == WORLD
     assert [p["rank"] for p in line["per_rank"]] == list(range(WORLD))
