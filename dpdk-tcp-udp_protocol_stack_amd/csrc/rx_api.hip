@@ -1122,10 +1122,12 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 }
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
-    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_COUNT_2BUF)))
+    if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_COUNT_2BUF |
+                                   RXG_TT_SLAB_HALF | RXG_TT_SLAB_QUARTER)))
         return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
+    c->ft.slab_div_log2 = (flags & RXG_TT_SLAB_QUARTER) ? 2u : (flags & RXG_TT_SLAB_HALF) ? 1u : 0u;
     c->ws_nbuf = (flags & RXG_TT_COUNT_2BUF) ? 2u : 3u;
     return RXG_OK;
 }

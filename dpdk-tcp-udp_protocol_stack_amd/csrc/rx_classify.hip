@@ -2905,8 +2905,9 @@ static uint32_t slab_words(const rx_ft_dev &ft) {
 // slab geometry: about one 1024-thread block per CU in all (256 blocks over
 // the ranges), >= 16384 frames per slab so the slabs stay small beside the
 // indices, a multiple of 4 frames (aligned 16-B index loads)
-static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per) {
-    const uint64_t want = std::max<uint64_t>(1, 256 / nranges);
+static void slab_geometry(uint32_t n, uint32_t nranges, uint32_t *nslabs, uint32_t *per,
+                          uint32_t div_log2 = 0) {
+    const uint64_t want = std::max<uint64_t>(1, (256u >> div_log2) / nranges);
     uint64_t pr = std::max<uint64_t>(((uint64_t)n + want - 1) / want, 16384);
     pr = (pr + 7) & ~7ull;
     const uint64_t nb = ((uint64_t)n + pr - 1) / pr;
@@ -2926,7 +2927,7 @@ static hipError_t launch_count_slab(const void *cidx, uint32_t n, const rx_ft_de
                                     unsigned long long *counts, uint32_t *slab, hipStream_t s) {
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
-    slab_geometry(n, nr, &nslabs, &per);
+    slab_geometry(n, nr, &nslabs, &per, ft.slab_div_log2);
     if (ft.cidx16)
         hipLaunchKernelGGL(rx_count_slab_kernel<uint16_t>, dim3(nslabs, nr), dim3(1024), 0, s,
                            static_cast<const uint16_t *>(cidx), n, per, words, nf,
@@ -3147,7 +3148,7 @@ size_t rx_classify_ws_bytes(uint32_t n, uint32_t g, uint32_t pipe, const rx_ft_d
     size_t b = ws_lists_bytes(n, g, pipe);
     if (use_slab(ft, counts)) {
         uint32_t nslabs, per;
-        slab_geometry(n, slab_ranges(ft), &nslabs, &per);
+        slab_geometry(n, slab_ranges(ft), &nslabs, &per, ft.slab_div_log2);
         b += ws_cidx_bytes(n) * std::max(nbuf, 1u) +
              (size_t)nslabs * slab_ranges(ft) * slab_words(ft) * 4;
     }

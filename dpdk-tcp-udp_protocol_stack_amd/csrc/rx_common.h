@@ -70,6 +70,9 @@ struct rx_ft_dev {
     // rxg_tune_tables(RXG_TT_COUNT_4B): 4-B count indices whatever the flow
     // count (the round-1 count path, for A/B)
     uint32_t count_4b;
+    // rxg_tune_tables(RXG_TT_SLAB_HALF / _QUARTER): the slab pass on 1/2 or 1/4 of
+    // the CUs (log2 of the divisor; 0 = one 1024-thread block per CU)
+    uint32_t slab_div_log2;
     // host side only: the burst's verdict format (0 = 16-B rxg_verdict, 1 =
     // 8-B rxg_verdict8, rxg_classify_dev8), which picks the launcher of the
     // RX_V8 build of rx_classify.hip; the kernels never read it

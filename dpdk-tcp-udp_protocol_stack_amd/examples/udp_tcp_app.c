@@ -168,10 +168,47 @@ int main(void) {
     if (nrecv(cfd, data, sizeof(data), MSG_DONTWAIT) != -1) FAIL("the corrupted segment was queued");
     const int ntx2 = nstack_tx_burst(tx, sizeof(tx), toff, tlen, 4, 1, &span); /* the data ACK */
     if (ntx2 < 1) FAIL("second tx pass: %d", ntx2);
+
+    /* the pipelined receive: burst B goes to the GPU while burst A is
+     * delivered (nstack_rx_submit / nstack_rx_complete); each burst carries
+     * 60 datagrams and one segment of the open connection */
+    uint32_t first[2];
+    int prc[2][MAXF];
+    for (int b = 0; b < 2; b++) {
+        first[b] = g_n;
+        for (int i = 0; i < 60; i++) {
+            const int l = snprintf(msg, sizeof(msg), "pipe %d/%02d", b, i);
+            add(frame(g_pool[g_n], "10.0.0.1", 5555, LOCAL_IP, 8889, 17, 0, 0, 0, msg, (size_t)l));
+        }
+        add(frame(g_pool[g_n], "10.0.0.9", 40000, LOCAL_IP, 9999, 6, 0x18, 1013 + 11 * b, isn + 1,
+                  b ? "pipelined-2" : "pipelined-1", 11));
+    }
+    const uint32_t na = first[1] - first[0], nb = g_n - first[1];
+    if (nstack_rx_submit(g_mp + first[0], na, prc[0], NULL) != RXG_OK) FAIL("submit A");
+    if (nstack_rx_submit(g_mp + first[1], nb, prc[1], NULL) != RXG_OK) FAIL("submit B");
+    if (nstack_rx_submit(g_mp + first[1], nb, prc[1], NULL) != RXG_EINVAL) FAIL("a third submit");
+    if (nstack_rx_pending() != 2) FAIL("pending %d", nstack_rx_pending());
+    if (nstack_rx_complete() != 60 || nstack_rx_complete() != 60) FAIL("completes");
+    if (nstack_rx_complete() != RXG_EINVAL) FAIL("a complete with nothing pending");
+    g_n = 0;
+    for (int b = 0; b < 2; b++)
+        for (uint32_t i = 0; i < 61; i++)
+            if (prc[b][i] != 0) FAIL("pipelined burst %d frame %u: rc %d", b, i, prc[b][i]);
+    for (int b = 0; b < 2; b++)
+        for (int i = 0; i < 60; i++) {
+            char buf[128];
+            const ssize_t r2 = nrecvfrom(ufd, buf, sizeof(buf), MSG_DONTWAIT, NULL, NULL);
+            const int l = snprintf(msg, sizeof(msg), "pipe %d/%02d", b, i);
+            if (r2 != l + 8 || memcmp(buf, msg, (size_t)l)) FAIL("pipelined datagram %d/%d: %zd", b, i, r2);
+        }
+    for (int b = 0; b < 2; b++) {
+        const ssize_t r2 = nrecv(cfd, data, sizeof(data), MSG_DONTWAIT);
+        if (r2 != 11 || memcmp(data, b ? "pipelined-2" : "pipelined-1", 11)) FAIL("pipelined nrecv %d: %zd", b, r2);
+    }
     nclose(cfd);
     nclose(lfd);
     nclose(ufd);
     nstack_fini();
-    printf("udp_tcp_app ok: 100 datagrams, 1 connection, %d + %d frames sent\n", ntx, ntx2);
+    printf("udp_tcp_app ok: 100 + 120 pipelined datagrams, 1 connection, %d + %d frames sent\n", ntx, ntx2);
     return 0;
 }

@@ -196,6 +196,8 @@ _tune_tables = _sig("rxg_tune_tables", _i32, _vp, _u32)
 TT_NO_UDP_PORT = 0x1
 TT_COUNT_4B = 0x2
 TT_COUNT_2BUF = 0x4
+TT_SLAB_HALF = 0x8     # the slab pass on half / a quarter of the CUs (fewer, larger slabs)
+TT_SLAB_QUARTER = 0x10
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)

@@ -524,6 +524,8 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
 #define RXG_TT_COUNT_2BUF 0x4u /* rxg_classify_dev_cs: two count-index buffers instead of
                                   three (each burst then waits for the count of the
                                   burst before the previous one) */
+#define RXG_TT_SLAB_HALF 0x8u     /* the count's slab pass on half / a quarter of the CUs */
+#define RXG_TT_SLAB_QUARTER 0x10u /* (fewer, larger slabs; applied at once) */
 
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 

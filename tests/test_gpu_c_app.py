@@ -2,8 +2,9 @@
 TCP server written as the reference's are (netfamily.c:211-383) on
 include/nstack.h alone, linked against libnstack.so / librxgpu.so like an
 application; its own checks (every datagram and its source, the handshake and
-naccept, nrecv's data, a corrupted segment dropped with rc -3, the TX pass's
-SYN|ACK and data ACK) end in exit 0."""
+naccept, nrecv's data, a corrupted segment dropped with rc -1 (tcp.c:352-357),
+the TX pass's SYN|ACK and data ACK, and two bursts through the pipelined
+receive, nstack_rx_submit / nstack_rx_complete) end in exit 0."""
 import os
 import subprocess
 

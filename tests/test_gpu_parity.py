@@ -716,6 +716,49 @@ def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
     assert np.array_equal(cnt, want)
 
 
+@pytest.mark.parametrize("tables", [R.TT_SLAB_HALF, R.TT_SLAB_QUARTER, R.TT_SLAB_HALF | R.TT_COUNT_4B])
+@pytest.mark.parametrize("nu", [65536, 200000])
+def test_count_slab_geometry(ctx, torch_dev, nu, tables):
+    """the slab pass on half / a quarter of the CUs (rxg_tune_tables
+    RXG_TT_SLAB_HALF / _QUARTER: fewer, larger slabs): frames to 5000 random
+    sockets of 65536 (2-B indices, flow 65535 among them) or 200000 (4 ranges),
+    the per-flow counts equal to the frames sent, with and without the count
+    stream"""
+    torch, dev = torch_dev
+    udp = _udp_socks(nu)
+    rng = np.random.default_rng(nu + tables)
+    ks = np.unique(np.concatenate([[nu - 1, 0], rng.integers(0, nu, 5000)]))
+    fr = [_sock_frame(int(k)) for k in ks]
+    buf, off0, lens0 = F.pack_frames(fr, 6)
+    pick = rng.integers(0, len(ks), 300001)
+    off = off0[pick].astype(np.uint32)
+    lens = lens0[pick]
+    ctx.flows_sync(udp, None)
+    want = np.zeros(nu, np.uint64)
+    np.add.at(want, ks[pick], 1)
+    ctx.tune_tables(tables)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, buf, off, lens, 6, 64, counts=True)
+        assert np.array_equal(cnt, want), (nu, tables)
+        # the same through the count stream (rxg_classify_dev_cs), three bursts
+        d_pk = torch.from_numpy(np.concatenate([buf, np.zeros(64, np.uint8)])).to(dev)
+        d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+        d_ln = torch.from_numpy(lens.view(np.int16)).to(dev)
+        d_out = torch.empty(len(off) * 16, dtype=torch.uint8, device=dev)
+        d_cnt = torch.zeros(nu, dtype=torch.int64, device=dev)
+        cs = torch.cuda.Stream(dev)
+        st = torch.cuda.current_stream(dev)
+        for _ in range(3):
+            ctx.classify_dev(d_pk, d_off, d_ln, len(off), 6, 64, d_out, d_cnt, stream=st.cuda_stream,
+                             count_stream=cs.cuda_stream)
+        st.wait_stream(cs)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 3 * want), (nu, tables, "cs")
+    finally:
+        ctx.tune_tables(0)
+    assert np.all(got["rc"] == 0)
+
+
 @pytest.mark.parametrize("nu", [65535, 65536])
 def test_count_idx16_all_ones(ctx, torch_dev, nu):
     """2-B count indices (<= 65536 flows): frames of flow 65535 (when it
