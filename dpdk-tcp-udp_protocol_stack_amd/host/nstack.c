@@ -1744,7 +1744,8 @@ int nstack_deliver(rxg_mbuf *const *m, uint32_t n, const rxg_verdict *v, uint64_
     if (!m || !v) return n ? RXG_EINVAL : 0;
     reclaim();
     pthread_mutex_lock(&g_lock);
-    int rc = g_ctx ? RXG_OK : RXG_EINVAL;
+    /* (refused while pipelined bursts are pending: their frames come first) */
+    int rc = g_ctx && !g_pend_n ? RXG_OK : RXG_EINVAL;
     int delivered = 0;
     if (rc == RXG_OK) {
         g_burst_stale = gen != g_snap_gen; /* classified against other lists */

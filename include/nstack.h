@@ -106,8 +106,9 @@ int nstack_rx_burst(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_
  * call changed a lookup (the reference's sequential outcome, netfamily.c:
  * 147-200 taking burst k+1 only after burst k).  The loop:
  *     nstack_rx_submit(b0); for (k...) { nstack_rx_submit(b[k+1]); nstack_rx_complete(); }
- * nstack_rx_pending: bursts submitted and not completed.  nstack_rx_burst is
- * refused while any is pending; nstack_fini waits for them and drops them. */
+ * nstack_rx_pending: bursts submitted and not completed.  nstack_rx_burst and
+ * nstack_deliver are refused while any is pending; nstack_fini waits for them
+ * and drops them. */
 int nstack_rx_submit(rxg_mbuf *const *m, uint32_t n, int *rc_out, rxg_verdict *v_out);
 int nstack_rx_complete(void);
 int nstack_rx_pending(void);

@@ -256,6 +256,8 @@ def test_socket_layer_pipelined_match_oracle(torch_dev):
                     st.ns.rx_submit(bursts[b + 1][:10])
                 with pytest.raises(R.RxgError):  # the one-shot call is refused meanwhile
                     st.ns.rx_burst(bursts[b][:10])
+                with pytest.raises(R.RxgError):  # and so is host-verdict delivery
+                    st.ns.deliver(bursts[b][:1], np.zeros(1, R.VERDICT_DTYPE))
             s0 = st.ns.stat(5)
             want = [st.os.rx(f) for f in bursts[b]]
             n, rcs, _ = st.ns.rx_complete()
