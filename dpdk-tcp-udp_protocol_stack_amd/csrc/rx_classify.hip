@@ -173,7 +173,7 @@ __device__ __forceinline__ void group_load(group_frames<FPG, P> &S, int32_t s0) 
 // loads of a lane in flight; a pass past a frame's end loads the frame's first
 // chunk again, an L1/L2 hit, and adds nothing), which keeps enough bytes in
 // flight for jumbo frames.
-template <int G, int P, int FPG, bool NTL = true, int RI = 0, bool WT = false>
+template <int G, int P, int FPG, bool NTL = true, int RI = 0, bool WT = false, bool H16 = false>
 __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t gl, uint32_t gbase,
                                               int32_t s0, const rx_ft_dev &ft,
                                               uint4 *__restrict__ out,
@@ -420,10 +420,14 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
             const bool counted = rc == RXG_RC_OK && flow[f] != RXG_FLOW_NONE;
             const uint32_t idx = (cls[f] == RXG_CLS_TCP ? ft.nu : 0u) + flow[f];
             if (counts && counted) {
-                if (lds_bins)
-                    atomicAdd(&hist[idx], 1u);
-                else
+                if (lds_bins) {
+                    if constexpr (H16) // 16-bit bin pairs (the launch bounds a block's frames < 65536)
+                        atomicAdd(&hist[idx >> 1], 1u << ((idx & 1u) * 16u));
+                    else
+                        atomicAdd(&hist[idx], 1u);
+                } else {
                     atomicAdd(&counts[idx], 1ull);
+                }
             }
             if (ft.count_idx) put_count_idx(ft, S.pf[f], counted ? idx : 0xFFFFFFFFu);
         }
@@ -442,8 +446,10 @@ __device__ __forceinline__ void group_process(group_frames<FPG, P> &S, uint32_t 
 // 16-B store per slot ran 12-14% slower than the same read without it, and
 // the same stores bunched per block 2-3% faster than per trip
 // (tools/membw_cfg3, profiles/r06c, r06d).
+// H16: the per-block LDS histogram in 16-bit bin pairs (half the LDS; the
+// launch uses it only when no block classifies 65536 frames or more)
 template <int G, int P, int FPG, int PIPE, bool NTL = true, int RI = 0, int MINW = 1, bool WT = false,
-          int WB = 0>
+          int WB = 0, bool H16 = false>
 __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     const uint8_t *__restrict__ pkts, const uint32_t *__restrict__ off,
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
@@ -462,14 +468,27 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
     const uint32_t grp = tid / G;
     const int32_t s0 = 16 * (int32_t)gl;
 
+    const uint32_t hwords = H16 ? (lds_bins + 1u) / 2u : lds_bins; // histogram words
     if (lds_bins) {
-        for (uint32_t i = tid; i < lds_bins; i += 256) hist[i] = 0;
+        for (uint32_t i = tid; i < hwords; i += 256) hist[i] = 0;
         __syncthreads();
     }
+    // the block's histogram into the global counts (H16: two bins per word)
+    auto flush_hist = [&]() {
+        for (uint32_t i = tid; i < hwords; i += 256) {
+            const uint32_t c = hist[i];
+            if constexpr (H16) {
+                if (c & 0xFFFFu) atomicAdd(&counts[2 * i], (unsigned long long)(c & 0xFFFFu));
+                if ((c >> 16) && 2 * i + 1 < lds_bins) atomicAdd(&counts[2 * i + 1], (unsigned long long)(c >> 16));
+            } else {
+                if (c) atomicAdd(&counts[i], (unsigned long long)c);
+            }
+        }
+    };
 
     if constexpr (WB > 0) {
         if (!idx) { // block-uniform
-            uint4 *vb = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u));
+            uint4 *vb = reinterpret_cast<uint4 *>(hist + ((hwords + 3u) & ~3u));
             const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
             const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
             const uint64_t t0 = (uint64_t)blockIdx.x * per;
@@ -482,8 +501,8 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
             uint32_t k = 0;
             uint64_t first = t0;
             for (uint64_t tile = t0; tile < t1; ++tile) { // block-uniform trips
-                group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins,
-                                                      vb + k * TILE);
+                group_process<G, P, FPG, NTL, RI, WT, H16>(A, gl, gbase, s0, ft, out, counts, hist,
+                                                           lds_bins, vb + k * TILE);
                 if (tile + 1 < t1) { // the next tile's loads go out before the batch is written
                     group_desc<G>(A, tile + 1, n, grp, pkts, off, len, unit_log2);
                     group_load<G, FPG, P, NTL>(A, s0);
@@ -502,10 +521,7 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
             }
             if (lds_bins) {
                 __syncthreads();
-                for (uint32_t i = tid; i < lds_bins; i += 256) {
-                    const uint32_t c = hist[i];
-                    if (c) atomicAdd(&counts[i], (unsigned long long)c);
-                }
+                flush_hist();
             }
             return;
         }
@@ -521,13 +537,13 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
         group_desc<G>(B, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         for (; tile * TILE < n; tile += gridDim.x) {
             group_load<G, FPG, P, NTL>(B, s0); // no-op lanes past the end (cap 0)
-            group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI, WT, H16>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             A = B;
             group_desc<G>(B, tile + 2 * (uint64_t)gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
         }
     } else {
         for (; tile * TILE < n; tile += gridDim.x) {
-            group_process<G, P, FPG, NTL, RI, WT>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
+            group_process<G, P, FPG, NTL, RI, WT, H16>(A, gl, gbase, s0, ft, out, counts, hist, lds_bins);
             group_desc<G>(A, tile + gridDim.x, n, grp, pkts, off, len, unit_log2, idx);
             group_load<G, FPG, P, NTL>(A, s0);
         }
@@ -535,26 +551,24 @@ __global__ __launch_bounds__(256, MINW) void rx_classify_kernel(
 
     if (lds_bins) {
         __syncthreads();
-        for (uint32_t i = tid; i < lds_bins; i += 256) {
-            const uint32_t c = hist[i];
-            if (c) atomicAdd(&counts[i], (unsigned long long)c);
-        }
+        flush_hist();
     }
 }
 
 template <int G, int P, int FPG, int PIPE = 0, bool NTL = true, int RI = 0, int MINW = 1,
-          bool WT = false, int WB = 0>
+          bool WT = false, int WB = 0, bool H16 = false>
 hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out, unsigned long long *counts,
                     uint32_t lds_bins, hipStream_t s, const uint32_t *idx = nullptr,
                     const uint32_t *n_dev = nullptr) {
     static_assert(WB == 0 || PIPE == 0, "write batching: PIPE 0 only");
     constexpr uint32_t TILE = (256 / G) * FPG;
-    const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u + (size_t)WB * TILE * 16u;
+    const uint32_t hwords = H16 ? (lds_bins + 1u) / 2u : lds_bins;
+    const size_t lds = (size_t)((hwords + 3u) & ~3u) * 4u + (size_t)WB * TILE * 16u;
     // resident blocks: one wave of blocks, equal shares, no tail
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
-        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB>), 256,
+        reinterpret_cast<const void *>(rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB, H16>), 256,
         lds, &cu, &bpc);
     if (e != hipSuccess) return e;
     const uint64_t tiles = ((uint64_t)n + TILE - 1) / TILE;
@@ -563,7 +577,15 @@ hipError_t launch_v(const uint8_t *pkts, const uint32_t *off, const uint16_t *le
     uint64_t blocks = (uint64_t)cu * occ;
     if (blocks > tiles) blocks = tiles;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB>), dim3((uint32_t)blocks), dim3(256), lds, s,
+    if constexpr (H16) {
+        // a 16-bit bin holds at most 65535: every block's share of the burst
+        // (index-list mode: n_dev may shorten it, never lengthen) stays below
+        // that, else the 32-bit histogram
+        if (lds_bins && ((tiles + blocks - 1) / blocks) * TILE > 65535u)
+            return launch_v<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB, false>(
+                pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, s, idx, n_dev);
+    }
+    hipLaunchKernelGGL((rx_classify_kernel<G, P, FPG, PIPE, NTL, RI, MINW, WT, WB, H16>), dim3((uint32_t)blocks), dim3(256), lds, s,
                        pkts, off, len, n, unit_log2, ft, out, counts, lds_bins, idx, n_dev);
     return hipGetLastError();
 }
@@ -2993,6 +3015,10 @@ static const variant_entry k_variants[] = {
     // writes the verdicts of 16 / 32 of them (16 / 32 KiB) at once (sc1)
     {8, 2, 2, 41, launch_v<8, 2, 2, 0, true, 0, 1, true, 16>},
     {8, 2, 2, 42, launch_v<8, 2, 2, 0, true, 0, 1, true, 32>},
+    // 48 (the 1500-B default): 24 tiles per batch with the per-block histogram
+    // in 16-bit bin pairs (32 KiB of LDS at 4097 flows, as 41's), the 32-bit
+    // histogram when a block's share reaches 65536 frames
+    {8, 2, 2, 48, launch_v<8, 2, 2, 0, true, 0, 1, true, 24, true>},
     {8, 2, 1, 0, launch_v<8, 2, 1, 0>},
     {16, 2, 2, 0, launch_v<16, 2, 2, 0>},
     {32, 3, 2, 0, launch_v<32, 3, 2, 0>},
@@ -3019,6 +3045,9 @@ static const variant_entry k_variants[] = {
     {8, 2, 2, 44, launch_v<8, 2, 2, 0, true, 0, 1, true, 12>},
     {8, 2, 2, 45, launch_v<8, 2, 2, 0, true, 0, 1, false, 16>},
     {8, 2, 2, 46, launch_v<8, 2, 2, 0, true, 0, 1, true, 24>},
+    // ... with a 16-bit histogram (half its LDS): WB 16 / 32 (24: pipe 48, the default)
+    {8, 2, 2, 47, launch_v<8, 2, 2, 0, true, 0, 1, true, 16, true>},
+    {8, 2, 2, 49, launch_v<8, 2, 2, 0, true, 0, 1, true, 32, true>},
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>}, // heads gathered 4 lanes/head
     {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>},              // 12-KiB tiles
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},        // partial sums in the stream
@@ -3085,8 +3114,9 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 0.9919 vs 1.0002 across processes (profiles/r03b/ab_store_policy_sc1.txt); written
         // in batches of 16 tiles per block (pipe 41): 0.9992-1.0046 vs 1.0243-1.0280 ms for
         // 40 on two boxes (WB 8 / 12 / 24: 1.038 / 1.024 / 1.054; WB 16 nt 1.013;
-        // profiles/r06e, r06f)
-        *g = 8, *p = 2, *fpg = 2, *pipe = 41;
+        // profiles/r06e, r06f); batches of 24 with a 16-bit histogram (pipe 48, the
+        // same 32 KiB of LDS): 0.9881 / 0.9901 vs 0.9927 / 0.9951 ms for 41 (profiles/r06l)
+        *g = 8, *p = 2, *fpg = 2, *pipe = 48;
     } else { // jumbo (cfg5: 9000 B): stream kernel (1.72 ms vs 1.77 for G=16, r01b sweep), pipe 38
         // (vs 30: 1.7275 vs 1.7309 and 1.7578 vs 1.7626 ms, r01g, r01j) with 16 frames per block:
         // 32 frames 1.6746 vs 1.7833 ms for 256 (64: 1.6810, 128: 1.7139; profiles/r03f/sweep_cfg5_fpb.txt),

@@ -51,7 +51,7 @@ HOST_ONLY = -1
 # (lanes per frame, passes, frames per group, pipeline); every one gives the
 # reference's verdicts (tests/test_gpu_parity.py runs each)
 KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 0),
-                   (4, 1, 1, 1), (8, 2, 2, 0), (8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42),
+                   (4, 1, 1, 1), (8, 2, 2, 0), (8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42), (8, 2, 2, 48),
                    (8, 2, 1, 0), (16, 2, 2, 0),
                    (32, 3, 2, 0), (64, 4, 1, 0),
                    (0, 0, 0, 20),  # size-class binned: lane kernel + G=8 kernel
@@ -60,7 +60,8 @@ KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 0),
 # compiled only into the RX_DIAG build (librxgpu_diag.so, RXGPU_LIB=...):
 # tuning shapes with correct verdicts ...
 DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (8, 2, 2, 1), (16, 2, 1, 0),
-                        (8, 2, 2, 43), (8, 2, 2, 44), (8, 2, 2, 45), (8, 2, 2, 46), (0, 0, 0, 54), (0, 0, 0, 66),
+                        (8, 2, 2, 43), (8, 2, 2, 44), (8, 2, 2, 45), (8, 2, 2, 46),
+                        (8, 2, 2, 47), (8, 2, 2, 49), (0, 0, 0, 54), (0, 0, 0, 66),
                         (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65),
                         (0, 0, 0, 80), (0, 0, 0, 81), (0, 0, 0, 82), (0, 0, 0, 83)]  # WC kernel
 # ... and ablations, wrong verdicts (or counts) by construction

@@ -204,7 +204,8 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
     assert got8.tobytes() == want8.tobytes(), (variant, "v8", _mismatch_report(got8, want8))
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42),
+                                                          (8, 2, 2, 47), (8, 2, 2, 48), (8, 2, 2, 49)]))
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1025, 64 * 16 * 3 + 17, 65536, 300001])
 @pytest.mark.parametrize("v8", [False, True])
 def test_group_write_batched(ctx, torch_dev, variant, n, v8):
@@ -714,6 +715,43 @@ def test_count_slab_bin_overflow(ctx, torch_dev, target, nu, n):
     want = np.zeros(nu, np.uint64)
     want[target] = n
     assert np.array_equal(cnt, want)
+
+
+@pytest.mark.parametrize("variant", R.compiled_variants([(8, 2, 2, 41), (8, 2, 2, 47), (8, 2, 2, 48)]))
+@pytest.mark.parametrize("extra", [0, 64 * 256])
+def test_group_hist16_edge(ctx, torch_dev, variant, extra):
+    """the G=8 kernels' per-block LDS histogram at its limit: every frame to
+    one socket, one resident block per CU (rxg_tune_grid 1), so each block
+    classifies 65,472 frames (extra 0: the 16-bit bins of the H16 variants
+    hold it) or 65,536 (extra one tile per block: the launch falls back to
+    32-bit bins); the count must be every frame"""
+    torch, dev = torch_dev
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    n = 1023 * ncu * 64 + extra
+    udp = _udp_socks(1000)
+    f = _sock_frame(321)
+    buf, _, _ = F.pack_frames([f], 6)
+    d_pk = torch.from_numpy(buf[:64]).to(dev).repeat(n + 1)
+    d_off = torch.arange(n, dtype=torch.int32, device=dev)
+    d_ln = torch.full((n,), len(f), dtype=torch.int16, device=dev)
+    d_out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    d_cnt = torch.zeros(1000, dtype=torch.int64, device=dev)
+    ctx.flows_sync(udp, None)
+    ctx.tune(*variant)
+    ctx.tune_grid(1)
+    try:
+        ctx.classify_dev(d_pk, d_off, d_ln, n, 6, 1500, d_out, d_cnt,
+                         stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+    finally:
+        ctx.tune_grid(0)
+        ctx.tune(0)
+    c = d_cnt.cpu().numpy()
+    assert c[321] == n and c.sum() == n, (variant, n, int(c[321]))
+    v = d_out.view(n, 16)
+    assert bool((v[:, 11].view(torch.int8) == 0).all()) and bool((v[:, 0:4].contiguous().view(torch.int32) == 321).all())
+    del d_pk, d_out
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("tables", [R.TT_SLAB_HALF, R.TT_SLAB_QUARTER, R.TT_SLAB_HALF | R.TT_COUNT_4B])
