@@ -45,7 +45,7 @@ for nm in names:
     for (v, b), t in times.items():
         t = sorted(t)
         print(f"tx {nm} variant={v} bpc={b}: median {t[2]:.4f} ms min {t[0]:.4f} -> "
-              f"{n / t[2] / 1e3:.0f} Mpps {txb / t[2] / 1e6:.0f} GB/s ({txb / t[2] / 8e6:.3f} of 8 TB/s)",
+              f"{n / t[2] / 1e3:.0f} Mpps {txb / t[2] / 1e6:.0f} GB/s ({txb / t[2] / 8e9:.3f} of 8 TB/s)",
               flush=True)
     del pk, off, ln
     torch.cuda.empty_cache()
