@@ -177,6 +177,7 @@ import rxdist  # noqa: E402
 import rxgpu as R  # noqa: E402
 
 COUNTS = True
+CS_PRIORITY = 0  # torch stream priority of the count stream (--count-stream-priority)
 # above 8192 flows the per-flow counts are two passes after the classify kernel;
 # on a second stream (rxg_classify_dev_cs) they overlap the next step's classify
 COUNT_STREAM = True
@@ -247,7 +248,8 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     # itself and the stream would only add an event per step (~3 us of GPU
     # idle between bursts, r02j)
     use_cs = COUNT_STREAM and COUNTS and nflows >= R.SLAB_MIN_FLOWS
-    cs = torch.cuda.Stream(dev) if (world > 1 or use_cs) else None
+    # (CS_PRIORITY: the count / collective stream at high priority, A/B)
+    cs = torch.cuda.Stream(dev, priority=CS_PRIORITY) if (world > 1 or use_cs) else None
     csh = cs.cuda_stream if use_cs else None
     step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)] if world > 1 else None
     k_ev = [torch.cuda.Event(), torch.cuda.Event()]
@@ -1647,6 +1649,8 @@ def main():
                          "timed steps (0 = none)")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--count-stream-priority", type=int, default=0,
+                    help="torch priority of the count stream (negative = higher; A/B)")
     ap.add_argument("--no-count-stream", action="store_true",
                     help="per-flow counts on the classify stream (rxg_classify_dev), not "
                          "overlapped with the next step (A/B)")
@@ -1746,7 +1750,8 @@ def main():
         ctx.tune_flow_load(a.flow_load)
     if a.tune_tables:
         ctx.tune_tables(a.tune_tables)
-    global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8
+    global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8, CS_PRIORITY
+    CS_PRIORITY = a.count_stream_priority
     V8 = not a.no_v8
     RAMP_MS = a.ramp_ms
     COUNT_STREAM = not a.no_count_stream

@@ -261,6 +261,39 @@ __global__ __launch_bounds__(256) void k_slotbuf(const u32x4 *__restrict__ in, s
     }
 }
 
+// the jumbo shape (cfg5: 1.25M 9000-B frames in 9024-B slots; the stream
+// kernel reads a block's 16 frames as one contiguous span, 1 KiB per wave
+// instruction, and writes their 16 verdicts at the block's end): one block
+// per 16-slot span, U loads per thread in flight; ST: 16 verdict stores (nt)
+// by threads 0..15 after the span; a non-resident grid as the stream kernel's
+template <bool ST, int U>
+__global__ __launch_bounds__(256) void k_span(const u32x4 *__restrict__ in, size_t nslots, size_t slot16,
+                                              u32x4 *__restrict__ out, unsigned *__restrict__ sink) {
+    __shared__ unsigned part[4];
+    const size_t s0 = (size_t)blockIdx.x * 16;
+    const size_t c0 = s0 * slot16, c1 = (s0 + 16 < nslots ? s0 + 16 : nslots) * slot16;
+    unsigned acc = 0;
+    size_t c = c0 + threadIdx.x;
+    for (; c + (U - 1) * 256 < c1; c += U * 256) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ldnt(in + c + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += csum(v[u]);
+    }
+    for (; c < c1; c += 256) acc += csum(ldnt(in + c));
+    for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const unsigned tot = part[0] + part[1] + part[2] + part[3];
+    if (ST) {
+        if (threadIdx.x < 16 && s0 + threadIdx.x < nslots)
+            __builtin_nontemporal_store(u32x4{tot, (unsigned)(s0 + threadIdx.x), 0, 0}, out + s0 + threadIdx.x);
+    } else if (tot == 0x12345678u) {
+        sink[0] = tot;
+    }
+}
+
 // the plain grid-stride read plus one 16-B non-temporal store per 96 chunks
 // (per 1536-B slot), issued by the lane that reads the slot's first chunk
 __global__ __launch_bounds__(256) void k_stream_st(const u32x4 *__restrict__ in, size_t n16,
@@ -359,14 +392,33 @@ int main() {
     const double alg = (double)nslots * (1500 + 22);
     u32x4 *in, *out;
     unsigned *sink;
-    CHK(hipMalloc(&in, bytes));
+    const size_t inbytes = bytes > (size_t)1250000 * 9024 ? bytes : (size_t)1250000 * 9024;
+    CHK(hipMalloc(&in, inbytes));
     CHK(hipMalloc(&out, nslots * 16));
     CHK(hipMalloc(&sink, 64));
-    CHK(hipMemset(in, 1, bytes));
+    CHK(hipMemset(in, 1, inbytes));
     int cu = 0;
     CHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
     const int reps = 20;
     // (the in-flight sweep of r06b: profiles/r06b/membw_cfg3_r06b.txt)
+    // cfg5's span shape with and without its verdict stores (r06)
+    {
+        const size_t nj = 1250000, slot16 = 9024 / 16;
+        if (nj * slot16 * 16 <= inbytes) {
+            const double jb = (double)nj * 9024;
+            for (int round = 0; round < 3; ++round) {
+                float ms;
+#define J(name, launch)                                                                            \
+    ms = timeit([&] { launch; }, reps);                                                            \
+    printf("j%d %-24s %.4f ms %7.0f GB/s (read)\n", round, name, ms, jb / ms / 1e6);
+                J("span U=4 no store", (k_span<false, 4><<<(nj + 15) / 16, 256>>>(in, nj, slot16, out, sink)))
+                J("span U=4 + 16 verdicts", (k_span<true, 4><<<(nj + 15) / 16, 256>>>(in, nj, slot16, out, sink)))
+                J("span U=8 no store", (k_span<false, 8><<<(nj + 15) / 16, 256>>>(in, nj, slot16, out, sink)))
+                J("span U=8 + 16 verdicts", (k_span<true, 8><<<(nj + 15) / 16, 256>>>(in, nj, slot16, out, sink)))
+#undef J
+            }
+        }
+    }
     // the decomposition, interleaved, 3 rounds: which component of the slot
     // shape costs the 0.912 -> 1.042 ms
     for (int round = 0; round < 3; ++round) {
