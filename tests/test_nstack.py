@@ -116,6 +116,18 @@ def test_rx_burst_needs_gpu(ns):
         ns.rx_burst([F.udp_frame("1.1.1.1", 1, L, 2, b"x")])
 
 
+def test_pipelined_receive_needs_gpu(ns):
+    """nstack_rx_submit on a host-only stack: the library refuses the burst
+    (RXG_ENODEV), nothing is left pending, a complete has nothing to
+    deliver (RXG_EINVAL) and host-verdict delivery still works"""
+    ns.socket(R.SOCK_DGRAM)
+    with pytest.raises(R.RxgError):
+        ns.rx_submit([F.udp_frame("1.1.1.1", 1, L, 2, b"x")])
+    assert ns.rx_pending() == 0
+    assert ns.lib.nstack_rx_complete() == -22
+    assert _deliver(ns, [F.udp_frame("1.1.1.1", 1, L, 2, b"x")]) == [-3]
+
+
 def _deliver(ns, frames):
     v = _verdicts(ns, frames)
     rcs = np.zeros(len(frames), np.int32)
