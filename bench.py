@@ -178,6 +178,7 @@ import rxgpu as R  # noqa: E402
 
 COUNTS = True
 CS_PRIORITY = 0  # torch stream priority of the count stream (--count-stream-priority)
+CU_SPLIT = 0  # CUs reserved for the count stream (--cu-split; 0 = shared)
 # above 8192 flows the per-flow counts are two passes after the classify kernel;
 # on a second stream (rxg_classify_dev_cs) they overlap the next step's classify
 COUNT_STREAM = True
@@ -204,6 +205,39 @@ def collective_fn(group, nccl_group, nflows):
             with torch.cuda.stream(cs):
                 torch.distributed.all_reduce(t, group=nccl_group)
     return run
+
+
+def cu_split_streams(dev, n_count):
+    """two streams on disjoint CUs (hipExtStreamCreateWithCUMask): the
+    classify stream on all but n_count CUs, the count stream on those n_count.
+    The slab pass's 1024-thread, 128-KiB-LDS blocks need a CU with nothing
+    else on it, which the next burst's classify never leaves free (DESIGN §6,
+    round 6); CUs of their own let the count of burst k run beside the
+    classify of burst k+1.  Returns (classify stream, count stream) as torch
+    ExternalStreams, and a function that destroys them."""
+    import ctypes as C
+    path = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln][0]
+    hip = C.CDLL(path)  # the HIP runtime this process already uses (torch's, librxgpu's)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    made = []
+
+    def make(lo, hi):
+        m = (C.c_uint32 * words)()
+        for i in range(lo, hi):
+            m[i // 32] |= 1 << (i % 32)
+        h = C.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(words), m)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+        made.append(h)
+        return torch.cuda.ExternalStream(h.value, device=dev)
+
+    def destroy():
+        torch.cuda.synchronize(dev)
+        for h in made:
+            hip.hipStreamDestroy(h)
+    return make(0, ncu - n_count), make(ncu - n_count, ncu), destroy
 
 
 def gather_rank_stats(world, el, steps, stream_ms, ar_ms, n):
@@ -250,6 +284,10 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     use_cs = COUNT_STREAM and COUNTS and nflows >= R.SLAB_MIN_FLOWS
     # (CS_PRIORITY: the count / collective stream at high priority, A/B)
     cs = torch.cuda.Stream(dev, priority=CS_PRIORITY) if (world > 1 or use_cs) else None
+    split_destroy = None
+    if use_cs and CU_SPLIT > 0:  # the count stream on CUs of its own (A/B)
+        stream, cs, split_destroy = cu_split_streams(dev, CU_SPLIT)
+        sh = stream.cuda_stream
     csh = cs.cuda_stream if use_cs else None
     step_counts = [torch.zeros_like(counts), torch.zeros_like(counts)] if world > 1 else None
     k_ev = [torch.cuda.Event(), torch.cuda.Event()]
@@ -446,6 +484,10 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
                                gb_per_s=round(tx_bytes / tms / 1e6, 1),
                                frac=round(tx_bytes / tms / 1e6 / HBM_PEAK_GBS, 4),
                                traffic=pmc_traffic(name, "tx_cksum"))
+    if split_destroy is not None:
+        split_destroy()
+        res["cu_split"] = dict(count_cus=CU_SPLIT, note="count stream on CUs of its own, "
+                               "classify on the rest (hipExtStreamCreateWithCUMask)")
     del pk, off, ln, out
     torch.cuda.empty_cache()
     return res
@@ -1649,6 +1691,9 @@ def main():
                          "timed steps (0 = none)")
     ap.add_argument("--variant", default="", help="force a kernel variant g,p,fpg (tuning)")
     ap.add_argument("--no-counts", action="store_true", help="skip per-flow counting (ablation)")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="slab-count workloads: run the count stream on this many CUs of its own "
+                         "and the classify on the rest (hipExtStreamCreateWithCUMask; 0 = off)")
     ap.add_argument("--count-stream-priority", type=int, default=0,
                     help="torch priority of the count stream (negative = higher; A/B)")
     ap.add_argument("--no-count-stream", action="store_true",
@@ -1750,8 +1795,9 @@ def main():
         ctx.tune_flow_load(a.flow_load)
     if a.tune_tables:
         ctx.tune_tables(a.tune_tables)
-    global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8, CS_PRIORITY
+    global COUNTS, TX, RAMP_MS, COUNT_STREAM, V8, CS_PRIORITY, CU_SPLIT
     CS_PRIORITY = a.count_stream_priority
+    CU_SPLIT = a.cu_split
     V8 = not a.no_v8
     RAMP_MS = a.ramp_ms
     COUNT_STREAM = not a.no_count_stream
