@@ -214,7 +214,10 @@ def cu_split_streams(dev, n_count):
     else on it, which the next burst's classify never leaves free (DESIGN §6,
     round 6); CUs of their own let the count of burst k run beside the
     classify of burst k+1.  Returns (classify stream, count stream) as torch
-    ExternalStreams, and a function that destroys them."""
+    ExternalStreams.  The streams live for the rest of the process (torch's
+    allocator keeps them in its records of the tensors they used).
+    n_count > 0: the count CUs spread one per 32-CU group (an XCD of MI355X,
+    as HIP numbers CUs); n_count < 0: the last |n_count| CUs."""
     import ctypes as C
     path = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln][0]
     hip = C.CDLL(path)  # the HIP runtime this process already uses (torch's, librxgpu's)
@@ -222,9 +225,15 @@ def cu_split_streams(dev, n_count):
     words = (ncu + 31) // 32
     made = []
 
-    def make(lo, hi):
+    if n_count > 0:  # spread: CU 32g + 31 - j of group g, round robin
+        groups = max(1, ncu // 32)
+        count_cus = {32 * (j % groups) + 31 - j // groups for j in range(n_count)}
+    else:
+        count_cus = set(range(ncu + n_count, ncu))
+
+    def make(cus):
         m = (C.c_uint32 * words)()
-        for i in range(lo, hi):
+        for i in cus:
             m[i // 32] |= 1 << (i % 32)
         h = C.c_void_p()
         rc = hip.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(words), m)
@@ -233,11 +242,9 @@ def cu_split_streams(dev, n_count):
         made.append(h)
         return torch.cuda.ExternalStream(h.value, device=dev)
 
-    def destroy():
-        torch.cuda.synchronize(dev)
-        for h in made:
-            hip.hipStreamDestroy(h)
-    return make(0, ncu - n_count), make(ncu - n_count, ncu), destroy
+    cls = make(sorted(set(range(ncu)) - count_cus))
+    cnt = make(sorted(count_cus))
+    return cls, cnt, lambda: torch.cuda.synchronize(dev)
 
 
 def gather_rank_stats(world, el, steps, stream_ms, ar_ms, n):
@@ -285,7 +292,7 @@ def run_workload(name, ctx, rank, world, steps, warmup, dev, coll=None, parity_s
     # (CS_PRIORITY: the count / collective stream at high priority, A/B)
     cs = torch.cuda.Stream(dev, priority=CS_PRIORITY) if (world > 1 or use_cs) else None
     split_destroy = None
-    if use_cs and CU_SPLIT > 0:  # the count stream on CUs of its own (A/B)
+    if use_cs and CU_SPLIT != 0:  # the count stream on CUs of its own (A/B)
         stream, cs, split_destroy = cu_split_streams(dev, CU_SPLIT)
         sh = stream.cuda_stream
     csh = cs.cuda_stream if use_cs else None
