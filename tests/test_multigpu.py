@@ -120,11 +120,14 @@ def test_two_contexts_classify_the_shards_of_one_burst(torch_dev):
 
 
 def test_rccl_group_one_rank(torch_dev):
-    """rxg_group over one GPU: the all-reduce is the identity (sum over one
-    rank), through the same ncclAllReduce call the N-GPU bench makes"""
+    """rxg_group over one GPU: the communicator reports one rank
+    (rxg_group_size, which the N-GPU bench line carries as rccl_nranks), and
+    the all-reduce is the identity (sum over one rank), through the same
+    ncclAllReduce call the N-GPU bench makes"""
     torch, dev = torch_dev
     g = R.Group(0, 1, 0, R.group_id())
     try:
+        assert g.size() == (1, 0)  # rxg_group_size: what the communicator reports
         x = torch.arange(5000, dtype=torch.int64, device=dev) * 3
         y = x.clone()
         g.allreduce(y, 5000, stream=torch.cuda.current_stream(dev).cuda_stream)
