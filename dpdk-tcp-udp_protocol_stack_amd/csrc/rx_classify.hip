@@ -3061,6 +3061,12 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 108, launch_lane<0, 8>},     {1, 4, 1, 113, launch_lane<0, 13>},
     {1, 4, 1, 201, launch_lane<0, 1, true, false>, 6}, {1, 4, 1, 204, launch_lane<0, 4, true, false>, 6},
     {1, 4, 1, 213, launch_lane<0, 13, true, false>, 6},
+    // the 64-B default (pipe 14) with the same ablations (round 6): 1401 no
+    // probe, 1404 no verdict store, 1408 no checksum arithmetic, 1413 = all three
+    {1, 4, 1, 1401, launch_lane_udpc<14, 1, true, false>, 2},
+    {1, 4, 1, 1404, launch_lane_udpc<14, 4, true, false>, 2},
+    {1, 4, 1, 1408, launch_lane_udpc<14, 8, true, false>, 2},
+    {1, 4, 1, 1413, launch_lane_udpc<14, 13, true, false>, 2},
     // stream kernel: no flow probe (130); pipe 46 (span from the descriptors)
     // and its ablations: no probe (146), no tail stream (246), no head loads
     // (446), neither heads nor stream (646); pipe 38: no head loads (438), no
