@@ -754,14 +754,16 @@ def test_group_hist16_edge(ctx, torch_dev, variant, extra):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("tables", [R.TT_SLAB_HALF, R.TT_SLAB_QUARTER, R.TT_SLAB_HALF | R.TT_COUNT_4B])
+@pytest.mark.parametrize("tables", [R.TT_SLAB_HALF, R.TT_SLAB_QUARTER, R.TT_SLAB_HALF | R.TT_COUNT_4B,
+                                    R.TT_COUNT_6BUF, R.TT_COUNT_2BUF])
 @pytest.mark.parametrize("nu", [65536, 200000])
 def test_count_slab_geometry(ctx, torch_dev, nu, tables):
     """the slab pass on half / a quarter of the CUs (rxg_tune_tables
     RXG_TT_SLAB_HALF / _QUARTER: fewer, larger slabs): frames to 5000 random
     sockets of 65536 (2-B indices, flow 65535 among them) or 200000 (4 ranges),
     the per-flow counts equal to the frames sent, with and without the count
-    stream"""
+    stream (eight bursts: around the two-, three- or six-buffer index ring
+    more than once, RXG_TT_COUNT_2BUF / _6BUF)"""
     torch, dev = torch_dev
     udp = _udp_socks(nu)
     rng = np.random.default_rng(nu + tables)
@@ -786,12 +788,12 @@ def test_count_slab_geometry(ctx, torch_dev, nu, tables):
         d_cnt = torch.zeros(nu, dtype=torch.int64, device=dev)
         cs = torch.cuda.Stream(dev)
         st = torch.cuda.current_stream(dev)
-        for _ in range(3):
+        for _ in range(8):
             ctx.classify_dev(d_pk, d_off, d_ln, len(off), 6, 64, d_out, d_cnt, stream=st.cuda_stream,
                              count_stream=cs.cuda_stream)
         st.wait_stream(cs)
         torch.cuda.synchronize(dev)
-        assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 3 * want), (nu, tables, "cs")
+        assert np.array_equal(d_cnt.cpu().numpy().view(np.uint64), 8 * want), (nu, tables, "cs")
     finally:
         ctx.tune_tables(0)
     assert np.all(got["rc"] == 0)

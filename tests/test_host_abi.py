@@ -226,3 +226,16 @@ def test_generator_rss_sharding(nsh):
             sp, dp = (int.from_bytes(b[34:36], "little"), int.from_bytes(b[36:38], "little")) \
                 if proto[k] in (6, 17) else (0, 0)
             assert O.rss_hash(sip, dip, sp, dp) % nsh == shard
+
+
+def test_tune_tables_flags():
+    """rxg_tune_tables takes every documented flag alone, refuses unknown bits
+    and the two- and six-buffer count rings together"""
+    with R.Context(R.HOST_ONLY) as c:
+        for f in (0, R.TT_NO_UDP_PORT, R.TT_COUNT_4B, R.TT_COUNT_2BUF, R.TT_SLAB_HALF,
+                  R.TT_SLAB_QUARTER, R.TT_COUNT_6BUF, R.TT_SLAB_HALF | R.TT_COUNT_6BUF):
+            c.tune_tables(f)
+        for f in (R.TT_COUNT_2BUF | R.TT_COUNT_6BUF, 0x40, 0x80000000):
+            with pytest.raises(R.RxgError):
+                c.tune_tables(f)
+        c.tune_tables(0)
