@@ -200,7 +200,7 @@ struct rxg_ctx {
         hipEvent_t ev = nullptr;
         hipStream_t st = nullptr;
         bool used = false;
-    } wu[7]; // index buffers 0..5, slabs (WS_*)
+    } wu[4]; // index buffers 0..2, slabs (WS_*)
     // region offsets depend on the burst shape (frame count, binned path, size);
     // a change of shape waits on every region
     struct ws_shape {
@@ -210,7 +210,7 @@ struct rxg_ctx {
         bool operator!=(const ws_shape &o) const { return n != o.n || lists != o.lists || bytes != o.bytes; }
     } ws_layout;
     uint32_t ws_flip = 0; // index buffer of the next split-stream burst
-    uint32_t ws_nbuf = 3; // index buffers of the split-stream bursts (RXG_TT_COUNT_2BUF: 2, _6BUF: 6)
+    uint32_t ws_nbuf = 3; // index buffers of the split-stream bursts (RXG_TT_COUNT_2BUF: 2)
     hipEvent_t ev_k1 = nullptr; // split-stream burst: classify done (count stream waits on it)
     void *d_aux = nullptr; // RSS split / gather workspace, grown on demand
     size_t d_aux_cap = 0;
@@ -1123,13 +1123,12 @@ int rxg_tune_tx(rxg_ctx *c, uint32_t variant, uint32_t blocks_per_cu) {
 
 int rxg_tune_tables(rxg_ctx *c, uint32_t flags) {
     if (!c || (flags & ~(uint32_t)(RXG_TT_NO_UDP_PORT | RXG_TT_COUNT_4B | RXG_TT_COUNT_2BUF |
-                                   RXG_TT_SLAB_HALF | RXG_TT_SLAB_QUARTER | RXG_TT_COUNT_6BUF)) ||
-        ((flags & RXG_TT_COUNT_2BUF) && (flags & RXG_TT_COUNT_6BUF)))
+                                   RXG_TT_SLAB_HALF | RXG_TT_SLAB_QUARTER)))
         return RXG_EINVAL;
     c->tune_tables = flags;
     c->ft.count_4b = (flags & RXG_TT_COUNT_4B) ? 1u : 0u;
     c->ft.slab_div_log2 = (flags & RXG_TT_SLAB_QUARTER) ? 2u : (flags & RXG_TT_SLAB_HALF) ? 1u : 0u;
-    c->ws_nbuf = (flags & RXG_TT_COUNT_2BUF) ? 2u : (flags & RXG_TT_COUNT_6BUF) ? 6u : 3u;
+    c->ws_nbuf = (flags & RXG_TT_COUNT_2BUF) ? 2u : 3u;
     return RXG_OK;
 }
 
@@ -1215,7 +1214,7 @@ uint32_t rxg_rss_hash(uint32_t sip, uint32_t dip, uint16_t sport, uint16_t dport
 }
 
 // workspace regions (rxg_ctx::wu)
-enum { WS_BUF0 = 0, WS_SLAB = 6 }; // index buffers 0..5
+enum { WS_BUF0 = 0, WS_BUF1 = 1, WS_BUF2 = 2, WS_SLAB = 3 };
 
 static hipError_t ws_wait(rxg_ctx *c, int r, hipStream_t s) {
     const rxg_ctx::ws_use &u = c->wu[r];
@@ -1242,7 +1241,7 @@ static int ws_prepare(rxg_ctx *c, size_t ws, const rxg_ctx::ws_shape &layout, hi
         int rc = ensure_dev_async((void **)&c->d_ws, &c->d_ws_cap, ws, s);
         if (rc) return rc;
     } else if (layout != c->ws_layout) {
-        for (int r = 0; r <= WS_SLAB; ++r) HIPCHK(ws_wait(c, r, s));
+        for (int r = 0; r < 4; ++r) HIPCHK(ws_wait(c, r, s));
     }
     c->ws_layout = layout;
     return RXG_OK;

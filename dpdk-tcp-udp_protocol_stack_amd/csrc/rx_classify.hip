@@ -2743,230 +2743,6 @@ __global__ __launch_bounds__(1024) void rx_count_slab_kernel(const T *__restrict
                                                               uint32_t words, uint32_t nflows,
                                                               uint32_t *__restrict__ slab,
                                                               unsigned long long *__restrict__ counts) {
-    constexpr uint32_t E = 16 / sizeof(T); // indices per 16-B piece
-    constexpr int U = 8;                   // pieces per thread per trip
-    constexpr uint64_t TRIP = (uint64_t)E * U * 1024;
-    // blockIdx.y = flow range: flows [y * 65536, y * 65536 + lim)
-    __shared__ uint4 bins4[SLAB_MAX_FLOWS / 8];
-    __shared__ uint32_t tally, sum;
-    uint32_t *bins = reinterpret_cast<uint32_t *>(bins4);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t f0 = blockIdx.y * SLAB_MAX_FLOWS;
-    const uint32_t lim = min(nflows - f0, SLAB_MAX_FLOWS);
-    const uint64_t b0 = (uint64_t)blockIdx.x * per;
-    const uint64_t b1 = min((uint64_t)n, b0 + per);
-    // A trip's U pieces are loaded unconditionally (a piece at or past b1
-    // re-reads the block's first one and counts nothing), so the compiler's
-    // wait before a trip's counting leaves the next trip's loads in flight.
-    // A piece that starts before b1 may reach past it (never past the buffer:
-    // 16 B x ceil(n / E) fits the 4 B per frame it holds); its indices at or
-    // past b1 belong to the next slab, or are no frame, and are masked.
-    auto issue = [&](uint64_t bs, uint4 (&v)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t k = bs + (uint64_t)E * ((uint32_t)u * 1024u + tid);
-            v[u] = ldg16<true>(reinterpret_cast<const uint8_t *>(cidx + (k < b1 ? k : b0)));
-        }
-    };
-    uint32_t mine = 0;
-    // a 2-B all-ones index is never counted here: with fewer than 65536 flows
-    // it is no flow, and with exactly 65536 flow 65535 was counted by the
-    // classify kernel (rx_ft_dev::count_ffff)
-    auto count = [&](uint32_t x, bool in) {
-        if constexpr (sizeof(T) == 2)
-            if (x == 0xFFFFu) in = false;
-        const uint32_t f = x - f0; // other ranges: f >= lim
-        if (in && f < lim) {
-            atomicAdd(&bins[f >> 1], 1u << (16u * (f & 1u)));
-            ++mine;
-        }
-    };
-    auto consume = [&](uint64_t bs, const uint4 (&v)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t k = bs + (uint64_t)E * ((uint32_t)u * 1024u + tid);
-            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if constexpr (sizeof(T) == 2) {
-                    count(w[j] & 0xFFFFu, k + 2 * j < b1);
-                    count(w[j] >> 16, k + 2 * j + 1 < b1);
-                } else {
-                    count(w[j], k + j < b1);
-                }
-            }
-        }
-    };
-    uint4 a[U], c[U];
-    issue(b0, a); // in flight while the bins are cleared
-    for (uint32_t k = tid; k < words / 4; k += 1024) bins4[k] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) tally = sum = 0;
-    __syncthreads();
-    for (uint64_t base = b0; base < b1;) { // block-uniform trips, two per iteration
-        issue(base + TRIP, c);
-        consume(base, a);
-        base += TRIP;
-        if (base >= b1) break;
-        issue(base + TRIP, a);
-        consume(base, c);
-        base += TRIP;
-    }
-    if (mine) atomicAdd(&tally, mine);
-    __syncthreads();
-    // write the slab (16-B non-temporal pieces: 32 MiB of slabs through the
-    // L2 would evict the flow tables the next burst's classify probes) and
-    // add up its bins in the same pass; words is a multiple of 4 (slab_words)
-    rx_u32x4 *dst = reinterpret_cast<rx_u32x4 *>(slab + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * words);
-    uint32_t part = 0;
-    for (uint32_t k = tid; k < words / 4; k += 1024) {
-        const uint4 x = bins4[k];
-        part += (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) + (x.z & 0xFFFFu) +
-                (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
-        const rx_u32x4 xv = {x.x, x.y, x.z, x.w};
-        st_stream16(dst + k, xv);
-    }
-    if (part) atomicAdd(&sum, part);
-    __syncthreads();
-    // A bin wrapped (more than 65535 of the block's frames to one flow: the
-    // bins' sum falls short of the tally; block-uniform, pathological traffic
-    // only): the block zeroes its slab (each thread the pieces it wrote, so
-    // the zero lands after them) and adds its frames with global atomics.
-    if (sum != tally) {
-        const rx_u32x4 z = {0u, 0u, 0u, 0u};
-        for (uint32_t k = tid; k < words / 4; k += 1024) st_stream16(dst + k, z);
-        for (uint64_t k = b0 + tid; k < b1; k += 1024) {
-            uint32_t x = cidx[k];
-            if constexpr (sizeof(T) == 2)
-                if (x == 0xFFFFu) continue;
-            const uint32_t f = x - f0;
-            if (f < lim) atomicAdd(&counts[(uint64_t)f0 + f], 1ull);
-        }
-    }
-}
-
-// block = 64 lanes x 4 bin pairs (one 16-B column piece per lane) x 16 waves,
-// wave w summing slabs w, w + 16, ... with up to 16 loads in flight (every
-// slab of the default 256-slab geometry in one trip); the 16 partial sums
-// meet in LDS.  words is a multiple of 4 (slab_words).  (Splitting the slabs
-// over 4x the blocks, adding with u64 atomics, was 7 us slower at cfg4:
-// profiles/r02f/ab_count_paths.txt.)  One block per CU is all the grid has
-// (128 blocks at one range), so the register budget is the 1024-thread one
-// (waves_per_eu 4): the compiler otherwise aims for two blocks per CU and
-// keeps only 8 of the 16 loads in flight.
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
-                                                                uint32_t nslabs, uint32_t words,
-                                                                uint32_t nflows,
-                                                                unsigned long long *__restrict__ counts) {
-    __shared__ uint4 part[2][16][64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    // blockIdx.y = flow range (its slabs, its 65536 counts)
-    slab += (uint64_t)blockIdx.y * nslabs * words;
-    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
-    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
-    const uint32_t w = (blockIdx.x * 64 + lane) * 4; // first of this lane's 4 words
-    const uint32_t wc = w < words ? w : 0;
-    uint4 lo = make_uint4(0, 0, 0, 0), hi = lo;
-    auto add = [&](uint4 x) {
-        lo.x += x.x & 0xFFFFu, hi.x += x.x >> 16;
-        lo.y += x.y & 0xFFFFu, hi.y += x.y >> 16;
-        lo.z += x.z & 0xFFFFu, hi.z += x.z >> 16;
-        lo.w += x.w & 0xFFFFu, hi.w += x.w >> 16;
-    };
-    auto ld = [&](uint32_t b) {
-        return ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)b * words + wc));
-    };
-    uint32_t b = wv;
-    for (; b + 16 * 15 < nslabs; b += 16 * 16) {
-        uint4 x[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) x[u] = ld(b + 16 * u);
-        __builtin_amdgcn_sched_barrier(0); // every load issued before the first add
-#pragma unroll
-        for (int u = 0; u < 16; ++u) add(x[u]);
-    }
-    for (; b + 16 * 3 < nslabs; b += 16 * 4) {
-        uint4 x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = ld(b + 16 * u);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) add(x[u]);
-    }
-    for (; b < nslabs; b += 16) add(ld(b));
-    part[0][wv][lane] = lo;
-    part[1][wv][lane] = hi;
-    __syncthreads();
-    if (wv == 0 && w < words) {
-        lo = hi = make_uint4(0, 0, 0, 0);
-#pragma unroll 4 // (fully unrolled it spilled 8 VGPRs at the 1024-thread budget)
-        for (int k = 0; k < 16; ++k) {
-            const uint4 a = part[0][k][lane], c = part[1][k][lane];
-            lo.x += a.x, lo.y += a.y, lo.z += a.z, lo.w += a.w;
-            hi.x += c.x, hi.y += c.y, hi.z += c.z, hi.w += c.w;
-        }
-        const uint32_t l[4] = {lo.x, lo.y, lo.z, lo.w}, h[4] = {hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t f = 2 * (w + k);
-            if (l[k] && f < nflows) counts[f] += l[k];
-            if (h[k] && f + 1 < nflows) counts[f + 1] += h[k];
-        }
-    }
-}
-
-// few slabs (the multi-range geometry): one thread per 4 bin pairs sums every
-// slab of its range, 16 loads in flight; 256-thread blocks of 1024 pairs
-__global__ __launch_bounds__(256) void rx_count_reduce_few_kernel(
-    const uint32_t *__restrict__ slab, uint32_t nslabs, uint32_t words, uint32_t nflows,
-    unsigned long long *__restrict__ counts) {
-    slab += (uint64_t)blockIdx.y * nslabs * words;
-    counts += (uint64_t)blockIdx.y * SLAB_MAX_FLOWS;
-    nflows -= blockIdx.y * SLAB_MAX_FLOWS;
-    const uint32_t w = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (w >= words) return;
-    uint32_t l[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0};
-    auto add = [&](uint4 x) {
-        l[0] += x.x & 0xFFFFu, h[0] += x.x >> 16;
-        l[1] += x.y & 0xFFFFu, h[1] += x.y >> 16;
-        l[2] += x.z & 0xFFFFu, h[2] += x.z >> 16;
-        l[3] += x.w & 0xFFFFu, h[3] += x.w >> 16;
-    };
-    auto ld = [&](uint32_t b) {
-        return ldg16<true>(reinterpret_cast<const uint8_t *>(slab + (uint64_t)b * words + w));
-    };
-    uint32_t b = 0;
-    for (; b + 16 <= nslabs; b += 16) {
-        uint4 x[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) x[u] = ld(b + u);
-#pragma unroll
-        for (int u = 0; u < 16; ++u) add(x[u]);
-    }
-    for (; b + 4 <= nslabs; b += 4) {
-        uint4 x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = ld(b + u);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) add(x[u]);
-    }
-    for (; b < nslabs; ++b) add(ld(b));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t f = 2 * (w + k);
-        if (l[k] && f < nflows) counts[f] += l[k];
-        if (h[k] && f + 1 < nflows) counts[f + 1] += h[k];
-    }
-}
-
-#if RX_COUNT_V1
-// A/B build only (librxgpu_cv1.so, RX_COUNT_V1=1): the round-5 count passes
-// (four index loads per trip, no prefetch across the bin clearing, 4-B slab
-// stores in a pass of their own; 4 / 8 reduce loads in flight)
-template <typename T> // count index: uint16_t (one range, <= 65536 flows) or uint32_t
-__global__ __launch_bounds__(1024) void rx_count_slab_v1_kernel(const T *__restrict__ cidx,
-                                                              uint32_t n, uint32_t per,
-                                                              uint32_t words, uint32_t nflows,
-                                                              uint32_t *__restrict__ slab,
-                                                              unsigned long long *__restrict__ counts) {
     constexpr uint32_t E = 16 / sizeof(T); // indices per 16-B load
     // blockIdx.y = flow range: flows [y * 65536, y * 65536 + lim)
     __shared__ uint32_t bins[SLAB_MAX_FLOWS / 2];
@@ -3042,7 +2818,7 @@ __global__ __launch_bounds__(1024) void rx_count_slab_v1_kernel(const T *__restr
 // sums meet in LDS.  words is a multiple of 4 (slab_words).  (Splitting the
 // slabs over 4x the blocks, adding with u64 atomics, was 7 us slower at cfg4:
 // profiles/r02f/ab_count_paths.txt.)
-__global__ __launch_bounds__(1024) void rx_count_reduce_v1_kernel(const uint32_t *__restrict__ slab,
+__global__ __launch_bounds__(1024) void rx_count_reduce_kernel(const uint32_t *__restrict__ slab,
                                                                 uint32_t nslabs, uint32_t words,
                                                                 uint32_t nflows,
                                                                 unsigned long long *__restrict__ counts) {
@@ -3095,7 +2871,7 @@ __global__ __launch_bounds__(1024) void rx_count_reduce_v1_kernel(const uint32_t
 
 // few slabs (the multi-range geometry): one thread per 4 bin pairs sums every
 // slab of its range, 8 loads in flight; 256-thread blocks of 1024 pairs
-__global__ __launch_bounds__(256) void rx_count_reduce_few_v1_kernel(
+__global__ __launch_bounds__(256) void rx_count_reduce_few_kernel(
     const uint32_t *__restrict__ slab, uint32_t nslabs, uint32_t words, uint32_t nflows,
     unsigned long long *__restrict__ counts) {
     slab += (uint64_t)blockIdx.y * nslabs * words;
@@ -3132,8 +2908,6 @@ __global__ __launch_bounds__(256) void rx_count_reduce_few_v1_kernel(
         if (h[k] && f + 1 < nflows) counts[f + 1] += h[k];
     }
 }
-
-#endif
 
 // Flows above 65536: the count is split into ranges of 65536 flows
 // (blockIdx.y), each range's blocks scanning every index; up to
@@ -3176,31 +2950,22 @@ static hipError_t launch_count_slab(const void *cidx, uint32_t n, const rx_ft_de
     const uint32_t nr = slab_ranges(ft), words = slab_words(ft), nf = ft.nu + ft.nt;
     uint32_t nslabs, per;
     slab_geometry(n, nr, &nslabs, &per, ft.slab_div_log2);
-#if RX_COUNT_V1
-    auto slab16 = rx_count_slab_v1_kernel<uint16_t>;
-    auto slab32 = rx_count_slab_v1_kernel<uint32_t>;
-    auto reduce = rx_count_reduce_v1_kernel;
-    auto reduce_few = rx_count_reduce_few_v1_kernel;
-#else
-    auto slab16 = rx_count_slab_kernel<uint16_t>;
-    auto slab32 = rx_count_slab_kernel<uint32_t>;
-    auto reduce = rx_count_reduce_kernel;
-    auto reduce_few = rx_count_reduce_few_kernel;
-#endif
     if (ft.cidx16)
-        hipLaunchKernelGGL(slab16, dim3(nslabs, nr), dim3(1024), 0, s,
-                           static_cast<const uint16_t *>(cidx), n, per, words, nf, slab, counts);
+        hipLaunchKernelGGL(rx_count_slab_kernel<uint16_t>, dim3(nslabs, nr), dim3(1024), 0, s,
+                           static_cast<const uint16_t *>(cidx), n, per, words, nf,
+                           slab, counts);
     else
-        hipLaunchKernelGGL(slab32, dim3(nslabs, nr), dim3(1024), 0, s,
-                           static_cast<const uint32_t *>(cidx), n, per, words, nf, slab, counts);
+        hipLaunchKernelGGL(rx_count_slab_kernel<uint32_t>, dim3(nslabs, nr), dim3(1024), 0, s,
+                           static_cast<const uint32_t *>(cidx), n, per, words, nf,
+                           slab, counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (nslabs <= 64)
-        hipLaunchKernelGGL(reduce_few, dim3((words / 4 + 255) / 256, nr), dim3(256), 0, s, slab,
-                           nslabs, words, nf, counts);
+        hipLaunchKernelGGL(rx_count_reduce_few_kernel, dim3((words / 4 + 255) / 256, nr), dim3(256),
+                           0, s, slab, nslabs, words, nf, counts);
     else
-        hipLaunchKernelGGL(reduce, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0, s, slab, nslabs,
-                           words, nf, counts);
+        hipLaunchKernelGGL(rx_count_reduce_kernel, dim3((words / 4 + 63) / 64, nr), dim3(1024), 0,
+                           s, slab, nslabs, words, nf, counts);
     return hipGetLastError();
 }
 

@@ -200,7 +200,6 @@ TT_COUNT_4B = 0x2
 TT_COUNT_2BUF = 0x4
 TT_SLAB_HALF = 0x8     # the slab pass on half / a quarter of the CUs (fewer, larger slabs)
 TT_SLAB_QUARTER = 0x10
-TT_COUNT_6BUF = 0x20   # six count-index buffers in the count-stream ring (A/B)
 TX_AUTO = 0xFFFFFFFF
 _lk_udp = _sig("rxg_ft_lookup_udp", _u32, _vp, _u32, _u16)
 _lk_tcp = _sig("rxg_ft_lookup_tcp", _u32, _vp, _u32, _u32, _u16, _u16)

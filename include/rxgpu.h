@@ -526,8 +526,6 @@ int rxg_tune_flow_load(rxg_ctx *ctx, uint32_t load_log2);
                                   burst before the previous one) */
 #define RXG_TT_SLAB_HALF 0x8u     /* the count's slab pass on half / a quarter of the CUs */
 #define RXG_TT_SLAB_QUARTER 0x10u /* (fewer, larger slabs; applied at once) */
-#define RXG_TT_COUNT_6BUF 0x20u   /* rxg_classify_dev_cs: six count-index buffers (A/B of
-                                     the ring depth; not with RXG_TT_COUNT_2BUF) */
 
 int rxg_tune_tables(rxg_ctx *ctx, uint32_t flags);
 

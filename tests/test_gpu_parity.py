@@ -755,15 +755,15 @@ def test_group_hist16_edge(ctx, torch_dev, variant, extra):
 
 
 @pytest.mark.parametrize("tables", [R.TT_SLAB_HALF, R.TT_SLAB_QUARTER, R.TT_SLAB_HALF | R.TT_COUNT_4B,
-                                    R.TT_COUNT_6BUF, R.TT_COUNT_2BUF])
+                                    R.TT_COUNT_2BUF])
 @pytest.mark.parametrize("nu", [65536, 200000])
 def test_count_slab_geometry(ctx, torch_dev, nu, tables):
     """the slab pass on half / a quarter of the CUs (rxg_tune_tables
     RXG_TT_SLAB_HALF / _QUARTER: fewer, larger slabs): frames to 5000 random
     sockets of 65536 (2-B indices, flow 65535 among them) or 200000 (4 ranges),
     the per-flow counts equal to the frames sent, with and without the count
-    stream (eight bursts: around the two-, three- or six-buffer index ring
-    more than once, RXG_TT_COUNT_2BUF / _6BUF)"""
+    stream (eight bursts: around the two- or three-buffer index ring more
+    than once, RXG_TT_COUNT_2BUF)"""
     torch, dev = torch_dev
     udp = _udp_socks(nu)
     rng = np.random.default_rng(nu + tables)
