@@ -3048,6 +3048,14 @@ static const variant_entry k_variants[] = {
     // ... with a 16-bit histogram (half its LDS): WB 16 / 32 (24: pipe 48, the default)
     {8, 2, 2, 47, launch_v<8, 2, 2, 0, true, 0, 1, true, 16, true>},
     {8, 2, 2, 49, launch_v<8, 2, 2, 0, true, 0, 1, true, 32, true>},
+    // ... five blocks per CU: pipe 48 needs 103 VGPRs and 32,784 B of LDS at
+    // 4097 flows (both just above a fifth of the CU), so it runs 4 per CU.
+    // WB 23 / 20 with the register budget of 5 blocks (MINW 5: <= 96 VGPRs)
+    // fit 5; WB 23 at 4 blocks isolates the batch depth
+    {8, 2, 2, 50, launch_v<8, 2, 2, 0, true, 0, 5, true, 23, true>},
+    {8, 2, 2, 51, launch_v<8, 2, 2, 0, true, 0, 5, true, 20, true>},
+    {8, 2, 2, 52, launch_v<8, 2, 2, 0, true, 0, 1, true, 23, true>},
+    {8, 2, 2, 53, launch_v<8, 2, 2, 0, true, 0, 5, true, 16, true>},
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>}, // heads gathered 4 lanes/head
     {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>},              // 12-KiB tiles
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},        // partial sums in the stream
