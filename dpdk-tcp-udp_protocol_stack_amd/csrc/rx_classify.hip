@@ -873,6 +873,78 @@ __device__ __forceinline__ uint4 lane_verdict(lane_frame &L, lane_frame *next, c
     return v;
 }
 
+// The common case of lane_verdict in straight-line code (LDS tables with a
+// port window): every lane of the wave invalid, or not TCP, with its checksum
+// span ending exactly at byte 64 when it has one, and, when UDP, decided by the
+// port window (dip == udp_dip) or by the absence of other keys.  Returns false
+// (wave-uniform) when some lane is not such a frame; the caller then runs
+// lane_verdict, whose result for these lanes this one equals field by field
+// (the same parse, class, checksum, probe and verdict rules, computed with
+// selects: lane_verdict's nested per-lane branches cost about as many scalar
+// mask instructions as vector ones, and the kernel is issue-bound once the
+// bytes are in flight: profiles/r06aa).
+__device__ __forceinline__ bool lane_verdict_fast(lane_frame &L, const rx_ft_dev &ft, uint4 *vout,
+                                                  uint32_t *count_idx, const uint16_t *lw) {
+    const int32_t cp = L.cap;
+    if (cp < 64) { // bytes past caplen read as 0 (rare: runts)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.c[j] = chunk_below(L.c[j], 16 * j, cp);
+    }
+    const uint4 c0 = L.c[0], c1 = L.c[1], c2 = L.c[2], c3 = L.c[3];
+    const uint32_t et = c0.w & 0xFFFFu;
+    const uint32_t tl = rx_bswap16(c1.x & 0xFFFFu);
+    const uint32_t proto = c1.y >> 24;
+    const uint32_t dip = (c1.w >> 16) | (c2.x << 16);
+    const uint32_t dport = c2.y & 0xFFFFu;
+    const uint32_t dgl = rx_bswap16(c2.y >> 16);
+    const bool is_ip = et == 0x0008u, is_arp = et == 0x0608u;
+    const bool is_udp = is_ip && proto == 17u, is_tcp = is_ip && proto == 6u;
+    const uint32_t l4n = tl >= 20u ? tl - 20u : 0u;
+    const bool do_sum = is_udp && tl >= 20u; // (no TCP lane on this path)
+    const int32_t e = min(34 + (int32_t)l4n, cp);
+    const bool win_key = dip == ft.udp_dip;
+    const bool fast = !L.valid || (!is_tcp && (!do_sum || e == 64) &&
+                                   (!is_udp || win_key || ft.udpc_other == 0u));
+    if (ft.udpw_n == 0u || __ballot(!fast) != 0ull) return false; // wave-uniform
+
+    const uint32_t cl = is_arp ? RXG_CLS_ARP
+                               : (!is_ip ? RXG_CLS_NON_IP
+                                         : (is_udp ? RXG_CLS_UDP : RXG_CLS_IPV4_OTHER));
+    uint32_t nd = (is_arp || is_udp) ? 42u : (is_ip ? 24u : 14u);
+    if (is_udp && 34u + l4n > nd) nd = 34u + l4n;
+    // the checksum words [26, 64) in two independent chains (no dependent
+    // v_dot2 back to back), field at 40 read as 0
+    const uint32_t a0 = add_halves(add_halves(add_halves(0u, c1.z & 0xFFFF0000u), c2.x), c2.z & 0xFFFF0000u);
+    const uint32_t a1 = add_halves(add_halves(add_halves(0u, c1.w), c2.y), c2.w);
+    const uint32_t a2 = add_halves(add_halves(a0, c3.x), c3.z);
+    const uint32_t a3 = add_halves(add_halves(a1, c3.y), c3.w);
+    uint32_t ck = (~fold16(a2 + a3 + (proto << 8) + rx_bswap16(l4n))) & 0xFFFFu;
+    if (ck == 0u) ck = 0xFFFFu; // UDP
+    ck = do_sum ? ck : 0u;
+    const uint32_t stored = is_udp ? (c2.z & 0xFFFFu) : 0u;
+    const bool ok = is_udp && stored == ck;
+    // the port window (one LDS read per lane, from entry 0 when not needed)
+    const bool probe = L.valid && is_udp;
+    const uint32_t k = rx_bswap16(dport) - ft.udpw_lo;
+    const bool in_win = probe && win_key && k < ft.udpw_n;
+    const uint32_t we = lw[in_win ? k : 0u];
+    const uint32_t flow = (in_win && we != 0xFFFFu) ? we : RXG_FLOW_NONE;
+    const int32_t rc = is_udp ? (flow == RXG_FLOW_NONE ? RXG_RC_UDP_NO_SOCKET
+                                                       : (dgl <= 8u ? RXG_RC_UDP_NOMEM : RXG_RC_OK))
+                              : RXG_RC_KNI;
+    const uint32_t plen = (is_udp && dgl > 8u) ? dgl - 8u : 0u;
+    if (rc == RXG_RC_OK && 42u + plen > nd) nd = 42u + plen;
+    const uint32_t flags = ((is_udp && dgl <= 8u) ? RXG_F_UDP_SHORT : 0u) | ((int32_t)nd > cp ? RXG_F_TRUNC : 0u);
+    uint4 v;
+    v.x = flow;
+    v.y = (is_udp ? 42u : 0u) | (plen << 16);
+    v.z = ck | (cl << 16) | (((uint32_t)rc & 0xFFu) << 24);
+    v.w = (ok ? 1u : 0u) | (flags << 8) | (stored << 16);
+    *vout = v;
+    *count_idx = (L.valid && rc == RXG_RC_OK && flow != RXG_FLOW_NONE) ? flow : 0xFFFFFFFFu;
+    return true;
+}
+
 __device__ __forceinline__ void lane_count(uint32_t idx, unsigned long long *__restrict__ counts,
                                            uint32_t *hist, uint32_t lds_bins) {
     if (counts && idx != 0xFFFFFFFFu) {
@@ -926,14 +998,17 @@ __device__ __forceinline__ void lane_store(const rx_ft_dev &ft, uint4 *__restric
 }
 
 // the original one-shot form: verdict, store, count
-template <int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false>
+// LEAN (PIPE 16): lane_verdict_fast first, lane_verdict for the waves it declines
+template <int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false, bool LEAN = false>
 __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
                                              const rx_ft_dev &ft, uint4 *__restrict__ out,
                                              unsigned long long *__restrict__ counts,
                                              uint32_t *hist, uint32_t lds_bins,
                                              const uint2 *lt = nullptr, const uint16_t *lw = nullptr) {
     uint32_t idx;
-    const uint4 v = lane_verdict<ABL, NTL, LDT>(L, next, ft, &idx, lt, lw);
+    uint4 v;
+    if (!(LEAN && LDT && (ABL & ~4) == 0 && lane_verdict_fast(L, ft, &v, &idx, lw)))
+        v = lane_verdict<ABL, NTL, LDT>(L, next, ft, &idx, lt, lw);
     if (L.valid) {
         if (ABL & 4)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
@@ -956,7 +1031,9 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14, "LDS table: PIPE 0 / 12 / 14 only");
+    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16,
+                  "LDS table: PIPE 0 / 12 / 14 / 16 only");
+    constexpr bool LEAN = PIPE == 16; // pipe 14 with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     // the port window after the compact table, then (PIPE 12/14/15) the stage
@@ -1036,7 +1113,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_load<NTL>(L);
             lane_process<ABL, ST_NT, NTL, LDT>(L, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
         }
-    } else if constexpr (PIPE == 14) {
+    } else if constexpr (PIPE == 14 || PIPE == 16) {
         // 12, software-pipelined: descriptors two trips ahead, frame bytes one
         // trip ahead (issued before the current trip is staged and processed),
         // so a wave keeps its next 4 KiB in flight across its parse / probe /
@@ -1064,7 +1141,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(B, pkts, lane, vb);
                 lane_stage(A, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1072,7 +1149,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(D, pkts, lane, va);
                 lane_stage(B, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1080,7 +1157,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(A, pkts, lane, vb);
                 lane_stage(D, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1088,7 +1165,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(D, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(B, pkts, lane, va);
                 lane_stage(A, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1096,7 +1173,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(A, p + 2 * stride, n, pkts, off, len, unit_log2);
                 cb = lane_issue(D, pkts, lane, vb);
                 lane_stage(B, va, ca, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1104,7 +1181,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 lane_desc_nb(B, p + 2 * stride, n, pkts, off, len, unit_log2);
                 ca = lane_issue(A, pkts, lane, va);
                 lane_stage(D, vb, cb, stage, lane);
-                lane_process<ABL, ST_NT, NTL, LDT>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                lane_process<ABL, ST_NT, NTL, LDT, LEAN>(D, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
                 base += stride;
                 p += stride;
                 if (base >= n) break;
@@ -1176,10 +1253,10 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
-    if (PIPE == 14 && idx) return hipErrorInvalidValue; // no index-list mode
+    if ((PIPE == 14 || PIPE == 16) && idx) return hipErrorInvalidValue; // no index-list mode
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
                        (LDT ? (size_t)(ft.udpc_mask + 1) * 8u + ((ft.udpw_n + 7u) & ~7u) * 2u : 0u) +
-                       (PIPE == 12 || PIPE == 14 ? 16384u : 0u);
+                       (PIPE == 12 || PIPE == 14 || PIPE == 16 ? 16384u : 0u);
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
         reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
@@ -3038,6 +3115,10 @@ static const variant_entry k_variants[] = {
 #if RX_DIAG
     // ---- tuning shapes (correct verdicts; sweeps in profiles/) ----
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6}, // 12 without the LDS UDP table
+    // 14 with lane_verdict_fast: 18% fewer vector and half the scalar
+    // instructions, the same time at cfg2 (the stores bound it, not issue:
+    // profiles/r06ab, r06ac)
+    {1, 4, 1, 16, launch_lane_udpc<16, 0, true, false>, 2},
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
     {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
     // write-batched G=8 around pipe 41 (WB 16, sc1): WB 8 / 12 / 24 (sc1), 16 (nt)
@@ -3075,6 +3156,7 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 1404, launch_lane_udpc<14, 4, true, false>, 2},
     {1, 4, 1, 1408, launch_lane_udpc<14, 8, true, false>, 2},
     {1, 4, 1, 1413, launch_lane_udpc<14, 13, true, false>, 2},
+    {1, 4, 1, 1604, launch_lane_udpc<16, 4, true, false>, 2}, // pipe 16, no verdict store
     // stream kernel: no flow probe (130); pipe 46 (span from the descriptors)
     // and its ablations: no probe (146), no tail stream (246), no head loads
     // (446), neither heads nor stream (646); pipe 38: no head loads (438), no

@@ -59,7 +59,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 0),
                    (0, 0, 0, 60), (0, 0, 0, 64), (0, 0, 0, 67)]  # SH kernel
 # compiled only into the RX_DIAG build (librxgpu_diag.so, RXGPU_LIB=...):
 # tuning shapes with correct verdicts ...
-DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (8, 2, 2, 1), (16, 2, 1, 0),
+DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (1, 4, 1, 16), (8, 2, 2, 1), (16, 2, 1, 0),
                         (8, 2, 2, 43), (8, 2, 2, 44), (8, 2, 2, 45), (8, 2, 2, 46),
                         (8, 2, 2, 47), (8, 2, 2, 49), (8, 2, 2, 50), (8, 2, 2, 51), (8, 2, 2, 52), (8, 2, 2, 53), (0, 0, 0, 54), (0, 0, 0, 66),
                         (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65),
@@ -70,7 +70,7 @@ DIAG_ABLATIONS = [(1, 4, 1, 101), (1, 4, 1, 104), (1, 4, 1, 108), (1, 4, 1, 113)
                   (0, 0, 0, 246), (0, 0, 0, 446), (0, 0, 0, 646), (0, 0, 0, 438), (0, 0, 0, 838),
                   (0, 0, 0, 1238), (0, 0, 0, 160), (0, 0, 0, 264), (0, 0, 0, 1064),
                   (0, 0, 0, 2064), (0, 0, 0, 167),
-                  (1, 4, 1, 1401), (1, 4, 1, 1404), (1, 4, 1, 1408), (1, 4, 1, 1413)]
+                  (1, 4, 1, 1401), (1, 4, 1, 1404), (1, 4, 1, 1408), (1, 4, 1, 1413), (1, 4, 1, 1604)]
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),

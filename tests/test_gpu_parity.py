@@ -234,7 +234,7 @@ def test_group_write_batched(ctx, torch_dev, variant, n, v8):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 16)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
@@ -264,8 +264,95 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
+def _udp_zero_sum_frame(src, sport, dst, dport):
+    """a 64-B UDP frame whose checksum computes to 0 (stored as 0xFFFF,
+    udp.c's rte_ipv4_udptcp_cksum rule): the payload's last word cancels the
+    rest of the sum"""
+    import struct
+    pay = bytearray(b"q" * 20 + b"\0\0")
+    udp = struct.pack(">HHHH", sport, dport, 8 + len(pay), 0) + bytes(pay)
+    ip = F.ipv4_header(src, dst, 17, len(udp))
+    psd = ip[12:20] + bytes([0, 17]) + struct.pack(">H", len(udp))
+    pay[20:22] = struct.pack("<H", (~F.fold_cksum(psd + udp)) & 0xFFFF)
+    f = F.udp_frame(src, sport, dst, dport, bytes(pay))
+    assert f[40:42] == b"\xff\xff" and len(f) == 64
+    return f
+
+
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16)]))
+@pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
+def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
+    """pipe 16's straight-line verdict (lane_verdict_fast) and the waves it
+    hands back to lane_verdict: 64-frame waves of 64-B UDP frames on the port
+    window's address, clean, or with one lane of each kind the fast path
+    declines or must get right itself: a TCP segment, ARP, ICMP (IPv4 other),
+    a non-IP ether type, an IP total length ending the checksum before byte
+    64, one below 20, a datagram length <= 8, a corrupted checksum, a
+    checksum that computes to 0 (stored 0xFFFF), a key on another address
+    (with and without sockets off the main address), a runt (caplen 48) and a
+    partial last wave; verdicts and counts bit-exact against the oracle"""
+    L, L2 = "192.168.100.77", "10.9.9.9"
+    socks = [(L, 30000 + 3 * k) for k in range(300)]
+    if others:
+        socks += [(L2, 30000 + 21 * k) for k in range(20)]
+    udp = np.zeros(len(socks), R.UDP_SOCK_DTYPE)
+    for i, (ip, port) in enumerate(socks):
+        udp[i] = (R.ip_raw(ip), R.port_raw(port), 17, 0)
+    tcb = np.zeros(0, R.TCB_DTYPE)
+    rng = np.random.default_rng(16)
+
+    def clean():
+        port = 30000 + int(rng.integers(0, 900))
+        return F.udp_frame("10.1.2.3", int(rng.integers(1024, 65535)), L, port,
+                           bytes(rng.integers(0, 256, 22, dtype=np.uint8)))
+
+    spoil = [
+        lambda: F.tcp_frame("10.1.2.3", 4000, L, 30003, b"t" * 10),
+        lambda: F.arp_frame("10.1.2.3", L),
+        lambda: F.icmp_frame("10.1.2.3", L),
+        lambda: F.ether(bytes(50), ethertype=0x86DD),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 30003, b"s" * 22, tl=40),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 30003, b"s" * 22, tl=18),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 30003, b"s" * 22, dgram_len=8),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 30003, b"s" * 22, dgram_len=3),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 30006, b"s" * 22, corrupt=True),
+        lambda: _udp_zero_sum_frame("10.1.2.3", 7, L, 30009),
+        lambda: F.udp_frame("10.1.2.3", 5, L2, 30021, b"s" * 22),
+        lambda: F.udp_frame("10.1.2.3", 5, "10.77.0.1", 30003, b"s" * 22),
+        lambda: F.udp_frame("10.1.2.3", 5, L, 29000, b"s" * 22),  # below the window
+    ]
+    frames, caps = [], []
+    for w in range(3 * len(spoil) + 6):
+        wave = [clean() for _ in range(64)]
+        cw = [len(f) for f in wave]
+        k = w % (len(spoil) + 2)
+        lane = int(rng.integers(0, 64))
+        if k < len(spoil):
+            wave[lane] = spoil[k]()
+            cw[lane] = min(len(wave[lane]), 64)
+        elif k == len(spoil):
+            cw[lane] = 48  # runt
+        frames += wave
+        caps += cw
+    frames += [clean() for _ in range(17)]  # a partial last wave
+    caps += [64] * 17
+    frames = [f[:64] + bytes(max(0, 64 - len(f))) if len(f) < 64 else f[:64] for f in frames]
+    pk, off, ln = F.pack_frames(frames, 6, caplens=caps)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), variant
+    # the oracle agrees on the spoilers' kinds (the cases are what they claim)
+    assert len(set(want["rc"].tolist())) >= 4
+
+
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
-                                     (0, 0, 0, 20)]))
+                                     (1, 4, 1, 16), (0, 0, 0, 20)]))
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("far", [False, True])
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
