@@ -1031,9 +1031,9 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16,
-                  "LDS table: PIPE 0 / 12 / 14 / 16 only");
-    constexpr bool LEAN = PIPE == 16; // pipe 14 with lane_verdict_fast
+    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 || PIPE == 19,
+                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 only");
+    constexpr bool LEAN = PIPE == 16 || PIPE == 18; // with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
     // the port window after the compact table, then (PIPE 12/14/15) the stage
@@ -1193,6 +1193,59 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 asm volatile("" ::"v"(B.cap), "v"(B.fb));
             }
         }
+    } else if constexpr (PIPE == 18 || PIPE == 19) {
+        // two adjacent 256-frame tiles per trip, the shape of the byte-pattern
+        // ceiling (tools/membw_cfg2, RDW U=2): both tiles' frame bytes are
+        // issued at the top of the trip (8 KiB per wave), then the next
+        // trip's descriptors; the two tiles are staged, classified and stored
+        // in turn.  Descriptors one trip ahead, so the frame loads never wait
+        // for them.  Two descriptor sets swap roles (unrolled twice, no
+        // register moves).  18: with lane_verdict_fast, 19: without
+        uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
+                                                 (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
+                       (tid >> 6) * 256u;
+        const uint32_t lane = tid & 63u;
+        const uint64_t stride2 = 2 * stride;
+        uint64_t base = (uint64_t)blockIdx.x * 512;
+        uint64_t q = base + tid;
+        if (base < n) {
+            lane_frame A0, A1, B0, B1;
+            lane_desc_nb(A0, q, n, pkts, off, len, unit_log2);
+            lane_desc_nb(A1, q + 256, n, pkts, off, len, unit_log2);
+            for (;;) {
+                {
+                    uint4 v0[4], v1[4];
+                    const bool c0 = lane_issue(A0, pkts, lane, v0);
+                    const bool c1 = lane_issue(A1, pkts, lane, v1);
+                    lane_desc_nb(B0, q + stride2, n, pkts, off, len, unit_log2);
+                    lane_desc_nb(B1, q + stride2 + 256, n, pkts, off, len, unit_log2);
+                    lane_stage(A0, v0, c0, stage, lane);
+                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                    lane_stage(A1, v1, c1, stage, lane);
+                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A1, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                }
+                base += stride2;
+                q += stride2;
+                if (base >= n) break;
+                {
+                    uint4 v0[4], v1[4];
+                    const bool c0 = lane_issue(B0, pkts, lane, v0);
+                    const bool c1 = lane_issue(B1, pkts, lane, v1);
+                    lane_desc_nb(A0, q + stride2, n, pkts, off, len, unit_log2);
+                    lane_desc_nb(A1, q + stride2 + 256, n, pkts, off, len, unit_log2);
+                    lane_stage(B0, v0, c0, stage, lane);
+                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                    lane_stage(B1, v1, c1, stage, lane);
+                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B1, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                }
+                base += stride2;
+                q += stride2;
+                if (base >= n) break;
+                // A's descriptor loads waited for here, where the count of
+                // later loads is exact (as in pipe 14)
+                asm volatile("" ::"v"(A0.cap), "v"(A0.fb), "v"(A1.cap), "v"(A1.fb));
+            }
+        }
     } else if constexpr (PIPE == 3) {
         lane_frame L;
         uint64_t base = (uint64_t)blockIdx.x * 256;
@@ -1253,10 +1306,10 @@ hipError_t launch_lane(const uint8_t *pkts, const uint32_t *off, const uint16_t 
                        uint32_t unit_log2, const rx_ft_dev &ft, uint4 *out,
                        unsigned long long *counts, uint32_t lds_bins, hipStream_t s,
                        const uint32_t *idx = nullptr, const uint32_t *n_dev = nullptr) {
-    if ((PIPE == 14 || PIPE == 16) && idx) return hipErrorInvalidValue; // no index-list mode
+    if ((PIPE == 14 || PIPE >= 16) && idx) return hipErrorInvalidValue; // no index-list mode
     const size_t lds = (size_t)((lds_bins + 3u) & ~3u) * 4u +
                        (LDT ? (size_t)(ft.udpc_mask + 1) * 8u + ((ft.udpw_n + 7u) & ~7u) * 2u : 0u) +
-                       (PIPE == 12 || PIPE == 14 || PIPE == 16 ? 16384u : 0u);
+                       (PIPE == 12 || PIPE == 14 || PIPE >= 16 ? 16384u : 0u);
     int cu = 0, bpc = 0;
     hipError_t e = rx_occupancy(
         reinterpret_cast<const void *>(rx_classify_lane_kernel<PIPE, ABL, ST_NT, NTL, LDT>), 256,
@@ -3119,6 +3172,10 @@ static const variant_entry k_variants[] = {
     // instructions, the same time at cfg2 (the stores bound it, not issue:
     // profiles/r06ab, r06ac)
     {1, 4, 1, 16, launch_lane_udpc<16, 0, true, false>, 2},
+    // two adjacent tiles per trip, the byte-pattern ceiling's shape: with
+    // (18) and without (19) lane_verdict_fast
+    {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
+    {1, 4, 1, 19, launch_lane_udpc<19, 0, true, false>, 2},
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
     {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
     // write-batched G=8 around pipe 41 (WB 16, sc1): WB 8 / 12 / 24 (sc1), 16 (nt)

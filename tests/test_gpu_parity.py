@@ -234,7 +234,8 @@ def test_group_write_batched(ctx, torch_dev, variant, n, v8):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 16)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 16),
+                                                          (1, 4, 1, 18), (1, 4, 1, 19)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
@@ -279,7 +280,7 @@ def _udp_zero_sum_frame(src, sport, dst, dport):
     return f
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18)]))
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
 def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
     """pipe 16's straight-line verdict (lane_verdict_fast) and the waves it
@@ -352,7 +353,7 @@ def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
 
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
-                                     (1, 4, 1, 16), (0, 0, 0, 20)]))
+                                     (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19), (0, 0, 0, 20)]))
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("far", [False, True])
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
