@@ -4,8 +4,8 @@
 // (bottom of this file); every shape is correct for any layout and length:
 //   lane kernel   (rx_classify_lane_kernel)   one frame per lane: 64-B frames
 //                 (heads staged through LDS by coalesced 1-KiB wave loads,
-//                 software-pipelined one trip ahead, UDP table and port
-//                 window in LDS);
+//                 two tiles' bytes in flight per trip, descriptors one trip
+//                 ahead, UDP table and port window in LDS);
 //   group kernel  (rx_classify_kernel)        G lanes per frame: 1500-B frames
 //                 (described below);
 //   stream kernel (rx_classify_stream_kernel) heads per thread, tails streamed
@@ -1031,8 +1031,9 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     const uint16_t *__restrict__ len, uint32_t n, uint32_t unit_log2, rx_ft_dev ft,
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
-    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 || PIPE == 19,
-                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 only");
+    static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 ||
+                      PIPE == 19 || PIPE == 21 || PIPE == 22,
+                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21 / 22 only");
     constexpr bool LEAN = PIPE == 16 || PIPE == 18; // with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
@@ -1193,57 +1194,54 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 asm volatile("" ::"v"(B.cap), "v"(B.fb));
             }
         }
-    } else if constexpr (PIPE == 18 || PIPE == 19) {
-        // two adjacent 256-frame tiles per trip, the shape of the byte-pattern
-        // ceiling (tools/membw_cfg2, RDW U=2): both tiles' frame bytes are
-        // issued at the top of the trip (8 KiB per wave), then the next
-        // trip's descriptors; the two tiles are staged, classified and stored
-        // in turn.  Descriptors one trip ahead, so the frame loads never wait
+    } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22) {
+        // T adjacent 256-frame tiles per trip, the shape of the byte-pattern
+        // ceiling (tools/membw_cfg2, RDW U=2): every tile's frame bytes are
+        // issued at the top of the trip (T x 4 KiB per wave), then the next
+        // trip's descriptors; the tiles are staged, classified and stored in
+        // turn.  Descriptors one trip ahead, so the frame loads never wait
         // for them.  Two descriptor sets swap roles (unrolled twice, no
-        // register moves).  18: with lane_verdict_fast, 19: without
+        // register moves).  T = 2: 18 (with lane_verdict_fast) and 19; T = 3:
+        // 21; T = 4: 22
+        constexpr int T = PIPE == 21 ? 3 : (PIPE == 22 ? 4 : 2);
         uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
                                                  (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
                        (tid >> 6) * 256u;
         const uint32_t lane = tid & 63u;
-        const uint64_t stride2 = 2 * stride;
-        uint64_t base = (uint64_t)blockIdx.x * 512;
+        const uint64_t strideT = (uint64_t)T * stride;
+        uint64_t base = (uint64_t)blockIdx.x * 256u * T;
         uint64_t q = base + tid;
         if (base < n) {
-            lane_frame A0, A1, B0, B1;
-            lane_desc_nb(A0, q, n, pkts, off, len, unit_log2);
-            lane_desc_nb(A1, q + 256, n, pkts, off, len, unit_log2);
+            lane_frame A[T], B[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) lane_desc_nb(A[u], q + 256u * u, n, pkts, off, len, unit_log2);
+            auto trip = [&](lane_frame (&X)[T], lane_frame (&Y)[T]) {
+                uint4 v[T][4];
+                bool c[T];
+#pragma unroll
+                for (int u = 0; u < T; ++u) c[u] = lane_issue(X[u], pkts, lane, v[u]);
+#pragma unroll
+                for (int u = 0; u < T; ++u)
+                    lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+#pragma unroll
+                for (int u = 0; u < T; ++u) {
+                    lane_stage(X[u], v[u], c[u], stage, lane);
+                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(X[u], nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                }
+            };
             for (;;) {
-                {
-                    uint4 v0[4], v1[4];
-                    const bool c0 = lane_issue(A0, pkts, lane, v0);
-                    const bool c1 = lane_issue(A1, pkts, lane, v1);
-                    lane_desc_nb(B0, q + stride2, n, pkts, off, len, unit_log2);
-                    lane_desc_nb(B1, q + stride2 + 256, n, pkts, off, len, unit_log2);
-                    lane_stage(A0, v0, c0, stage, lane);
-                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
-                    lane_stage(A1, v1, c1, stage, lane);
-                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(A1, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
-                }
-                base += stride2;
-                q += stride2;
+                trip(A, B);
+                base += strideT;
+                q += strideT;
                 if (base >= n) break;
-                {
-                    uint4 v0[4], v1[4];
-                    const bool c0 = lane_issue(B0, pkts, lane, v0);
-                    const bool c1 = lane_issue(B1, pkts, lane, v1);
-                    lane_desc_nb(A0, q + stride2, n, pkts, off, len, unit_log2);
-                    lane_desc_nb(A1, q + stride2 + 256, n, pkts, off, len, unit_log2);
-                    lane_stage(B0, v0, c0, stage, lane);
-                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B0, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
-                    lane_stage(B1, v1, c1, stage, lane);
-                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(B1, nullptr, ft, out, counts, hist, lds_bins, lt, lw);
-                }
-                base += stride2;
-                q += stride2;
+                trip(B, A);
+                base += strideT;
+                q += strideT;
                 if (base >= n) break;
                 // A's descriptor loads waited for here, where the count of
                 // later loads is exact (as in pipe 14)
-                asm volatile("" ::"v"(A0.cap), "v"(A0.fb), "v"(A1.cap), "v"(A1.fb));
+#pragma unroll
+                for (int u = 0; u < T; ++u) asm volatile("" ::"v"(A[u].cap), "v"(A[u].fb));
             }
         }
     } else if constexpr (PIPE == 3) {
@@ -3134,6 +3132,10 @@ static const variant_entry k_variants[] = {
     // 14 (the 64-B default): 12 software-pipelined (descriptors two trips,
     // frame bytes one trip ahead)
     {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 2},
+    // 19 (the 64-B default from round 6): two adjacent 256-frame tiles per
+    // trip, both tiles' frame bytes issued at the top of the trip,
+    // descriptors one trip ahead (the byte-pattern ceiling's shape)
+    {1, 4, 1, 19, launch_lane_udpc<19, 0, true, false>, 2},
     {1, 4, 1, 0, launch_lane<0>},
     // group kernels, one per G (the first entry per g is its default)
     {4, 1, 1, 1, launch_v<4, 1, 1, 1>},
@@ -3172,10 +3174,11 @@ static const variant_entry k_variants[] = {
     // instructions, the same time at cfg2 (the stores bound it, not issue:
     // profiles/r06ab, r06ac)
     {1, 4, 1, 16, launch_lane_udpc<16, 0, true, false>, 2},
-    // two adjacent tiles per trip, the byte-pattern ceiling's shape: with
-    // (18) and without (19) lane_verdict_fast
+    // two adjacent tiles per trip (19, the 64-B default) with
+    // lane_verdict_fast: 0.2326 vs 0.2240 ms for 19 (profiles/r06ad)
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
-    {1, 4, 1, 19, launch_lane_udpc<19, 0, true, false>, 2},
+    {1, 4, 1, 21, launch_lane_udpc<21, 0, true, false>, 2}, // three tiles per trip
+    {1, 4, 1, 22, launch_lane_udpc<22, 0, true, false>, 2}, // four
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
     {16, 2, 1, 0, launch_v<16, 2, 1, 0>},
     // write-batched G=8 around pipe 41 (WB 16, sc1): WB 8 / 12 / 24 (sc1), 16 (nt)
@@ -3254,8 +3257,11 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // software-pipelined one trip ahead (pipe 14: 0.2487-0.2506 vs 0.2641-0.2660 ms for
         // pipe 12 at 3 blocks/CU, r02i); with the LDS port window the two tie within 1%
         // and pipe 14 is best at 2 blocks/CU (0.2328-0.2343 vs 0.2346-0.2352 for pipe 12 at
-        // 4-6, r02m, r02o)
-        *g = 1, *p = 4, *fpg = 1, *pipe = 14;
+        // 4-6, r02m, r02o); two adjacent tiles per trip with both tiles' bytes issued at the
+        // top (pipe 19): 0.2271 vs 0.2346 ms in an interleaved sweep, 0.2270-0.2277 vs
+        // 0.2355-0.2361 per step across alternating processes (profiles/r06ae); 3 / 4
+        // tiles per trip 0.2364 / 0.2396, 19 at 3 blocks/CU 0.2393
+        *g = 1, *p = 4, *fpg = 1, *pipe = 19;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
         // out of the block stream and a four-slot first probe window (SH): 1.2704 vs 1.3417 ms
         // for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716 on

@@ -153,7 +153,7 @@ def test_generated_bursts_match_oracle(ctx, torch_dev, name, n):
 @pytest.mark.parametrize("shift", [0, 8])
 @pytest.mark.parametrize("n", [1, 2, 63, 65, 4097, 40001])
 def test_verdict8_odd_and_unaligned(ctx, torch_dev, n, shift):
-    """64-B frames (lane kernel, pipe 14) into 8-B verdicts, the output 16-B
+    """64-B frames (lane kernel, the 64-B default) into 8-B verdicts, the output 16-B
     aligned (shift 0) or only 8-B aligned as rxgpu.h allows (shift 8), bursts
     of odd lengths (a lane-pair store variant was measured and dropped:
     DESIGN.md, compact verdicts).  Nothing is written outside
@@ -235,7 +235,7 @@ def test_group_write_batched(ctx, torch_dev, variant, n, v8):
 
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 16),
-                                                          (1, 4, 1, 18), (1, 4, 1, 19)]))
+                                                          (1, 4, 1, 18), (1, 4, 1, 19), (1, 4, 1, 21), (1, 4, 1, 22)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
@@ -280,7 +280,7 @@ def _udp_zero_sum_frame(src, sport, dst, dport):
     return f
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19)]))
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
 def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
     """pipe 16's straight-line verdict (lane_verdict_fast) and the waves it
@@ -353,7 +353,7 @@ def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
 
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
-                                     (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19), (0, 0, 0, 20)]))
+                                     (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19), (1, 4, 1, 21), (0, 0, 0, 20)]))
 @pytest.mark.parametrize("tables", [0, R.TT_NO_UDP_PORT])
 @pytest.mark.parametrize("far", [False, True])
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
