@@ -173,8 +173,14 @@ struct tx_variant {
     tx_launch_fn fn;
     uint32_t bpc; // resident blocks per CU cap (0 = occupancy)
 };
-// 0..3: the defaults for <= 64, <= 128, <= 1536 and longer frames, 10 the one
-// for mixed sizes; the rest are tuning alternatives (rxg_tune_tx).
+// 10: the default for <= 64 B frames and for mixed sizes; 1..3 for <= 128,
+// <= 1536 and longer frames; the rest are tuning alternatives (rxg_tune_tx).
+// At 64 B one block per 64-frame tile (10) ran 0.3945-0.3962 ms against
+// 0.4468-0.4478 for the resident grid with 4 frames per group (0), and 4 /
+// 1 block per tile with 2 / 4 frames per group 0.4084 / 0.4109; the next
+// trip's descriptors loaded one trip ahead (resident grid) 0.4523-0.4533
+// (interleaved sweeps, profiles/r06ag).  Round 1 had measured 10 behind 0
+// (0.4538 vs 0.4460, r01d).
 // Measured (tools/tx_sweep.py, profiles/r01d/tx_sweep.txt): the write mode and
 // the schedule move these by only 2-4%.  Changing 4 bytes in a frame's first
 // 64 B dirties its first 128-B line, and the line goes back to HBM whole, so
@@ -203,7 +209,7 @@ hipError_t tx_cksum_launch(uint8_t *pkts, const uint32_t *off, const uint16_t *l
     if (len_hint == 0) len_hint = 1518;
     // (mixed sizes, e.g. IMIX at 354 B average: G=4, one frame per group and
     // block per tile, 1.88 ms vs 2.30 for G=8 on cfg4, profiles/r01d + r01e)
-    uint32_t v = len_hint <= 64 ? 0 : (len_hint <= 128 ? 1 : (len_hint <= 600 ? 10 : (len_hint <= 1536 ? 2 : 3)));
+    uint32_t v = len_hint <= 64 ? 10 : (len_hint <= 128 ? 1 : (len_hint <= 600 ? 10 : (len_hint <= 1536 ? 2 : 3)));
     if (variant < tx_num_variants()) v = variant;
     return k_tx[v].fn(pkts, off, len, n, unit_log2, bpc_cap ? bpc_cap : k_tx[v].bpc, s);
 }
