@@ -17,7 +17,8 @@
 #include "rx_common.h"
 #include "rx_flows.h"
 
-void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe);
+void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe,
+                     bool v8 = false);
 bool rx_variant_exists(uint32_t g, uint32_t p, uint32_t fpg, uint32_t pipe);
 const char *rx_variant_kernel(uint32_t g, uint32_t pipe);
 hipError_t rx_classify_launch(const uint8_t *pkts, const uint32_t *off, const uint16_t *len,
@@ -1337,7 +1338,7 @@ static int classify_dev_impl(rxg_ctx *c, const uint8_t *d_pkts, const uint32_t *
     if (off_unit_log2 < 4 || off_unit_log2 > 16) return RXG_EINVAL;
     DEVGUARD(c);
     uint32_t g = c->tune_g, p = c->tune_p, fpg = c->tune_fpg, pipe = c->tune_pipe;
-    if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe);
+    if (!g && pipe == ~0u) rx_pick_variant(len_hint, &g, &p, &fpg, &pipe, v8 != 0);
     c->ft.v8 = v8; // read by this burst's launches only (they copy c->ft)
     const int rc = classify_ws(c, d_pkts, d_off, d_len, n, off_unit_log2, g, p, fpg, pipe,
                                static_cast<uint4 *>(d_out),

@@ -3251,7 +3251,8 @@ static const variant_entry k_variants[] = {
 // with any variant (frames longer than P passes take the remainder loop); the
 // choice only moves speed.
 #if !RX_V8
-void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe) {
+void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg, uint32_t *pipe,
+                     bool v8) {
     if (len_hint == 0) len_hint = 1518;
     if (len_hint <= 64) { // cfg2: 64 B; LDS-staged coalesced loads (0.258 vs 0.280 ms, r01b),
         // software-pipelined one trip ahead (pipe 14: 0.2487-0.2506 vs 0.2641-0.2660 ms for
@@ -3260,8 +3261,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // 4-6, r02m, r02o); two adjacent tiles per trip with both tiles' bytes issued at the
         // top (pipe 19): 0.2271 vs 0.2346 ms in an interleaved sweep, 0.2270-0.2277 vs
         // 0.2355-0.2361 per step across alternating processes (profiles/r06ae); 3 / 4
-        // tiles per trip 0.2364 / 0.2396, 19 at 3 blocks/CU 0.2393
-        *g = 1, *p = 4, *fpg = 1, *pipe = 19;
+        // tiles per trip 0.2364 / 0.2396, 19 at 3 blocks/CU 0.2393.  With 8-B verdicts
+        // (rxg_classify_dev8) pipe 14 stays ahead: 77.6-77.7 vs 72.9-73.2 Gpps across
+        // alternating processes (profiles/r06ai)
+        *g = 1, *p = 4, *fpg = 1, *pipe = v8 ? 14 : 19;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
         // out of the block stream and a four-slot first probe window (SH): 1.2704 vs 1.3417 ms
         // for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716 on
