@@ -3136,6 +3136,11 @@ static const variant_entry k_variants[] = {
     // trip, both tiles' frame bytes issued at the top of the trip,
     // descriptors one trip ahead (the byte-pattern ceiling's shape)
     {1, 4, 1, 19, launch_lane_udpc<19, 0, true, false>, 2},
+    // 16 (the 64-B default for 8-B verdicts): 14 with lane_verdict_fast, 18%
+    // fewer vector and half the scalar instructions; with 16-B verdicts the
+    // same time as 14 (the stores bound it: profiles/r06ab, r06ac), with
+    // 8-B verdicts 79.0-79.5 vs 76.2-77.4 Gpps for 14 (profiles/r06ak)
+    {1, 4, 1, 16, launch_lane_udpc<16, 0, true, false>, 2},
     {1, 4, 1, 0, launch_lane<0>},
     // group kernels, one per G (the first entry per g is its default)
     {4, 1, 1, 1, launch_v<4, 1, 1, 1>},
@@ -3170,10 +3175,6 @@ static const variant_entry k_variants[] = {
 #if RX_DIAG
     // ---- tuning shapes (correct verdicts; sweeps in profiles/) ----
     {1, 4, 1, 13, launch_lane<12, 0, true, false>, 6}, // 12 without the LDS UDP table
-    // 14 with lane_verdict_fast: 18% fewer vector and half the scalar
-    // instructions, the same time at cfg2 (the stores bound it, not issue:
-    // profiles/r06ab, r06ac)
-    {1, 4, 1, 16, launch_lane_udpc<16, 0, true, false>, 2},
     // two adjacent tiles per trip (19, the 64-B default) with
     // lane_verdict_fast: 0.2326 vs 0.2240 ms for 19 (profiles/r06ad)
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
@@ -3262,9 +3263,10 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // top (pipe 19): 0.2271 vs 0.2346 ms in an interleaved sweep, 0.2270-0.2277 vs
         // 0.2355-0.2361 per step across alternating processes (profiles/r06ae); 3 / 4
         // tiles per trip 0.2364 / 0.2396, 19 at 3 blocks/CU 0.2393.  With 8-B verdicts
-        // (rxg_classify_dev8) pipe 14 stays ahead: 77.6-77.7 vs 72.9-73.2 Gpps across
-        // alternating processes (profiles/r06ai)
-        *g = 1, *p = 4, *fpg = 1, *pipe = v8 ? 14 : 19;
+        // (rxg_classify_dev8) the one-tile pipeline stays ahead, 14 at 77.6-77.7 vs
+        // 72.9-73.2 Gpps for 19 (profiles/r06ai), and 14 with the straight-line verdict
+        // (16) at 79.0-79.5 vs 76.2-77.4 (profiles/r06ak)
+        *g = 1, *p = 4, *fpg = 1, *pipe = v8 ? 16 : 19;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
         // out of the block stream and a four-slot first probe window (SH): 1.2704 vs 1.3417 ms
         // for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716 on

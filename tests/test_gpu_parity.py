@@ -282,7 +282,8 @@ def _udp_zero_sum_frame(src, sport, dst, dport):
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19)]))
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
-def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
+@pytest.mark.parametrize("v8", [False, True])
+def test_lane_fast_path_waves(ctx, torch_dev, variant, others, v8):
     """pipe 16's straight-line verdict (lane_verdict_fast) and the waves it
     hands back to lane_verdict: 64-frame waves of 64-B UDP frames on the port
     window's address, clean, or with one lane of each kind the fast path
@@ -291,7 +292,8 @@ def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
     64, one below 20, a datagram length <= 8, a corrupted checksum, a
     checksum that computes to 0 (stored 0xFFFF), a key on another address
     (with and without sockets off the main address), a runt (caplen 48) and a
-    partial last wave; verdicts and counts bit-exact against the oracle"""
+    partial last wave; verdicts (16- and 8-B) and counts bit-exact against
+    the oracle"""
     L, L2 = "192.168.100.77", "10.9.9.9"
     socks = [(L, 30000 + 3 * k) for k in range(300)]
     if others:
@@ -341,15 +343,17 @@ def test_lane_fast_path_waves(ctx, torch_dev, variant, others):
     pk, off, ln = F.pack_frames(frames, 6, caplens=caps)
     ctx.flows_sync(udp, tcb)
     want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
-    ctx.tune(*variant)
-    try:
-        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True)
-    finally:
-        ctx.tune(0)
-    assert got.tobytes() == want.tobytes(), (variant, _mismatch_report(got, want))
-    assert np.array_equal(cnt, wcnt), variant
     # the oracle agrees on the spoilers' kinds (the cases are what they claim)
     assert len(set(want["rc"].tolist())) >= 4
+    ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True, v8=v8)
+    finally:
+        ctx.tune(0)
+    if v8:
+        want = R.verdict8_of(want)
+    assert got.tobytes() == want.tobytes(), (variant, v8, _mismatch_report(got, want))
+    assert np.array_equal(cnt, wcnt), variant
 
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 0), (1, 4, 1, 5), (1, 4, 1, 12), (1, 4, 1, 14),
