@@ -998,6 +998,22 @@ __device__ __forceinline__ void lane_store(const rx_ft_dev &ft, uint4 *__restric
 }
 
 // the original one-shot form: verdict, store, count
+// the store and count half of lane_process (PIPE 23 defers it to the trip's end)
+template <int ABL = 0, bool ST_NT = true>
+__device__ __forceinline__ void lane_finish(const lane_frame &L, uint4 v, uint32_t idx,
+                                            const rx_ft_dev &ft, uint4 *__restrict__ out,
+                                            unsigned long long *__restrict__ counts, uint32_t *hist,
+                                            uint32_t lds_bins) {
+    if (L.valid) {
+        if (ABL & 4)
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+        else
+            lane_store<ST_NT>(ft, out, L.p, v);
+        lane_count(idx, counts, hist, lds_bins);
+        if (ft.count_idx) put_count_idx(ft, L.p, idx);
+    }
+}
+
 // LEAN (PIPE 16): lane_verdict_fast first, lane_verdict for the waves it declines
 template <int ABL = 0, bool ST_NT = true, bool NTL = true, bool LDT = false, bool LEAN = false>
 __device__ __forceinline__ void lane_process(lane_frame &L, lane_frame *next,
@@ -1032,8 +1048,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
     static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 ||
-                      PIPE == 19 || PIPE == 21 || PIPE == 22,
-                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21 / 22 only");
+                      PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23,
+                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21 / 22 / 23 only");
     constexpr bool LEAN = PIPE == 16 || PIPE == 18; // with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
@@ -1194,7 +1210,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 asm volatile("" ::"v"(B.cap), "v"(B.fb));
             }
         }
-    } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22) {
+    } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23) {
         // T adjacent 256-frame tiles per trip, the shape of the byte-pattern
         // ceiling (tools/membw_cfg2, RDW U=2): every tile's frame bytes are
         // issued at the top of the trip (T x 4 KiB per wave), then the next
@@ -1223,10 +1239,23 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
 #pragma unroll
                 for (int u = 0; u < T; ++u)
                     lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                if constexpr (PIPE == 23) { // every tile's verdict first, the stores at the end
+                    uint4 vd[T];
+                    uint32_t ix[T];
 #pragma unroll
-                for (int u = 0; u < T; ++u) {
-                    lane_stage(X[u], v[u], c[u], stage, lane);
-                    lane_process<ABL, ST_NT, NTL, LDT, LEAN>(X[u], nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                    for (int u = 0; u < T; ++u) {
+                        lane_stage(X[u], v[u], c[u], stage, lane);
+                        vd[u] = lane_verdict<ABL, NTL, LDT>(X[u], nullptr, ft, &ix[u], lt, lw);
+                    }
+#pragma unroll
+                    for (int u = 0; u < T; ++u)
+                        lane_finish<ABL, ST_NT>(X[u], vd[u], ix[u], ft, out, counts, hist, lds_bins);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < T; ++u) {
+                        lane_stage(X[u], v[u], c[u], stage, lane);
+                        lane_process<ABL, ST_NT, NTL, LDT, LEAN>(X[u], nullptr, ft, out, counts, hist, lds_bins, lt, lw);
+                    }
                 }
             };
             for (;;) {
@@ -3178,6 +3207,7 @@ static const variant_entry k_variants[] = {
     // two adjacent tiles per trip (19, the 64-B default) with
     // lane_verdict_fast: 0.2326 vs 0.2240 ms for 19 (profiles/r06ad)
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
+    {1, 4, 1, 23, launch_lane_udpc<23, 0, true, false>, 2}, // 19, both tiles' stores at the trip's end
     {1, 4, 1, 21, launch_lane_udpc<21, 0, true, false>, 2}, // three tiles per trip
     {1, 4, 1, 22, launch_lane_udpc<22, 0, true, false>, 2}, // four
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
