@@ -3228,6 +3228,11 @@ static const variant_entry k_variants[] = {
     {8, 2, 2, 51, launch_v<8, 2, 2, 0, true, 0, 5, true, 20, true>},
     {8, 2, 2, 52, launch_v<8, 2, 2, 0, true, 0, 1, true, 23, true>},
     {8, 2, 2, 53, launch_v<8, 2, 2, 0, true, 0, 5, true, 16, true>},
+    // pipe 48 with the remaining passes of both frames loaded together, 2 / 4
+    // / 10 per frame per batch (RI)
+    {8, 2, 2, 54, launch_v<8, 2, 2, 0, true, 2, 1, true, 24, true>},
+    {8, 2, 2, 55, launch_v<8, 2, 2, 0, true, 4, 1, true, 24, true>},
+    {8, 2, 2, 56, launch_v<8, 2, 2, 0, true, 10, 1, true, 24, true>},
     {0, 1, 1, 54, launch_stream<true, 0, 3, 1, true, false, true>}, // heads gathered 4 lanes/head
     {0, 1, 1, 66, launch_sh<0, 4, SH_MAPC, false, 3>},              // 12-KiB tiles
     {0, 1, 1, 68, launch_sh<0, 4, SH_MAPC, false, 2, true>},        // partial sums in the stream

@@ -207,7 +207,8 @@ def test_every_kernel_variant(ctx, torch_dev, variant):
 @pytest.mark.parametrize("variant", R.compiled_variants([(8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42),
                                                           (8, 2, 2, 47), (8, 2, 2, 48), (8, 2, 2, 49),
                                                           (8, 2, 2, 50), (8, 2, 2, 51), (8, 2, 2, 52),
-                                                          (8, 2, 2, 53)]))
+                                                          (8, 2, 2, 53), (8, 2, 2, 54), (8, 2, 2, 55),
+                                                          (8, 2, 2, 56)]))
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1025, 64 * 16 * 3 + 17, 65536, 300001])
 @pytest.mark.parametrize("v8", [False, True])
 def test_group_write_batched(ctx, torch_dev, variant, n, v8):
