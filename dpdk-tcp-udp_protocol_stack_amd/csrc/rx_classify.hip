@@ -1048,8 +1048,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
     static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 ||
-                      PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23,
-                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21 / 22 / 23 only");
+                      PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23 || PIPE == 24,
+                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21-24 only");
     constexpr bool LEAN = PIPE == 16 || PIPE == 18; // with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
@@ -1210,7 +1210,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
                 asm volatile("" ::"v"(B.cap), "v"(B.fb));
             }
         }
-    } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23) {
+    } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23 ||
+                         PIPE == 24) {
         // T adjacent 256-frame tiles per trip, the shape of the byte-pattern
         // ceiling (tools/membw_cfg2, RDW U=2): every tile's frame bytes are
         // issued at the top of the trip (T x 4 KiB per wave), then the next
@@ -1234,11 +1235,18 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             auto trip = [&](lane_frame (&X)[T], lane_frame (&Y)[T]) {
                 uint4 v[T][4];
                 bool c[T];
+                if constexpr (PIPE == 24) { // the next trip's descriptors first
+#pragma unroll
+                    for (int u = 0; u < T; ++u)
+                        lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                }
 #pragma unroll
                 for (int u = 0; u < T; ++u) c[u] = lane_issue(X[u], pkts, lane, v[u]);
+                if constexpr (PIPE != 24) {
 #pragma unroll
-                for (int u = 0; u < T; ++u)
-                    lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                    for (int u = 0; u < T; ++u)
+                        lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                }
                 if constexpr (PIPE == 23) { // every tile's verdict first, the stores at the end
                     uint4 vd[T];
                     uint32_t ix[T];
@@ -3208,6 +3216,7 @@ static const variant_entry k_variants[] = {
     // lane_verdict_fast: 0.2326 vs 0.2240 ms for 19 (profiles/r06ad)
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
     {1, 4, 1, 23, launch_lane_udpc<23, 0, true, false>, 2}, // 19, both tiles' stores at the trip's end
+    {1, 4, 1, 24, launch_lane_udpc<24, 0, true, false>, 2}, // 19, next descriptors before the frames
     {1, 4, 1, 21, launch_lane_udpc<21, 0, true, false>, 2}, // three tiles per trip
     {1, 4, 1, 22, launch_lane_udpc<22, 0, true, false>, 2}, // four
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
