@@ -2079,7 +2079,9 @@ __device__ __forceinline__ uint32_t sh_head_sum(const uint4 (&c)[4], const sh_he
 
 // ABL (diagnostic builds, pipes 160 / 264): 1 = no flow-table probe (flow id
 // from the port; wrong verdicts by construction), 2 = every partial last
-// chunk loaded from HBM after the stream (no partial marks).  PW: slots of the first probe window
+// chunk loaded from HBM after the stream (no partial marks), 16 = no count-index
+// store, 32 = the count-index store before the verdict store, 64 = no verdict
+// store.  PW: slots of the first probe window
 // (1, 2 or 4 consecutive slots of the hashed table loaded together; the table
 // mirrors its first slots past its end), so a displaced key costs no dependent
 // second round trip at the end of the block (pipes 60 / 63 / 64).
@@ -2543,7 +2545,10 @@ __global__ __launch_bounds__(256, MAPC > SH_MAPC ? 3 : (PS && L == 2 ? 6 : 5)) v
         vd.w = (ok ? 1u : 0u) | (flags << 8) | (h.stored << 16);
         if constexpr ((ABL & 32) != 0)
             if (wvu * 64u < (uint32_t)FPB) put_count_idx_wave(ft, p, cidx, lane); // (diagnostic order)
-        st_verdict<WT>(ft, out, p, vd);
+        if constexpr ((ABL & 64) != 0) // diagnostic: no verdict store
+            asm volatile("" ::"v"(vd.x), "v"(vd.y), "v"(vd.z), "v"(vd.w));
+        else
+            st_verdict<WT>(ft, out, p, vd);
         lane_count(cidx, counts, hist, lds_bins);
     }
     if constexpr ((ABL & 48) == 0)
@@ -3281,6 +3286,9 @@ static const variant_entry k_variants[] = {
     {0, 1, 1, 1064, launch_sh<16, 4>}, {0, 1, 1, 2064, launch_sh<32, 4>},
     // 167: 67 without the flow probe
     {0, 1, 1, 167, launch_sh<1, 4, SH_MAPC, false, 2>},
+    // pipe 67 without the count-index store (1667) / the verdict store (6467)
+    {0, 1, 1, 1667, launch_sh<16, 4, SH_MAPC, false, 2>},
+    {0, 1, 1, 6467, launch_sh<64, 4, SH_MAPC, false, 2>},
     // ---- the wave-contiguous shape (WC kernel): F frames per wave trip, NL
     // loads per lane; 80 / 81: F = 2, NL = 3 (1.5-KiB slots) with / without
     // the next trip's span in flight; 82 / 83: F = 4, NL = 6

@@ -70,7 +70,7 @@ DIAG_ABLATIONS = [(1, 4, 1, 101), (1, 4, 1, 104), (1, 4, 1, 108), (1, 4, 1, 113)
                   (0, 0, 0, 246), (0, 0, 0, 446), (0, 0, 0, 646), (0, 0, 0, 438), (0, 0, 0, 838),
                   (0, 0, 0, 1238), (0, 0, 0, 160), (0, 0, 0, 264), (0, 0, 0, 1064),
                   (0, 0, 0, 2064), (0, 0, 0, 167),
-                  (1, 4, 1, 1401), (1, 4, 1, 1404), (1, 4, 1, 1408), (1, 4, 1, 1413), (1, 4, 1, 1604)]
+                  (1, 4, 1, 1401), (1, 4, 1, 1404), (1, 4, 1, 1408), (1, 4, 1, 1413), (1, 4, 1, 1604), (0, 0, 0, 1667), (0, 0, 0, 6467)]
 
 VERDICT_DTYPE = np.dtype([
     ("flow_id", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"), ("l4_cksum", "<u2"),
