@@ -267,6 +267,35 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 19)]) + [None],
+                         ids=lambda v: "default" if v is None else "v" + "-".join(map(str, v)))
+@pytest.mark.parametrize("flows", ["udp5000", "mixed"])
+def test_lane_without_lds_table(ctx, torch_dev, variant, flows):
+    """64-B frames with no compact UDP table in LDS (the lane kernels' global
+    probe path): 5000 UDP sockets (more than the compact table holds), and
+    TCP/UDP half and half over 300 sockets and 2000 tcbs; the default pick
+    and each lane variant, 16- and 8-B verdicts and counts, bit-exact against
+    the oracle; ragged burst (not a multiple of the two-tile trip)"""
+    kw = dict(n_udp=5000) if flows == "udp5000" else dict(n_udp=300, n_tcp=2000, proto_mode=2)
+    cfg = rxdist.gen_cfg("cfg2", **kw)
+    n = 3 * 512 * 7 + 333
+    pk, off, ln = R.gen_host(cfg, 11, n, 6)
+    udp, tcb = R.gen_flows(cfg)
+    ctx.flows_sync(udp, tcb)
+    want, wcnt = O.Tables(udp, tcb).classify(pk, off, ln, 6, counts=True)
+    if variant:
+        ctx.tune(*variant)
+    try:
+        got, cnt = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True)
+        got8, cnt8 = _dev_classify(torch_dev, ctx, pk, off, ln, 6, 64, counts=True, v8=True)
+    finally:
+        ctx.tune(0)
+    assert got.tobytes() == want.tobytes(), (variant, flows, _mismatch_report(got, want))
+    assert got8.tobytes() == R.verdict8_of(want).tobytes(), (variant, flows, "v8")
+    assert np.array_equal(cnt, wcnt) and np.array_equal(cnt8, wcnt), (variant, flows)
+    assert (want["rc"] == 0).sum() > n // 2
+
+
 def _udp_zero_sum_frame(src, sport, dst, dport):
     """a 64-B UDP frame whose checksum computes to 0 (stored as 0xFFFF,
     udp.c's rte_ipv4_udptcp_cksum rule): the payload's last word cancels the
