@@ -1048,8 +1048,8 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
     uint4 *__restrict__ out, unsigned long long *__restrict__ counts, uint32_t lds_bins,
     const uint32_t *__restrict__ idx, const uint32_t *__restrict__ n_dev) {
     static_assert(!LDT || PIPE == 0 || PIPE == 12 || PIPE == 14 || PIPE == 16 || PIPE == 18 ||
-                      PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23 || PIPE == 24,
-                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21-24 only");
+                      PIPE == 19 || (PIPE >= 21 && PIPE <= 25),
+                  "LDS table: PIPE 0 / 12 / 14 / 16 / 18 / 19 / 21-25 only");
     constexpr bool LEAN = PIPE == 16 || PIPE == 18; // with lane_verdict_fast
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint2 *lt = reinterpret_cast<uint2 *>(hist + ((lds_bins + 3u) & ~3u));
@@ -1211,7 +1211,7 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
             }
         }
     } else if constexpr (PIPE == 18 || PIPE == 19 || PIPE == 21 || PIPE == 22 || PIPE == 23 ||
-                         PIPE == 24) {
+                         PIPE == 24 || PIPE == 25) {
         // T adjacent 256-frame tiles per trip, the shape of the byte-pattern
         // ceiling (tools/membw_cfg2, RDW U=2): every tile's frame bytes are
         // issued at the top of the trip (T x 4 KiB per wave), then the next
@@ -1221,31 +1221,33 @@ __global__ __launch_bounds__(256, PIPE == 2 ? 6 : 1) void rx_classify_lane_kerne
         // register moves).  T = 2: 18 (with lane_verdict_fast) and 19; T = 3:
         // 21; T = 4: 22
         constexpr int T = PIPE == 21 ? 3 : (PIPE == 22 ? 4 : 2);
+        // the trip's tiles: adjacent (every pipe but 25) or a grid stride apart (25)
         uint4 *stage = reinterpret_cast<uint4 *>(hist + ((lds_bins + 3u) & ~3u) +
                                                  (LDT ? 2u * (ft.udpc_mask + 1u) + lw_words : 0u)) +
                        (tid >> 6) * 256u;
         const uint32_t lane = tid & 63u;
         const uint64_t strideT = (uint64_t)T * stride;
-        uint64_t base = (uint64_t)blockIdx.x * 256u * T;
+        const uint64_t TO = PIPE == 25 ? stride : 256u;
+        uint64_t base = (uint64_t)blockIdx.x * (PIPE == 25 ? 256u : 256u * T);
         uint64_t q = base + tid;
         if (base < n) {
             lane_frame A[T], B[T];
 #pragma unroll
-            for (int u = 0; u < T; ++u) lane_desc_nb(A[u], q + 256u * u, n, pkts, off, len, unit_log2);
+            for (int u = 0; u < T; ++u) lane_desc_nb(A[u], q + TO * u, n, pkts, off, len, unit_log2);
             auto trip = [&](lane_frame (&X)[T], lane_frame (&Y)[T]) {
                 uint4 v[T][4];
                 bool c[T];
                 if constexpr (PIPE == 24) { // the next trip's descriptors first
 #pragma unroll
                     for (int u = 0; u < T; ++u)
-                        lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                        lane_desc_nb(Y[u], q + strideT + TO * u, n, pkts, off, len, unit_log2);
                 }
 #pragma unroll
                 for (int u = 0; u < T; ++u) c[u] = lane_issue(X[u], pkts, lane, v[u]);
                 if constexpr (PIPE != 24) {
 #pragma unroll
                     for (int u = 0; u < T; ++u)
-                        lane_desc_nb(Y[u], q + strideT + 256u * u, n, pkts, off, len, unit_log2);
+                        lane_desc_nb(Y[u], q + strideT + TO * u, n, pkts, off, len, unit_log2);
                 }
                 if constexpr (PIPE == 23) { // every tile's verdict first, the stores at the end
                     uint4 vd[T];
@@ -3222,6 +3224,7 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
     {1, 4, 1, 23, launch_lane_udpc<23, 0, true, false>, 2}, // 19, both tiles' stores at the trip's end
     {1, 4, 1, 24, launch_lane_udpc<24, 0, true, false>, 2}, // 19, next descriptors before the frames
+    {1, 4, 1, 25, launch_lane_udpc<25, 0, true, false>, 2}, // 19, the trip's tiles a grid stride apart
     {1, 4, 1, 21, launch_lane_udpc<21, 0, true, false>, 2}, // three tiles per trip
     {1, 4, 1, 22, launch_lane_udpc<22, 0, true, false>, 2}, // four
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},

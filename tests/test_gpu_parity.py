@@ -237,7 +237,7 @@ def test_group_write_batched(ctx, torch_dev, variant, n, v8):
 
 @pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 12), (1, 4, 1, 14), (1, 4, 1, 16),
                                                           (1, 4, 1, 18), (1, 4, 1, 19), (1, 4, 1, 21), (1, 4, 1, 22),
-                                                          (1, 4, 1, 23), (1, 4, 1, 24)]))
+                                                          (1, 4, 1, 23), (1, 4, 1, 24), (1, 4, 1, 25)]))
 @pytest.mark.parametrize("n", [1, 63, 300, 70001])
 def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     """the LDS-staged lane kernels on 64-B slotted bursts (the coalesced head
