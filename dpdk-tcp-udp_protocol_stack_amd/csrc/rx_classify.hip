@@ -4,8 +4,8 @@
 // (bottom of this file); every shape is correct for any layout and length:
 //   lane kernel   (rx_classify_lane_kernel)   one frame per lane: 64-B frames
 //                 (heads staged through LDS by coalesced 1-KiB wave loads,
-//                 two tiles' bytes in flight per trip, descriptors one trip
-//                 ahead, UDP table and port window in LDS);
+//                 two tiles' bytes (a grid stride apart) issued per trip,
+//                 descriptors one trip ahead, UDP table and port window in LDS);
 //   group kernel  (rx_classify_kernel)        G lanes per frame: 1500-B frames
 //                 (described below);
 //   stream kernel (rx_classify_stream_kernel) heads per thread, tails streamed
@@ -3176,10 +3176,13 @@ static const variant_entry k_variants[] = {
     // 14 (the 64-B default): 12 software-pipelined (descriptors two trips,
     // frame bytes one trip ahead)
     {1, 4, 1, 14, launch_lane_udpc<14, 0, true, false>, 2},
-    // 19 (the 64-B default from round 6): two adjacent 256-frame tiles per
-    // trip, both tiles' frame bytes issued at the top of the trip,
-    // descriptors one trip ahead (the byte-pattern ceiling's shape)
+    // 19: two adjacent 256-frame tiles per trip, both tiles' frame bytes
+    // issued at the top of the trip, descriptors one trip ahead (the
+    // byte-pattern ceiling's shape); 25 (the 64-B default from round 6): the
+    // same with the trip's two tiles a grid stride apart, 0.2242-0.2248 vs
+    // 0.2263-0.2268 ms per step for 19 (profiles/r06az)
     {1, 4, 1, 19, launch_lane_udpc<19, 0, true, false>, 2},
+    {1, 4, 1, 25, launch_lane_udpc<25, 0, true, false>, 2},
     // 16 (the 64-B default for 8-B verdicts): 14 with lane_verdict_fast, 18%
     // fewer vector and half the scalar instructions; with 16-B verdicts the
     // same time as 14 (the stores bound it: profiles/r06ab, r06ac), with
@@ -3224,7 +3227,6 @@ static const variant_entry k_variants[] = {
     {1, 4, 1, 18, launch_lane_udpc<18, 0, true, false>, 2},
     {1, 4, 1, 23, launch_lane_udpc<23, 0, true, false>, 2}, // 19, both tiles' stores at the trip's end
     {1, 4, 1, 24, launch_lane_udpc<24, 0, true, false>, 2}, // 19, next descriptors before the frames
-    {1, 4, 1, 25, launch_lane_udpc<25, 0, true, false>, 2}, // 19, the trip's tiles a grid stride apart
     {1, 4, 1, 21, launch_lane_udpc<21, 0, true, false>, 2}, // three tiles per trip
     {1, 4, 1, 22, launch_lane_udpc<22, 0, true, false>, 2}, // four
     {8, 2, 2, 1, launch_v<8, 2, 2, 1>},
@@ -3321,7 +3323,9 @@ void rx_pick_variant(uint32_t len_hint, uint32_t *g, uint32_t *p, uint32_t *fpg,
         // (rxg_classify_dev8) the one-tile pipeline stays ahead, 14 at 77.6-77.7 vs
         // 72.9-73.2 Gpps for 19 (profiles/r06ai), and 14 with the straight-line verdict
         // (16) at 79.0-79.5 vs 76.2-77.4 (profiles/r06ak)
-        *g = 1, *p = 4, *fpg = 1, *pipe = v8 ? 16 : 19;
+        // The trip's two tiles a grid stride apart instead of adjacent (pipe 25): 0.2242-
+        // 0.2248 vs 0.2263-0.2268 ms per step in alternating processes (profiles/r06az)
+        *g = 1, *p = 4, *fpg = 1, *pipe = v8 ? 16 : 25;
     } else if (len_hint <= 600) { // IMIX-like mixes (cfg4): stream kernel with the heads taken
         // out of the block stream and a four-slot first probe window (SH): 1.2704 vs 1.3417 ms
         // for pipe 54 (heads gathered before the stream) on one box, 1.1401 vs 1.1716 on

@@ -50,7 +50,8 @@ HOST_ONLY = -1
 # the product library's classify variants (csrc/rx_classify.hip k_variants):
 # (lanes per frame, passes, frames per group, pipeline); every one gives the
 # reference's verdicts (tests/test_gpu_parity.py runs each)
-KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 19), (1, 4, 1, 16), (1, 4, 1, 0),
+KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 19), (1, 4, 1, 25), (1, 4, 1, 16),
+                   (1, 4, 1, 0),
                    (4, 1, 1, 1), (8, 2, 2, 0), (8, 2, 2, 40), (8, 2, 2, 41), (8, 2, 2, 42), (8, 2, 2, 48),
                    (8, 2, 1, 0), (16, 2, 2, 0),
                    (32, 3, 2, 0), (64, 4, 1, 0),
@@ -59,7 +60,7 @@ KERNEL_VARIANTS = [(1, 4, 1, 12), (1, 4, 1, 5), (1, 4, 1, 14), (1, 4, 1, 19), (1
                    (0, 0, 0, 60), (0, 0, 0, 64), (0, 0, 0, 67)]  # SH kernel
 # compiled only into the RX_DIAG build (librxgpu_diag.so, RXGPU_LIB=...):
 # tuning shapes with correct verdicts ...
-DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (1, 4, 1, 18), (1, 4, 1, 23), (1, 4, 1, 24), (1, 4, 1, 25), (1, 4, 1, 21), (1, 4, 1, 22), (8, 2, 2, 1), (16, 2, 1, 0),
+DIAG_TUNING_VARIANTS = [(1, 4, 1, 13), (1, 4, 1, 18), (1, 4, 1, 23), (1, 4, 1, 24), (1, 4, 1, 21), (1, 4, 1, 22), (8, 2, 2, 1), (16, 2, 1, 0),
                         (8, 2, 2, 43), (8, 2, 2, 44), (8, 2, 2, 45), (8, 2, 2, 46),
                         (8, 2, 2, 47), (8, 2, 2, 49), (8, 2, 2, 50), (8, 2, 2, 51), (8, 2, 2, 52), (8, 2, 2, 53), (8, 2, 2, 54), (8, 2, 2, 55), (8, 2, 2, 56), (0, 0, 0, 54), (0, 0, 0, 66),
                         (0, 0, 0, 68), (0, 0, 0, 75), (0, 0, 0, 65),

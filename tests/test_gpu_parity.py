@@ -267,7 +267,8 @@ def test_lane_staged_slotted_bursts(ctx, torch_dev, variant, n):
     assert np.array_equal(cnt, wcnt), (variant, n)
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 19)]) + [None],
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 19),
+                                                          (1, 4, 1, 25)]) + [None],
                          ids=lambda v: "default" if v is None else "v" + "-".join(map(str, v)))
 @pytest.mark.parametrize("flows", ["udp5000", "mixed"])
 def test_lane_without_lds_table(ctx, torch_dev, variant, flows):
@@ -311,7 +312,8 @@ def _udp_zero_sum_frame(src, sport, dst, dport):
     return f
 
 
-@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19)]))
+@pytest.mark.parametrize("variant", R.compiled_variants([(1, 4, 1, 14), (1, 4, 1, 16), (1, 4, 1, 18), (1, 4, 1, 19),
+                                                          (1, 4, 1, 25)]))
 @pytest.mark.parametrize("others", [True, False], ids=["others", "one_address"])
 @pytest.mark.parametrize("v8", [False, True])
 def test_lane_fast_path_waves(ctx, torch_dev, variant, others, v8):

@@ -243,11 +243,11 @@ def test_tune_tables_flags():
 
 def test_default_variant_per_frame_size():
     """rxg_kernel_variant reports the defaults rx_pick_variant chooses (16-B
-    verdicts): the two-tile lane kernel at <= 64 B (pipe 19, round 6), the SH
+    verdicts): the two-tile lane kernel at <= 64 B (pipe 25, round 6), the SH
     stream kernel for mixed sizes, the write-batched G=8 kernel at 1500 B and
     the jumbo stream kernel; a forced variant is reported as forced"""
     with R.Context(R.HOST_ONLY) as c:
-        want = {64: ("rx_classify_lane_kernel", [1, 4, 1, 19]),
+        want = {64: ("rx_classify_lane_kernel", [1, 4, 1, 25]),
                 354: ("rx_classify_sh_kernel", [0, 0, 0, 67]),
                 1500: ("rx_classify_kernel", [8, 2, 2, 48]),
                 9000: ("rx_classify_stream_kernel", [0, 0, 0, 938])}
